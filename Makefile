@@ -1,0 +1,40 @@
+# Build of the MI355X-native library (gfx950 only), the drivers and the oracle.
+#   make            -> nonlinear-solvers_amd/lib/libnls_amd.so + drivers + oracle
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+PKG      := nonlinear-solvers_amd
+CSRC     := $(PKG)/csrc
+BUILD    := $(PKG)/build
+LIBDIR   := $(PKG)/lib
+BINDIR   := $(PKG)/bin
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall
+LDFLAGS  := -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+LIB      := $(LIBDIR)/libnls_amd.so
+OBJS     := $(BUILD)/nls_kernels.o $(BUILD)/nls_api.o
+
+all: $(LIB) drivers oracle
+
+$(BUILD) $(LIBDIR) $(BINDIR):
+	mkdir -p $@
+
+$(BUILD)/nls_kernels.o: $(CSRC)/nls_kernels.hip $(CSRC)/nls_device.hpp $(CSRC)/nls_kernels.hpp | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/nls_api.o: $(CSRC)/nls_api.cpp $(CSRC)/nls_device.hpp $(CSRC)/nls_kernels.hpp include/nls.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS) | $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) $(OBJS) $(LDFLAGS) -o $@
+
+drivers: $(LIB)
+	@if [ -f $(PKG)/drivers/Makefile ]; then $(MAKE) -C $(PKG)/drivers; fi
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR) $(BINDIR)
+	$(MAKE) -C oracle clean
+
+.PHONY: all drivers oracle clean

@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mcells*steps/s of the Krylov/Lanczos exponential
+time-stepper (BASELINE.json metric), one JSON line on rank 0.
+
+Default workload = BASELINE.json configs[2]: 3D cubic NLSE 512^3, Krylov m=16,
+complex128, dt=1e-3, L=10 (dx = 2L/(n-1), nlse_call.cpp:35).  A "step" is one
+full Strang SS2 step (N(1/2) -> Krylov exp -> N(1/2)).  Inputs are resident in
+HBM before the timed region.  With --gpus N (launched by torch.distributed.run)
+the 512^3 grid is z-slab decomposed over N ranks (strong scaling) with RCCL halo
+exchange + all-reduce of the Lanczos dot products.
+
+roofline: the dominant kernel is k_update<J=m-2> (the Lanczos update pass that
+streams J+1 basis vectors and writes one): algorithmic bytes per launch =
+(J+2) * 16 B * cells, timed with HIP events on the
+solver's own stream over the timed region.
+cpu_baseline: the oracle (single-threaded C++ restatement of the reference's
+Eigen path, oracle/) on a bounded 128^3 sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nonlinear-solvers_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+WORKLOADS = {
+    # name: dim, n, L, m, equation, dt, description (BASELINE.json configs)
+    "nlse3d_512": dict(dim=3, n=512, L=10.0, m=16, eq=0, dt=1e-3,
+                       desc="3D cubic NLSE 512^3, Krylov m=16, fp64 complex"),
+    "nlse2d_4096": dict(dim=2, n=4096, L=10.0, m=16, eq=0, dt=1e-3,
+                        desc="2D cubic NLSE 4096x4096, Krylov m=16, fp64 complex"),
+    "sg2d_8192": dict(dim=2, n=8192, L=3.0, m=10, eq=2, dt=5.0 / 500,
+                      desc="2D sine-Gordon 8192x8192, Gautschi, Krylov m=10, fp64"),
+    "cq3d_1024": dict(dim=3, n=1024, L=10.0, m=16, eq=1, dt=1e-3,
+                      desc="3D cubic-quintic NLSE 1024^3, Krylov m=16, fp64 complex"),
+}
+
+
+def algorithmic_bytes_per_cell_step(m: int, eq: int) -> int:
+    """E(m) = ((m-1)(m+2)/2 + m + 3) * 16 B (NLSE c128);
+    E_SG(m) = ((m-1)(m+2) + 2m + 10) * 8 B (sine-Gordon f64)."""
+    if eq == 2:
+        return ((m - 1) * (m + 2) + 2 * m + 10) * 8
+    return ((m - 1) * (m + 2) // 2 + m + 3) * 16
+
+
+def synthetic_ic(w, z0, nzl, seed=1234):
+    """8 random Gaussian solitons with phases + 1e-3 complex white noise.
+    Noise is drawn per global plane, so the field does not depend on the rank split."""
+    n, L, dim = w["n"], w["L"], w["dim"]
+    rng = np.random.default_rng(seed)
+    cen = rng.uniform(-L / 2, L / 2, (8, 3))
+    kv = rng.uniform(-2, 2, (8, 3))
+    wid = rng.uniform(0.5, 1.5, 8)
+    x = np.linspace(-L, L, n)
+    plane = n * n if dim == 3 else n
+    if w["eq"] == 2:
+        out = np.empty(nzl * plane, dtype=np.float64)
+    else:
+        out = np.empty(nzl * plane, dtype=np.complex128)
+    if dim == 3:
+        # separable Gaussian solitons: exp(-r^2/w^2) exp(i k.x) = prod over axes
+        ax = lambda d: np.stack([np.exp(-((x - cen[s, d]) / wid[s]) ** 2 + 1j * kv[s, d] * x)
+                                 for s in range(8)], axis=1)   # (n, 8)
+        fx, fy, fz = ax(0), ax(1), ax(2)
+        for q in range(nzl):
+            k = z0 + q
+            f = fy @ (fz[k][:, None] * fx.T)     # sum_s fz_s(k) fy_s(y) fx_s(x)
+            nr = np.random.default_rng((seed, k))
+            f += 1e-3 * (nr.standard_normal((n, n)) + 1j * nr.standard_normal((n, n)))
+            out[q * plane:(q + 1) * plane] = f.ravel()
+    else:
+        for q in range(nzl):
+            k = z0 + q
+            y = x[k]
+            nr = np.random.default_rng((seed, k))
+            if w["eq"] == 2:  # sg_driver_dev.cpp:34-36 + noise
+                r = np.sqrt(x * x + y * y)
+                out[q * plane:(q + 1) * plane] = 2.0 * np.arctan(np.exp(3.0 - 5.0 * r)) + \
+                    1e-3 * nr.standard_normal(n)
+            else:
+                f = np.zeros(n, dtype=np.complex128)
+                for s in range(8):
+                    r2 = ((x - cen[s, 0]) ** 2 + (y - cen[s, 1]) ** 2) / wid[s] ** 2
+                    f += np.exp(-r2 + 1j * (kv[s, 0] * x + kv[s, 1] * y))
+                f += 1e-3 * (nr.standard_normal(n) + 1j * nr.standard_normal(n))
+                out[q * plane:(q + 1) * plane] = f
+    return out
+
+
+def cpu_baseline(args):
+    """Oracle (single-threaded restatement of nlse_driver.cpp -> NLSESolver::step ->
+    expm_multiply) on a bounded sample of the workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+
+    w = dict(WORKLOADS[args.workload])
+    if w["eq"] == 2:
+        ns, steps = 256, 3
+        w["n"] = ns
+        dx = 2 * w["L"] / (ns - 1)
+        u = synthetic_ic(w, 0, ns)
+        g = oracle_py.grid(2, ns, ns, 1, dx, dx)
+        up = u.copy()
+        mf = -np.ones_like(u)
+        t0 = time.perf_counter()
+        oracle_py.sg_steps(g, u, up, mf, w["dt"], steps, w["m"])
+        el = time.perf_counter() - t0
+        cells = ns * ns
+        sample = f"2D sine-Gordon {ns}^2 m={w['m']}, {steps} Gautschi steps (sub-grid of the workload)"
+    else:
+        ns = 128 if w["dim"] == 3 else 1024
+        steps = args.cpu_steps
+        w["n"] = ns
+        dx = 2 * w["L"] / (ns - 1)
+        u = synthetic_ic(w, 0, ns)
+        g = oracle_py.grid(w["dim"], ns, ns, ns, dx, dx)
+        oracle_py.nlse_steps(g, u, w["dt"], 1, w["m"], nonlin=w["eq"])  # warm caches
+        t0 = time.perf_counter()
+        oracle_py.nlse_steps(g, u, w["dt"], steps, w["m"], nonlin=w["eq"])
+        el = time.perf_counter() - t0
+        cells = ns ** w["dim"]
+        sample = (f"{w['dim']}D {'cubic' if w['eq'] == 0 else 'cubic-quintic'} NLSE {ns}^{w['dim']} "
+                  f"m={w['m']}, {steps} SS2 steps (sub-grid of the workload, oracle/ C++ -O2, 1 thread)")
+    return {"value": cells * steps / el / 1e6, "unit": "Mcells*steps/s", "cores": 1,
+            "kind": "port", "sample": sample, "seconds": el}
+
+
+def load_traffic(workload, m):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary
+    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950 read-side x2 correction)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("m") != m:
+            return None
+        return d.get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="nlse3d_512", choices=sorted(WORKLOADS))
+    ap.add_argument("--n", type=int, default=None, help="override grid side (testing only)")
+    ap.add_argument("--m", type=int, default=None, help="override Krylov dim (testing only)")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        dist.init_process_group("gloo")
+
+    import nls_amd
+
+    w = dict(WORKLOADS[args.workload])
+    if args.n:
+        w["n"] = args.n
+    if args.m:
+        w["m"] = args.m
+    n, dim, m = w["n"], w["dim"], w["m"]
+    dx = 2 * w["L"] / (n - 1)
+    rid = None
+    if world > 1:
+        obj = [nls_amd.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        rid = obj[0]
+    s = nls_amd.Solver(dim, n, n, n if dim == 3 else 1, dx, dx, equation=w["eq"], m=m,
+                       device=local_rank, nranks=world, rank=rank, rccl_id=rid)
+    u = synthetic_ic(w, s.z0, s.nzl)
+    if w["eq"] == 2:
+        s.set_sg_state(u, u.copy(), -np.ones(u.size))
+    else:
+        dv = dx ** dim
+        mass = float(np.sum(np.abs(u) ** 2) * dv)
+        if dist is not None:
+            import torch
+            t = torch.tensor([mass], dtype=torch.float64)
+            dist.all_reduce(t)
+            mass = float(t.item())
+        u /= np.sqrt(mass)  # nlse_call.cpp:41-49
+        s.set_field(u)
+    del u
+    dt = w["dt"]
+    if args.warmup:
+        s.step(dt, args.warmup)
+    s.sync()
+    s.reset_timing()
+    s.set_timing(True)
+    if dist is not None:
+        dist.barrier()
+    s.sync()
+    t0 = time.perf_counter()
+    s.step(dt, args.steps)
+    s.sync()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    tm = s.timing()
+    s.set_timing(False)
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    cells_total = n ** dim
+    value = cells_total * args.steps / el / 1e6
+    n_local = s.n_local
+
+    # dominant kernel: k_update<J = m-2>
+    J = max(m - 2, 0)
+    cnt = tm["update_count"][J]
+    avg_ms = tm["update_ms"][J] / cnt if cnt else float("nan")
+    esz = 8 if w["eq"] == 2 else 16
+    bytes_launch = (J + 2) * esz * n_local
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if cnt else None
+    traffic = load_traffic(args.workload, m) if world == 1 else None
+    step_bytes = algorithmic_bytes_per_cell_step(m, w["eq"]) * n_local
+    step_ms = el * 1e3 / args.steps
+    result = {
+        "metric": "Mcells*steps/s and achieved HBM GB/s, 3D NLSE 512^3 at 1/2/4/8 MI355X"
+        if args.workload == "nlse3d_512" else f"Mcells*steps/s ({w['desc']})",
+        "value": value,
+        "unit": "Mcells*steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": step_ms,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64" if w["eq"] == 2 else "c128 (fp64 complex)",
+        "data": "synthetic (8 random Gaussian solitons + 1e-3 complex white noise, seeded)",
+        "config": {"workload": w["desc"], "grid": [n] * dim, "krylov_m": m, "dt": dt,
+                   "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi"][w["eq"]],
+                   "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": f"k_update<J={J}> (stencil + CGS + write, {J + 1} reads + 1 write)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": traffic,
+            "bytes_per_launch": bytes_launch,
+            "avg_launch_ms": avg_ms,
+        },
+        "step_roofline": {
+            "algorithmic_bytes_per_cell_step": algorithmic_bytes_per_cell_step(m, w["eq"]),
+            "achieved_GBs": step_bytes / (step_ms * 1e-3) / 1e9,
+            "frac": step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "gpu_kernel_ms_per_step": {k: v / max(tm["steps"], 1) for k, v in tm["class_ms"].items()},
+        },
+    }
+    s.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

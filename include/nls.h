@@ -1,0 +1,151 @@
+/*
+ * nls.h -- C-ABI of libnls_amd.so, the MI355X-native (gfx950) Krylov/Lanczos
+ * exponential time-stepper for the 2D/3D NLSE and the 2D sine-Gordon
+ * Gautschi integrator of konradha/nonlinear-solvers.
+ *
+ * Plain C types only: no HIP, torch or Eigen types cross this boundary.
+ * Every entry point returns an int status (NLS_OK == 0, negative on error)
+ * and never throws; nls_last_error() gives the message.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   nls_create       <- NLSESolverDevice(L, host_u0, Parameters)          device/nlse_solver_dev.hpp:53-84
+ *                       NLSECubicQuinticSolver(L, host_u0, Parameters)    device/nlse_cq_solver.hpp:55-86
+ *                       SGESolverDevice(row_ptr, col_ind, values, c, m, n, nnz, u0, v0, u_past, params)
+ *                                                                          device/sg_solver_dev.hpp:104-149
+ *                       build_laplacian_noflux{,_3d}(nx-2, ...)            laplacians.hpp:10-105
+ *                       (the operator is described by grid parameters, not by a CSR matrix)
+ *   nls_set_field    <- cudaMemcpy H2D of host_u0 in the ctors above       device/nlse_solver_dev.hpp:63-64
+ *   nls_set_sg_state <- SGESolverDevice ctor u0/u_past/m uploads           device/sg_solver_dev.hpp:118-135
+ *   nls_step         <- NLSESolverDevice::step(tau=1j*dt, i)               device/nlse_solver_dev.hpp:94-111
+ *                       SGESolverDevice::step(tau=dt, i)                   device/sg_solver_dev.hpp:168-193
+ *   nls_get_field    <- transfer_snapshots(dst) / store_snapshot D2D+D2H   device/nlse_solver_dev.hpp:113-124
+ *   nls_get_sg_velocity <- transfer_snapshots(dst, 'v')                    device/sg_solver_dev.hpp:195-222
+ *   nls_krylov_apply <- MatrixFunctionApplicator{Complex,Real}::apply(out, in, t[, type])
+ *                                                                          device/matfunc_complex.hpp:155-177
+ *                                                                          device/matfunc_real.hpp:171-233
+ *   nls_laplacian_apply <- DeviceSpMV<T>::multiply(x, y)                   device/spmv.hpp:65-73
+ *   nls_destroy      <- ~NLSESolverDevice / ~SGESolverDevice (cudaFree)
+ *
+ * Threading: handles are independent (no globals besides the create-error
+ * string); one handle must not be used from two threads at once -- the same
+ * contract as one NLSESolverDevice per OpenMP thread in
+ * device/nlse_driver_omp.cpp:103-121.  Each handle owns its HIP stream(s),
+ * device buffers and (multi-GPU) RCCL communicator.
+ *
+ * Data layout (host side): complex fields are interleaved (re, im) doubles in
+ * C order, 2D [ny][nx], 3D [nz][ny][nx] -- the .npy layout of the reference
+ * drivers.  With nranks > 1 each rank passes/receives its slab of planes
+ * (3D: z-planes, 2D: y-rows), see nls_local_planes().
+ */
+#ifndef NLS_AMD_H
+#define NLS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NLS_ABI_VERSION 1
+#define NLS_MAX_KRYLOV 32
+
+enum nls_status {
+  NLS_OK = 0,
+  NLS_ERR_ARG = -1,     /* invalid argument / config */
+  NLS_ERR_SHAPE = -2,   /* buffer length does not match the grid */
+  NLS_ERR_OOM = -3,     /* device allocation failed */
+  NLS_ERR_HIP = -4,     /* HIP runtime error (launch or async fault) */
+  NLS_ERR_RCCL = -5,    /* RCCL error */
+  NLS_ERR_STATE = -6    /* call not valid in this state (e.g. no field set) */
+};
+
+enum nls_equation {
+  NLS_NLSE_CUBIC = 0,   /* i u_t + Lap u + |u|^2 u = 0, SS2 (nlse_solver.hpp:53-77) */
+  NLS_NLSE_CQ = 1,      /* rho = s1|u|^2 + s2|u|^4 (device/nlse_cq_solver.hpp:16-39) */
+  NLS_SG_GAUTSCHI = 2   /* u_tt = Lap u + m sin u, Gautschi (sg_solver.hpp:53-74) */
+};
+
+/* Krylov matrix functions f, applied as f(L) u (nls_krylov_apply) */
+enum nls_func {
+  NLS_F_EXP_ABS = 0,    /* exp(t*|lambda|)          eigen_krylov_complex.hpp:71-77 */
+  NLS_F_EXP = 1,        /* exp(t*lambda)  (G2)      nlsolvers/host/include/eigen_krylov_complex.hpp:67-72 */
+  NLS_F_COS_SQRT = 2,   /* cos(t*sqrt|lambda|)      eigen_krylov_real.hpp:53-85 */
+  NLS_F_SINC_SQRT = 3,  /* sinc(t*sqrt|lambda|)     eigen_krylov_real.hpp:87-105 */
+  NLS_F_SINC2_SQRT = 4, /* sinc^2(t*sqrt|lambda|)   eigen_krylov_real.hpp:107-141 */
+  NLS_F_ID_SQRT = 5,    /* t*sqrt|lambda|           eigen_krylov_real.hpp:143-170 */
+  NLS_F_SINC2_HALF = 6  /* sinc^2(t/2*sqrt|lambda|) eigen_krylov_real.hpp:172-201 */
+};
+
+typedef struct nls_config {
+  int32_t dim;          /* 2 or 3 */
+  int32_t equation;     /* enum nls_equation */
+  uint32_t nx, ny, nz;  /* full grid incl. boundary layer (nz ignored for dim 2) */
+  double dx, dy;        /* operator scale: 2D 1/(dx*dy), 3D 1/(dx*dx) (laplacians.hpp:49,102) */
+  uint32_t krylov_m;    /* Krylov dimension, 1..NLS_MAX_KRYLOV (reference default 10) */
+  double sigma1[2];     /* CQ only: complex sigma_1 (reference default 0 + 0.5i) */
+  double sigma2[2];     /* CQ only: complex sigma_2 (reference default -0.5 + 0i) */
+  int32_t device;       /* HIP device ordinal, -1 = current device */
+  int32_t nranks;       /* slab decomposition over ranks (1 = single GPU) */
+  int32_t rank;         /* this rank, 0..nranks-1 */
+  const void *rccl_id;  /* 128-byte RCCL unique id (nls_rccl_unique_id on rank 0), NULL if nranks == 1 */
+} nls_config;
+
+typedef struct nls_handle nls_handle;
+
+/* Fill cfg with the reference defaults (m=10, CQ sigmas 0.5i / -0.5, 1 rank). */
+void nls_config_default(nls_config *cfg);
+int nls_abi_version(void);
+
+int nls_create(const nls_config *cfg, nls_handle **out);
+int nls_destroy(nls_handle *h);
+const char *nls_last_error(const nls_handle *h); /* h == NULL: last nls_create error */
+
+/* Slab owned by this rank: planes [*z0, *z0 + *nzl) of the slowest dimension
+ * (3D: z, 2D: y); n_local = nzl * plane size. */
+int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t *n_local);
+
+/* NLSE: u (complex interleaved, 2*n_local doubles).  SG: u (n_local doubles). */
+int nls_set_field(nls_handle *h, const double *u, uint64_t n_local);
+/* SG only: u, u_past = u0 - dt*v0 (sg_driver_dev.cpp:64,106) and the m(x) field. */
+int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past,
+                     const double *mfield, uint64_t n_local);
+
+/* Enqueue nsteps time steps (NLSE: tau = 1j*dt; SG: tau = dt) on the handle's
+ * stream and return.  Errors of asynchronous execution surface at nls_sync /
+ * nls_get_field. */
+int nls_step(nls_handle *h, double dt, uint32_t nsteps);
+int nls_sync(nls_handle *h);
+
+int nls_get_field(nls_handle *h, double *u, uint64_t n_local);
+int nls_get_sg_velocity(nls_handle *h, double dt, double *v, uint64_t n_local);
+
+/* One Krylov matrix-function action out = f(L) in (no time stepping), t complex
+ * (real paths use t_re).  Complex for NLSE handles, real for SG handles. */
+int nls_krylov_apply(nls_handle *h, const double *in, double t_re, double t_im,
+                     int32_t func, double *out, uint64_t n_local);
+/* y = L x (stencil only; complex for NLSE handles, real for SG handles). */
+int nls_laplacian_apply(nls_handle *h, const double *x, double *y, uint64_t n_local);
+
+/* Multi-GPU: 128-byte RCCL unique id, created on rank 0 and broadcast by the caller. */
+int nls_rccl_unique_id(void *out128);
+
+/* Instrumentation: HIP-event timing around every launch on the handle's
+ * stream.  Classes: 0 alpha (stencil + dot), 1 update (stencil + CGS +
+ * write), 2 reduce/eigen, 3 nonlinear/final, 4 halo exchange.  For the
+ * update class the per-j times are also kept (index = j). */
+typedef struct nls_timing {
+  double class_ms[5];
+  uint64_t class_count[5];
+  double update_ms[NLS_MAX_KRYLOV];
+  uint64_t update_count[NLS_MAX_KRYLOV];
+  uint64_t steps;
+} nls_timing;
+int nls_set_timing(nls_handle *h, int32_t enable);
+int nls_get_timing(nls_handle *h, nls_timing *out); /* synchronises */
+int nls_reset_timing(nls_handle *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NLS_AMD_H */

@@ -1,0 +1,694 @@
+// nls_api.cpp -- host side of libnls_amd.so: the C-ABI of include/nls.h.
+//
+// A handle owns one HIP stream, the Krylov bases in HBM, the device-resident
+// Lanczos state and (nranks > 1) an RCCL communicator.  A time step is a
+// fixed sequence of launches on that stream with no host synchronisation
+// (the reference synchronises on every dot product: host-pointer-mode cuBLAS
+// in device/lanczos_complex.hpp:413-500 and a D2H of T per dot in
+// device/lanczos.hpp:126-194).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "nls.h"
+#include "nls_device.hpp"
+#include "nls_kernels.hpp"
+
+using namespace nls;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct Basis {
+  void *W = nullptr;      // m vectors x vs elements (ghost plane, nzl planes, ghost plane)
+  KState *st = nullptr;   // device-resident Lanczos state
+};
+
+struct TimingRec {
+  int cls, j;
+  hipEvent_t a, b;
+};
+
+struct Fail {
+  int code;
+};
+
+}  // namespace
+
+struct nls_handle {
+  nls_config cfg{};
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  bool cplx_ = true;
+  size_t esize = 16;
+  Geo geo{};
+  int64_t vs = 0;  // elements per stored vector (incl. 2 ghost planes)
+  int m = 10;
+  int nbasis = 1;
+  Basis B[2];
+  void *u = nullptr;        // NLSE state u (nloc complex)
+  double *up = nullptr;     // SG u_past
+  double *mf = nullptr;     // SG m(x)
+  void *scratch = nullptr;  // nloc elements
+  cplx *partA = nullptr, *partU = nullptr;
+  int grid_alpha = 1, grid_lap = 1, grid_pw = 1;
+  int grid_update[MMAX] = {};
+  bool field_set = false, w0_ready = false;
+  int nonlin = 0;
+  cplx s1{0.0, 0.5}, s2{-0.5, 0.0};
+  std::string err;
+  // timing
+  bool timing = false;
+  std::vector<TimingRec> recs;
+  std::vector<hipEvent_t> evpool;
+  nls_timing tacc{};
+  // multi-rank
+  ncclComm_t comm = nullptr;
+  int rank = 0, nranks = 1;
+};
+
+namespace {
+
+void hip_check(nls_handle *h, hipError_t e, const char *what) {
+  if (e != hipSuccess) {
+    h->err = std::string(what) + ": " + hipGetErrorString(e);
+    throw Fail{e == hipErrorOutOfMemory ? NLS_ERR_OOM : NLS_ERR_HIP};
+  }
+}
+
+void rccl_check(nls_handle *h, ncclResult_t e, const char *what) {
+  if (e != ncclSuccess) {
+    h->err = std::string(what) + ": " + ncclGetErrorString(e);
+    throw Fail{NLS_ERR_RCCL};
+  }
+}
+
+template <class F> int guarded(nls_handle *h, F &&f) {
+  if (!h) return NLS_ERR_ARG;
+  try {
+    hip_check(h, hipSetDevice(h->dev), "hipSetDevice");
+    f();
+    return NLS_OK;
+  } catch (const Fail &e) {
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    h->err = "host allocation failed";
+    return NLS_ERR_OOM;
+  } catch (...) {
+    h->err = "unknown error";
+    return NLS_ERR_HIP;
+  }
+}
+
+void fail(nls_handle *h, int code, const std::string &msg) {
+  h->err = msg;
+  throw Fail{code};
+}
+
+char *vec_ptr(nls_handle *h, int b, int k) {  // local plane 0 of vector k of basis b
+  return static_cast<char *>(h->B[b].W) + ((int64_t)k * h->vs + h->geo.P) * (int64_t)h->esize;
+}
+
+hipEvent_t get_event(nls_handle *h) {
+  if (!h->evpool.empty()) {
+    hipEvent_t e = h->evpool.back();
+    h->evpool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hip_check(h, hipEventCreate(&e), "hipEventCreate");
+  return e;
+}
+
+void harvest_timing(nls_handle *h) {
+  if (h->recs.empty()) return;
+  hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  for (auto &r : h->recs) {
+    float ms = 0.f;
+    hip_check(h, hipEventElapsedTime(&ms, r.a, r.b), "hipEventElapsedTime");
+    h->tacc.class_ms[r.cls] += ms;
+    h->tacc.class_count[r.cls] += 1;
+    if (r.cls == 1 && r.j >= 0 && r.j < NLS_MAX_KRYLOV) {
+      h->tacc.update_ms[r.j] += ms;
+      h->tacc.update_count[r.j] += 1;
+    }
+    h->evpool.push_back(r.a);
+    h->evpool.push_back(r.b);
+  }
+  h->recs.clear();
+}
+
+void launch(nls_handle *h, int cls, int j, const void *fn, int grid, void **args) {
+  if (!fn) fail(h, NLS_ERR_ARG, "kernel variant not instantiated");
+  TimingRec rec{cls, j, nullptr, nullptr};
+  if (h->timing) {
+    if (h->recs.size() >= 4096) harvest_timing(h);
+    rec.a = get_event(h);
+    rec.b = get_event(h);
+    hip_check(h, hipEventRecord(rec.a, h->stream), "hipEventRecord");
+  }
+  hip_check(h, hipLaunchKernel(fn, dim3(grid), dim3(NTHREADS), args, 0, h->stream),
+            "hipLaunchKernel");
+  if (h->timing) {
+    hip_check(h, hipEventRecord(rec.b, h->stream), "hipEventRecord");
+    h->recs.push_back(rec);
+  }
+}
+
+// ---- multi-rank plumbing ---------------------------------------------------
+
+// Exchange the boundary planes of vector k of basis b into the neighbours'
+// ghost planes (z-slab decomposition; one plane covers the 3D y-wrap too).
+void halo(nls_handle *h, int b, int k) {
+  if (h->nranks == 1) return;
+  const int64_t P = h->geo.P;
+  const size_t cnt = (size_t)P * (h->cplx_ ? 2 : 1);
+  char *v = vec_ptr(h, b, k);
+  const int64_t es = (int64_t)h->esize;
+  char *first = v, *last = v + (h->geo.nzl - 1) * P * es;
+  char *gbelow = v - P * es, *gabove = v + h->geo.nzl * P * es;
+  TimingRec rec{4, -1, nullptr, nullptr};
+  if (h->timing) {
+    rec.a = get_event(h);
+    rec.b = get_event(h);
+    hip_check(h, hipEventRecord(rec.a, h->stream), "hipEventRecord");
+  }
+  rccl_check(h, ncclGroupStart(), "ncclGroupStart");
+  if (h->rank > 0) {
+    rccl_check(h, ncclSend(first, cnt, ncclDouble, h->rank - 1, h->comm, h->stream), "ncclSend");
+    rccl_check(h, ncclRecv(gbelow, cnt, ncclDouble, h->rank - 1, h->comm, h->stream), "ncclRecv");
+  }
+  if (h->rank < h->nranks - 1) {
+    rccl_check(h, ncclSend(last, cnt, ncclDouble, h->rank + 1, h->comm, h->stream), "ncclSend");
+    rccl_check(h, ncclRecv(gabove, cnt, ncclDouble, h->rank + 1, h->comm, h->stream), "ncclRecv");
+  }
+  rccl_check(h, ncclGroupEnd(), "ncclGroupEnd");
+  if (h->timing) {
+    hip_check(h, hipEventRecord(rec.b, h->stream), "hipEventRecord");
+    h->recs.push_back(rec);
+  }
+}
+
+void allreduce_sums(nls_handle *h, int b, int ncplx) {
+  void *p = &h->B[b].st->sums[0];
+  rccl_check(h, ncclAllReduce(p, p, (size_t)ncplx * 2, ncclDouble, ncclSum, h->comm, h->stream),
+             "ncclAllReduce");
+}
+
+// ---- one Krylov basis: Lanczos + eigensolve + final coefficients ----------
+
+void reduce_iter(nls_handle *h, int b, int j) {
+  KState *st = h->B[b].st;
+  int nbA = h->grid_alpha, nbU = j >= 1 ? h->grid_update[j - 1] : 0;
+  const void *fn = kernel_reduce_iter();
+  if (h->nranks == 1) {
+    int ds = 1, dc = 1;
+    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc};
+    launch(h, 2, j, fn, 1, args);
+  } else {
+    int ds = 1, dc = 0;
+    void *a1[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc};
+    launch(h, 2, j, fn, 1, a1);
+    allreduce_sums(h, b, 2 + (j >= 1 ? j + 1 : 0));
+    ds = 0;
+    dc = 1;
+    void *a2[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc};
+    launch(h, 2, j, fn, 1, a2);
+  }
+}
+
+void reduce_final(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
+  KState *st = h->B[b].st;
+  int m = h->m, nbU = m >= 2 ? h->grid_update[m - 2] : 0;
+  const void *fn = kernel_reduce_final();
+  if (h->nranks == 1) {
+    int ds = 1, dc = 1;
+    void *args[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti};
+    launch(h, 2, m, fn, 1, args);
+  } else {
+    int ds = 1, dc = 0;
+    void *a1[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti};
+    launch(h, 2, m, fn, 1, a1);
+    if (m >= 2) allreduce_sums(h, b, m);
+    ds = 0;
+    dc = 1;
+    void *a2[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti};
+    launch(h, 2, m, fn, 1, a2);
+  }
+}
+
+// Precondition: vector 0 of basis b holds the start vector and its halo.
+void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
+  const int m = h->m;
+  Geo g = h->geo;
+  const void *fa = kernel_alpha(h->cplx_, (int)h->cfg.dim);
+  {
+    void *v0 = vec_ptr(h, b, 0);
+    void *args[] = {&v0, &g, &h->partA};
+    launch(h, 0, 0, fa, h->grid_alpha, args);
+  }
+  reduce_iter(h, b, 0);
+  void *W = vec_ptr(h, b, 0);
+  int64_t vs = h->vs;
+  KState *st = h->B[b].st;
+  for (int j = 0; j + 1 < m; ++j) {
+    if (j >= 1) {
+      void *vj = vec_ptr(h, b, j);
+      void *args[] = {&vj, &g, &h->partA};
+      launch(h, 0, j, fa, h->grid_alpha, args);
+      reduce_iter(h, b, j);
+    }
+    void *args[] = {&W, &vs, &g, &st, &h->partU};
+    launch(h, 1, j, kernel_update(h->cplx_, (int)h->cfg.dim, j), h->grid_update[j], args);
+    if (j + 1 <= m - 2) halo(h, b, j + 1);
+  }
+  reduce_final(h, b, nf, f0, f1, tr, ti);
+}
+
+int occupancy_grid(nls_handle *h, const void *fn, int64_t work_items) {
+  int per_cu = 0;
+  hip_check(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHREADS, 0),
+            "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+  int ncu = 0;
+  hip_check(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev),
+            "hipDeviceGetAttribute");
+  int64_t grid = (int64_t)std::max(per_cu, 1) * std::max(ncu, 1);
+  grid = std::min<int64_t>(grid, std::max<int64_t>(work_items, 1));
+  return (int)grid;
+}
+
+void setup_geometry(nls_handle *h) {
+  const nls_config &c = h->cfg;
+  Geo &g = h->geo;
+  if (c.dim == 3) {
+    g.nx = c.nx;
+    g.nyp = c.ny;
+    g.npl = c.nz;
+  } else {
+    g.nx = c.nx;
+    g.nyp = 1;
+    g.npl = c.ny;
+  }
+  g.P = g.nx * g.nyp;
+  g.Ng = g.P * g.npl;
+  const int64_t base = g.npl / h->nranks, rem = g.npl % h->nranks;
+  g.nzl = base + (h->rank < rem ? 1 : 0);
+  g.z0 = (int64_t)h->rank * base + std::min<int64_t>(h->rank, rem);
+  g.nloc = g.nzl * g.P;
+  // laplacians.hpp:49 (2D 1/(dx*dy)) and :102 (3D 1/(dx*dx)); values -4/-3, -6/-5 times scale
+  g.s = c.dim == 2 ? 1.0 / (c.dx * c.dy) : 1.0 / (c.dx * c.dx);
+  g.sd_in = (c.dim == 2 ? -4.0 : -6.0) * g.s;
+  g.sd_bd = (c.dim == 2 ? -3.0 : -5.0) * g.s;
+  const int BX = c.dim == 3 ? 64 : 256, BY = c.dim == 3 ? 4 : 1;
+  g.ntx = (int32_t)((g.nx + BX - 1) / BX);
+  g.nty = (int32_t)((g.nyp + BY - 1) / BY);
+  int kz = 32;
+  auto tiles = [&](int k) { return (int64_t)g.ntx * g.nty * ((g.nzl + k - 1) / k); };
+  while (kz > 4 && tiles(kz) < 4096) kz /= 2;
+  g.kz = kz;
+  g.ntz = (int32_t)((g.nzl + kz - 1) / kz);
+  g.ntiles = (int64_t)g.ntx * g.nty * g.ntz;
+  h->vs = (g.nzl + 2) * g.P;
+}
+
+void alloc_all(nls_handle *h) {
+  const Geo &g = h->geo;
+  for (int b = 0; b < h->nbasis; ++b) {
+    const size_t bytes = (size_t)h->m * h->vs * h->esize;
+    hip_check(h, hipMalloc(&h->B[b].W, bytes), "hipMalloc(basis)");
+    hip_check(h, hipMemsetAsync(h->B[b].W, 0, bytes, h->stream), "hipMemset");
+    hip_check(h, hipMalloc(&h->B[b].st, sizeof(KState)), "hipMalloc(state)");
+    hip_check(h, hipMemsetAsync(h->B[b].st, 0, sizeof(KState), h->stream), "hipMemset");
+  }
+  const size_t nbytes = (size_t)g.nloc * h->esize;
+  if (h->cplx_) {
+    hip_check(h, hipMalloc(&h->u, nbytes), "hipMalloc(u)");
+  } else {
+    hip_check(h, hipMalloc(&h->up, nbytes), "hipMalloc(u_past)");
+    hip_check(h, hipMalloc(&h->mf, nbytes), "hipMalloc(m)");
+  }
+  hip_check(h, hipMalloc(&h->scratch, nbytes), "hipMalloc(scratch)");
+  // grid sizes from measured occupancy; partial buffers sized for the largest
+  const bool c = h->cplx_;
+  const int dim = h->cfg.dim;
+  h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim), g.ntiles);
+  h->grid_lap = occupancy_grid(h, kernel_lap(c, dim), g.ntiles);
+  int64_t cap = 2 * (int64_t)h->grid_alpha;
+  for (int j = 0; j + 1 < h->m; ++j) {
+    h->grid_update[j] = occupancy_grid(h, kernel_update(c, dim, j), g.ntiles);
+    cap = std::max<int64_t>(cap, (int64_t)h->grid_update[j] * (j + 2));
+  }
+  hip_check(h, hipMalloc(&h->partA, 2 * (size_t)h->grid_alpha * sizeof(cplx)), "hipMalloc(partA)");
+  hip_check(h, hipMalloc(&h->partU, (size_t)cap * sizeof(cplx)), "hipMalloc(partU)");
+  h->grid_pw = (int)std::max<int64_t>(1, std::min<int64_t>((g.nloc + NTHREADS - 1) / NTHREADS, 8192));
+}
+
+void free_all(nls_handle *h) {
+  for (int b = 0; b < 2; ++b) {
+    if (h->B[b].W) (void)hipFree(h->B[b].W);
+    if (h->B[b].st) (void)hipFree(h->B[b].st);
+    h->B[b] = Basis{};
+  }
+  for (void *p : {h->u, (void *)h->up, (void *)h->mf, h->scratch, (void *)h->partA,
+                  (void *)h->partU})
+    if (p) (void)hipFree(p);
+  h->u = h->scratch = nullptr;
+  h->up = h->mf = nullptr;
+  h->partA = h->partU = nullptr;
+}
+
+void copy_in_vector(nls_handle *h, int b, int k, const double *src) {
+  hip_check(h, hipMemcpyAsync(vec_ptr(h, b, k), src, (size_t)h->geo.nloc * h->esize,
+                              hipMemcpyHostToDevice, h->stream),
+            "hipMemcpy H2D");
+}
+
+void check_len(nls_handle *h, uint64_t n) {
+  if (n != (uint64_t)h->geo.nloc)
+    fail(h, NLS_ERR_SHAPE,
+         "length " + std::to_string(n) + " != local cells " + std::to_string(h->geo.nloc));
+}
+
+void pw_launch(nls_handle *h, int cls, const void *fn, void **args) {
+  launch(h, cls, -1, fn, h->grid_pw, args);
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" {
+
+int nls_abi_version(void) { return NLS_ABI_VERSION; }
+
+void nls_config_default(nls_config *c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->dim = 2;
+  c->equation = NLS_NLSE_CUBIC;
+  c->krylov_m = 10;                // device/nlse_solver_dev.hpp:48
+  c->sigma1[0] = 0.0;              // device/nlse_cq_solver.hpp:19
+  c->sigma1[1] = 0.5;
+  c->sigma2[0] = -0.5;
+  c->sigma2[1] = 0.0;
+  c->device = -1;
+  c->nranks = 1;
+  c->rank = 0;
+  c->rccl_id = nullptr;
+}
+
+int nls_create(const nls_config *cfg, nls_handle **out) {
+  if (!out) return NLS_ERR_ARG;
+  *out = nullptr;
+  if (!cfg) {
+    g_create_error = "cfg is NULL";
+    return NLS_ERR_ARG;
+  }
+  const nls_config &c = *cfg;
+  std::string why;
+  if (c.dim != 2 && c.dim != 3) why = "dim must be 2 or 3";
+  else if (c.equation < 0 || c.equation > 2) why = "unknown equation";
+  else if (c.equation == NLS_SG_GAUTSCHI && c.dim != 2 && c.dim != 3) why = "bad dim";
+  else if (c.nx < 2 || c.ny < 2 || (c.dim == 3 && c.nz < 2)) why = "grid too small (need >= 2 per dimension)";
+  else if (!(c.dx > 0.0) || !(c.dy > 0.0)) why = "dx, dy must be > 0";
+  else if (c.krylov_m < 1 || c.krylov_m > NLS_MAX_KRYLOV) why = "krylov_m must be in 1..32";
+  else if (c.nranks < 1 || c.rank < 0 || c.rank >= c.nranks) why = "bad rank/nranks";
+  else if (c.nranks > 1 && !c.rccl_id) why = "nranks > 1 needs rccl_id";
+  else if ((uint32_t)c.nranks > (c.dim == 3 ? c.nz : c.ny)) why = "more ranks than planes";
+  if (!why.empty()) {
+    g_create_error = why;
+    return NLS_ERR_ARG;
+  }
+  nls_handle *h = new (std::nothrow) nls_handle();
+  if (!h) {
+    g_create_error = "host allocation failed";
+    return NLS_ERR_OOM;
+  }
+  h->cfg = c;
+  h->cplx_ = c.equation != NLS_SG_GAUTSCHI;
+  h->esize = h->cplx_ ? 16 : 8;
+  h->m = (int)c.krylov_m;
+  h->nbasis = h->cplx_ ? 1 : 2;
+  h->nonlin = c.equation == NLS_NLSE_CQ ? 1 : 0;
+  h->s1 = {c.sigma1[0], c.sigma1[1]};
+  h->s2 = {c.sigma2[0], c.sigma2[1]};
+  h->rank = c.rank;
+  h->nranks = c.nranks;
+  if (c.device >= 0) {
+    h->dev = c.device;
+  } else if (hipGetDevice(&h->dev) != hipSuccess) {
+    g_create_error = "no HIP device";
+    delete h;
+    return NLS_ERR_HIP;
+  }
+  int rc = guarded(h, [&] {
+    hip_check(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+    setup_geometry(h);
+    alloc_all(h);
+    if (h->nranks > 1) {
+      ncclUniqueId id;
+      std::memcpy(&id, c.rccl_id, sizeof(id));
+      rccl_check(h, ncclCommInitRank(&h->comm, h->nranks, id, h->rank), "ncclCommInitRank");
+    }
+    hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+  if (rc != NLS_OK) {
+    g_create_error = h->err;
+    free_all(h);
+    if (h->comm) ncclCommDestroy(h->comm);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return NLS_OK;
+}
+
+int nls_destroy(nls_handle *h) {
+  if (!h) return NLS_ERR_ARG;
+  (void)hipSetDevice(h->dev);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto &r : h->recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto e : h->evpool) (void)hipEventDestroy(e);
+  free_all(h);
+  if (h->comm) ncclCommDestroy(h->comm);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return NLS_OK;
+}
+
+const char *nls_last_error(const nls_handle *h) {
+  return h ? h->err.c_str() : g_create_error.c_str();
+}
+
+int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t *n_local) {
+  if (!h) return NLS_ERR_ARG;
+  if (z0) *z0 = (uint32_t)h->geo.z0;
+  if (nzl) *nzl = (uint32_t)h->geo.nzl;
+  if (n_local) *n_local = (uint64_t)h->geo.nloc;
+  return NLS_OK;
+}
+
+int nls_set_field(nls_handle *h, const double *u, uint64_t n) {
+  return guarded(h, [&] {
+    if (!u) fail(h, NLS_ERR_ARG, "u is NULL");
+    check_len(h, n);
+    if (h->cplx_) {
+      hip_check(h, hipMemcpyAsync(h->u, u, (size_t)n * h->esize, hipMemcpyHostToDevice, h->stream),
+                "hipMemcpy H2D");
+      h->w0_ready = false;
+    } else {
+      copy_in_vector(h, 0, 0, u);
+      halo(h, 0, 0);
+    }
+    h->field_set = true;
+    hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+}
+
+int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past, const double *mfield,
+                     uint64_t n) {
+  return guarded(h, [&] {
+    if (h->cplx_) fail(h, NLS_ERR_STATE, "nls_set_sg_state on an NLSE handle");
+    if (!u || !u_past || !mfield) fail(h, NLS_ERR_ARG, "NULL input");
+    check_len(h, n);
+    copy_in_vector(h, 0, 0, u);
+    const size_t bytes = (size_t)n * sizeof(double);
+    hip_check(h, hipMemcpyAsync(h->up, u_past, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    hip_check(h, hipMemcpyAsync(h->mf, mfield, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    halo(h, 0, 0);
+    h->field_set = true;
+    hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+}
+
+int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
+  return guarded(h, [&] {
+    if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
+    if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");
+    const int m = h->m;
+    const int64_t n = h->geo.nloc;
+    int64_t vs = h->vs;
+    for (uint32_t s = 0; s < nsteps; ++s) {
+      if (h->cplx_) {
+        // NLSESolverDevice::step (device/nlse_solver_dev.hpp:94-111), tau = 1j*dt:
+        //   N(1/2) -> exp(L*dt) via exp(t|lambda|), t = -tau -> N(1/2)
+        if (!h->w0_ready) {
+          void *w0 = vec_ptr(h, 0, 0);
+          int nl = h->nonlin;
+          void *args[] = {&h->u, &w0, (void *)&n, &dt, &nl, &h->s1, &h->s2};
+          pw_launch(h, 3, kernel_nl_init(), args);
+          halo(h, 0, 0);
+        }
+        run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt);
+        void *W = vec_ptr(h, 0, 0);
+        KState *st = h->B[0].st;
+        int nl = h->nonlin;
+        void *args[] = {&W, &vs, (void *)&n, &st, &h->u, &dt, &nl, &h->s1, &h->s2};
+        pw_launch(h, 3, kernel_final_nlse(m), args);
+        halo(h, 0, 0);
+        h->w0_ready = true;
+      } else {
+        // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u
+        run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0);
+        {
+          void *W = vec_ptr(h, 0, 0);
+          void *g0 = vec_ptr(h, 1, 0);
+          KState *st = h->B[0].st;
+          void *args[] = {&W, &vs, (void *)&n, &st, &h->mf, &h->up, &g0};
+          pw_launch(h, 3, kernel_sg_mid(m), args);
+          halo(h, 1, 0);
+        }
+        run_lanczos(h, 1, 1, NLS_F_SINC2_HALF, 0, dt, 0.0);
+        {
+          void *W2 = vec_ptr(h, 1, 0);
+          void *u = vec_ptr(h, 0, 0);
+          KState *st = h->B[1].st;
+          void *args[] = {&W2, &vs, (void *)&n, &st, &u, &h->up, &dt};
+          pw_launch(h, 3, kernel_sg_end(m), args);
+          halo(h, 0, 0);
+        }
+      }
+      h->tacc.steps += 1;
+    }
+    hip_check(h, hipGetLastError(), "kernel launch");
+  });
+}
+
+int nls_sync(nls_handle *h) {
+  return guarded(h, [&] { hip_check(h, hipStreamSynchronize(h->stream), "nls_sync"); });
+}
+
+int nls_get_field(nls_handle *h, double *u, uint64_t n) {
+  return guarded(h, [&] {
+    if (!u) fail(h, NLS_ERR_ARG, "u is NULL");
+    check_len(h, n);
+    const void *src = h->cplx_ ? h->u : (const void *)vec_ptr(h, 0, 0);
+    hip_check(h, hipMemcpyAsync(u, src, (size_t)n * h->esize, hipMemcpyDeviceToHost, h->stream),
+              "hipMemcpy D2H");
+    hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+}
+
+int nls_get_sg_velocity(nls_handle *h, double dt, double *v, uint64_t n) {
+  return guarded(h, [&] {
+    if (h->cplx_) fail(h, NLS_ERR_STATE, "velocity of an NLSE handle");
+    if (!v) fail(h, NLS_ERR_ARG, "v is NULL");
+    check_len(h, n);
+    void *u = vec_ptr(h, 0, 0);
+    int64_t nn = (int64_t)n;
+    void *args[] = {&u, &h->up, &h->scratch, &nn, &dt};
+    pw_launch(h, 3, kernel_sg_velocity(), args);
+    hip_check(h, hipMemcpyAsync(v, h->scratch, (size_t)n * 8, hipMemcpyDeviceToHost, h->stream),
+              "hipMemcpy D2H");
+    hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+}
+
+int nls_krylov_apply(nls_handle *h, const double *in, double t_re, double t_im, int32_t func,
+                     double *out, uint64_t n) {
+  return guarded(h, [&] {
+    if (!in || !out) fail(h, NLS_ERR_ARG, "NULL buffer");
+    if (func < 0 || func > 6) fail(h, NLS_ERR_ARG, "unknown func");
+    check_len(h, n);
+    const int b = h->cplx_ ? 0 : 1;  // SG: the scratch basis keeps u intact
+    copy_in_vector(h, b, 0, in);
+    if (h->cplx_) h->w0_ready = false;
+    halo(h, b, 0);
+    run_lanczos(h, b, 1, func, 0, t_re, t_im);
+    void *W = vec_ptr(h, b, 0);
+    int64_t vs = h->vs, nn = (int64_t)n;
+    KState *st = h->B[b].st;
+    void *args[] = {&W, &vs, &nn, &st, &h->scratch};
+    pw_launch(h, 3, kernel_combine(h->cplx_, h->m), args);
+    hip_check(h, hipMemcpyAsync(out, h->scratch, (size_t)n * h->esize, hipMemcpyDeviceToHost,
+                                h->stream),
+              "hipMemcpy D2H");
+    hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+}
+
+int nls_laplacian_apply(nls_handle *h, const double *x, double *y, uint64_t n) {
+  return guarded(h, [&] {
+    if (!x || !y) fail(h, NLS_ERR_ARG, "NULL buffer");
+    check_len(h, n);
+    const int b = h->cplx_ ? 0 : 1;
+    copy_in_vector(h, b, 0, x);
+    if (h->cplx_) h->w0_ready = false;
+    halo(h, b, 0);
+    void *v0 = vec_ptr(h, b, 0);
+    Geo g = h->geo;
+    void *args[] = {&v0, &g, &h->scratch};
+    launch(h, 0, -1, kernel_lap(h->cplx_, (int)h->cfg.dim), h->grid_lap, args);
+    hip_check(h, hipMemcpyAsync(y, h->scratch, (size_t)n * h->esize, hipMemcpyDeviceToHost,
+                                h->stream),
+              "hipMemcpy D2H");
+    hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+}
+
+int nls_rccl_unique_id(void *out128) {
+  if (!out128) return NLS_ERR_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) {
+    g_create_error = "ncclGetUniqueId failed";
+    return NLS_ERR_RCCL;
+  }
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(out128, &id, sizeof(id));
+  return NLS_OK;
+}
+
+int nls_set_timing(nls_handle *h, int32_t enable) {
+  return guarded(h, [&] {
+    if (!enable) harvest_timing(h);
+    h->timing = enable != 0;
+  });
+}
+
+int nls_get_timing(nls_handle *h, nls_timing *out) {
+  return guarded(h, [&] {
+    if (!out) fail(h, NLS_ERR_ARG, "out is NULL");
+    harvest_timing(h);
+    *out = h->tacc;
+  });
+}
+
+int nls_reset_timing(nls_handle *h) {
+  return guarded(h, [&] {
+    harvest_timing(h);
+    h->tacc = nls_timing{};
+  });
+}
+
+}  // extern "C"

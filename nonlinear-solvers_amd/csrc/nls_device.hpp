@@ -1,0 +1,80 @@
+// nls_device.hpp -- device-side types shared by the gfx950 kernels and the
+// host code of libnls_amd.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nls {
+
+constexpr int MMAX = 32;      // == NLS_MAX_KRYLOV
+constexpr int NTHREADS = 256; // every kernel: 4 wave64s per workgroup
+
+struct __align__(16) cplx {
+  double re, im;
+};
+
+// ---- scalar helpers: S is double (sine-Gordon, f64) or cplx (NLSE, c128) ----
+__host__ __device__ inline cplx operator+(cplx a, cplx b) { return {a.re + b.re, a.im + b.im}; }
+__host__ __device__ inline cplx operator-(cplx a, cplx b) { return {a.re - b.re, a.im - b.im}; }
+__host__ __device__ inline cplx operator*(double s, cplx a) { return {s * a.re, s * a.im}; }
+__host__ __device__ inline cplx &operator+=(cplx &a, cplx b) { a.re += b.re; a.im += b.im; return a; }
+__host__ __device__ inline cplx cmul(cplx a, cplx b) {
+  return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+__host__ __device__ inline cplx cconj(cplx a) { return {a.re, -a.im}; }
+
+// conj(a) * b  -- the Lanczos inner product v^H w
+__host__ __device__ inline double cj_mul(double a, double b) { return a * b; }
+__host__ __device__ inline cplx cj_mul(cplx a, cplx b) {
+  return {a.re * b.re + a.im * b.im, a.re * b.im - a.im * b.re};
+}
+__host__ __device__ inline double abs2(double a) { return a * a; }
+__host__ __device__ inline double abs2(cplx a) { return a.re * a.re + a.im * a.im; }
+// coefficient (stored complex, imaginary part 0 on real paths) times element
+__host__ __device__ inline double coef_mul(cplx c, double v) { return c.re * v; }
+__host__ __device__ inline cplx coef_mul(cplx c, cplx v) { return cmul(c, v); }
+__host__ __device__ inline cplx to_c(double v) { return {v, 0.0}; }
+__host__ __device__ inline cplx to_c(cplx v) { return v; }
+template <class S> __host__ __device__ inline S zero();
+template <> __host__ __device__ inline double zero<double>() { return 0.0; }
+template <> __host__ __device__ inline cplx zero<cplx>() { return {0.0, 0.0}; }
+
+// ---- geometry of the (local slab of the) grid --------------------------------
+// Planes are the slowest dimension: 3D z-planes (P = nx*ny), 2D y-rows (P = nx).
+// Every basis vector is stored with one ghost plane below and above its
+// nzl local planes; kernels get a pointer to local plane 0, so the ghost
+// planes sit at -P and nzl*P (multi-GPU halo; zero and never read on 1 GPU).
+struct Geo {
+  int64_t nx;     // x extent
+  int64_t nyp;    // rows per plane (3D: ny, 2D: 1)
+  int64_t P;      // plane size nx*nyp
+  int64_t npl;    // global number of planes (3D: nz, 2D: ny)
+  int64_t z0;     // first global plane of this slab
+  int64_t nzl;    // local planes
+  int64_t Ng;     // global cells npl*P
+  int64_t nloc;   // local cells nzl*P
+  double s;       // off-diagonal value 1/(dx*dy) (2D) or 1/(dx*dx) (3D)
+  double sd_in;   // interior diagonal  -4*s / -6*s
+  double sd_bd;   // boundary diagonal  -3*s / -5*s
+  int32_t ntx, nty, ntz, kz;  // tiling of the stencil kernels
+  int64_t ntiles;
+};
+
+// Device-resident Lanczos state of one Krylov basis (no host round trip in
+// the j-loop; the reference reads every dot back to the host,
+// device/lanczos_complex.hpp:413-500).
+struct KState {
+  double s[MMAX + 1];       // s_k = ||W_k|| (stored vectors are unnormalised)
+  cplx H[MMAX][MMAX];       // H[j][k] = v_k^H L v_j  (k <= j), column j of the Hessenberg
+  cplx G[MMAX][MMAX];       // G[j][k] = v_k^H v_j   (k <= j), Gram
+  double Td[MMAX];          // diag of T (real part of alpha), Td[m-1] = 0
+  double To[MMAX];          // sub-diagonal of T: To[j] = T(j+1, j) = s_{j+1}
+  cplx coef[MMAX + 2];      // coefficients of the next update kernel
+  cplx fin[2][MMAX];        // final combination coefficients, one row per f
+  cplx sums[2 * MMAX + 8];  // reduced sums (written by the sum phase)
+  double lam[MMAX];         // Ritz values of the last eigensolve
+  int32_t breakdown;        // first j with s_j == 0 (+1), 0 if none
+  int32_t pad[3];
+};
+
+}  // namespace nls

@@ -1,0 +1,41 @@
+// nls_kernels.hpp -- host-visible handles of the kernels in nls_kernels.hip.
+// Launched with hipLaunchKernel(fn, grid, block, args, 0, stream).
+#pragma once
+#include "nls_device.hpp"
+
+namespace nls {
+
+// stencil kernels (tiled march), argument lists:
+//   update : (S* W, int64_t vs, Geo g, const KState* st, cplx* part)
+//   alpha  : (const S* V, Geo g, cplx* part)
+//   lap    : (const S* V, Geo g, S* out)
+const void *kernel_update(bool complex_, int dim, int J);
+const void *kernel_alpha(bool complex_, int dim);
+const void *kernel_lap(bool complex_, int dim);
+
+// single workgroup:
+//   reduce_iter  : (KState*, const cplx* partA, int nbA, const cplx* partU, int nbU, int j,
+//                   int do_sum, int do_coef)
+//   reduce_final : (KState*, const cplx* partU, int nbU, int m, int do_sum, int do_coef,
+//                   int nf, int f0, int f1, double t_re, double t_im)
+const void *kernel_reduce_iter();
+const void *kernel_reduce_final();
+
+// pointwise (grid-stride):
+//   nl_init   : (const cplx* u, cplx* w0, int64_t n, double dt, int nonlin, cplx s1, cplx s2)
+//   final_nlse: (cplx* W, int64_t vs, int64_t n, const KState*, cplx* u, double dt, int nonlin,
+//                cplx s1, cplx s2)
+//   combine   : (const S* W, int64_t vs, int64_t n, const KState*, S* out)
+//   sg_mid    : (const double* W, int64_t vs, int64_t n, const KState*, const double* mf,
+//                double* up, double* g0)
+//   sg_end    : (const double* W2, int64_t vs, int64_t n, const KState*, double* u, double* up,
+//                double dt)
+//   sg_velocity: (const double* u, const double* up, double* v, int64_t n, double dt)
+const void *kernel_nl_init();
+const void *kernel_final_nlse(int M);
+const void *kernel_combine(bool complex_, int M);
+const void *kernel_sg_mid(int M);
+const void *kernel_sg_end(int M);
+const void *kernel_sg_velocity();
+
+}  // namespace nls

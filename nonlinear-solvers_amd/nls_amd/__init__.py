@@ -1,0 +1,244 @@
+"""nls_amd -- Python binding of libnls_amd.so (the MI355X-native C-ABI, include/nls.h).
+
+Mirrors the reference's in-process solver API (device/nlse_solver_dev.hpp,
+device/sg_solver_dev.hpp, device/matfunc_{complex,real}.hpp) on top of the
+C-ABI with ctypes.  There is no CPU fallback: if the HIP library is missing or
+cannot be loaded this module raises at import of the library, and every
+compute call goes to the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = [
+    "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
+    "F_SINC2_SQRT", "F_ID_SQRT", "F_SINC2_HALF", "MAX_KRYLOV", "NlsError", "Config", "Solver",
+    "lib", "lib_path", "rccl_unique_id", "EXPORTED_SYMBOLS",
+]
+
+NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI = 0, 1, 2
+F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF = range(7)
+MAX_KRYLOV = 32
+
+EXPORTED_SYMBOLS = (
+    "nls_abi_version", "nls_config_default", "nls_create", "nls_destroy", "nls_last_error",
+    "nls_local_planes", "nls_set_field", "nls_set_sg_state", "nls_step", "nls_sync",
+    "nls_get_field", "nls_get_sg_velocity", "nls_krylov_apply", "nls_laplacian_apply",
+    "nls_rccl_unique_id", "nls_set_timing", "nls_get_timing", "nls_reset_timing",
+)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+
+
+def lib_path() -> str:
+    return os.environ.get("NLS_AMD_LIB", os.path.join(_PKG, "lib", "libnls_amd.so"))
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("dim", C.c_int32), ("equation", C.c_int32),
+        ("nx", C.c_uint32), ("ny", C.c_uint32), ("nz", C.c_uint32),
+        ("dx", C.c_double), ("dy", C.c_double),
+        ("krylov_m", C.c_uint32),
+        ("sigma1", C.c_double * 2), ("sigma2", C.c_double * 2),
+        ("device", C.c_int32), ("nranks", C.c_int32), ("rank", C.c_int32),
+        ("rccl_id", C.c_void_p),
+    ]
+
+
+class Timing(C.Structure):
+    _fields_ = [
+        ("class_ms", C.c_double * 5), ("class_count", C.c_uint64 * 5),
+        ("update_ms", C.c_double * MAX_KRYLOV), ("update_count", C.c_uint64 * MAX_KRYLOV),
+        ("steps", C.c_uint64),
+    ]
+
+
+class NlsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"nls error {code}: {msg}")
+        self.code = code
+
+
+_LIB = None
+
+
+def lib():
+    """Load libnls_amd.so (raises if it is absent -- no fallback path exists)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built: run `make` (or __graft_entry__.build())")
+    L = C.CDLL(path)
+    H = C.c_void_p
+    dp = C.POINTER(C.c_double)
+    L.nls_abi_version.restype = C.c_int
+    L.nls_config_default.argtypes = [C.POINTER(Config)]
+    L.nls_config_default.restype = None
+    L.nls_create.argtypes = [C.POINTER(Config), C.POINTER(H)]
+    L.nls_destroy.argtypes = [H]
+    L.nls_last_error.argtypes = [H]
+    L.nls_last_error.restype = C.c_char_p
+    L.nls_local_planes.argtypes = [H, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                   C.POINTER(C.c_uint64)]
+    L.nls_set_field.argtypes = [H, dp, C.c_uint64]
+    L.nls_set_sg_state.argtypes = [H, dp, dp, dp, C.c_uint64]
+    L.nls_step.argtypes = [H, C.c_double, C.c_uint32]
+    L.nls_sync.argtypes = [H]
+    L.nls_get_field.argtypes = [H, dp, C.c_uint64]
+    L.nls_get_sg_velocity.argtypes = [H, C.c_double, dp, C.c_uint64]
+    L.nls_krylov_apply.argtypes = [H, dp, C.c_double, C.c_double, C.c_int32, dp, C.c_uint64]
+    L.nls_laplacian_apply.argtypes = [H, dp, dp, C.c_uint64]
+    L.nls_rccl_unique_id.argtypes = [C.c_void_p]
+    L.nls_set_timing.argtypes = [H, C.c_int32]
+    L.nls_get_timing.argtypes = [H, C.POINTER(Timing)]
+    L.nls_reset_timing.argtypes = [H]
+    if L.nls_abi_version() != 1:
+        raise RuntimeError("libnls_amd ABI mismatch")
+    _LIB = L
+    return L
+
+
+def rccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    rc = lib().nls_rccl_unique_id(buf)
+    if rc != 0:
+        raise NlsError(rc, lib().nls_last_error(None).decode())
+    return buf.raw
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Solver:
+    """One device handle (nls_handle).
+
+    equation: NLSE_CUBIC / NLSE_CQ (complex128 fields) or SG_GAUTSCHI (float64).
+    Grid: dim 2 -> (ny, nx), dim 3 -> (nz, ny, nx); dx, dy as the reference
+    drivers compute them (dx = 2 Lx / (nx - 1)).
+    """
+
+    def __init__(self, dim, nx, ny, nz=1, dx=1.0, dy=None, equation=NLSE_CUBIC, m=10,
+                 sigma1=(0.0, 0.5), sigma2=(-0.5, 0.0), device=-1, nranks=1, rank=0,
+                 rccl_id: bytes | None = None):
+        L = lib()
+        cfg = Config()
+        L.nls_config_default(C.byref(cfg))
+        cfg.dim, cfg.equation = dim, equation
+        cfg.nx, cfg.ny, cfg.nz = nx, ny, nz if dim == 3 else 1
+        cfg.dx = dx
+        cfg.dy = dx if dy is None else dy
+        cfg.krylov_m = m
+        cfg.sigma1[0], cfg.sigma1[1] = sigma1
+        cfg.sigma2[0], cfg.sigma2[1] = sigma2
+        cfg.device, cfg.nranks, cfg.rank = device, nranks, rank
+        self._id = C.create_string_buffer(rccl_id, 128) if rccl_id else None
+        cfg.rccl_id = C.cast(self._id, C.c_void_p) if self._id is not None else None
+        self.cfg = cfg
+        self.complex = equation != SG_GAUTSCHI
+        self.dtype = np.complex128 if self.complex else np.float64
+        h = C.c_void_p()
+        rc = L.nls_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise NlsError(rc, L.nls_last_error(None).decode())
+        self._h = h
+        z0, nzl, nloc = C.c_uint32(), C.c_uint32(), C.c_uint64()
+        self._call(L.nls_local_planes, C.byref(z0), C.byref(nzl), C.byref(nloc))
+        self.z0, self.nzl, self.n_local = z0.value, nzl.value, nloc.value
+
+    # -- plumbing ---------------------------------------------------------
+    def _call(self, fn, *args):
+        rc = fn(self._h, *args)
+        if rc != 0:
+            raise NlsError(rc, lib().nls_last_error(self._h).decode())
+        return rc
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nls_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _in(self, a, dtype=None):
+        a = np.ascontiguousarray(np.asarray(a, dtype=dtype or self.dtype)).ravel()
+        if a.size != self.n_local:
+            raise NlsError(-2, f"expected {self.n_local} cells, got {a.size}")
+        return a.view(np.float64) if np.iscomplexobj(a) else a
+
+    def _out(self, dtype=None):
+        return np.empty(self.n_local, dtype=dtype or self.dtype)
+
+    # -- reference API mirror ----------------------------------------------
+    def set_field(self, u):
+        a = self._in(u)
+        self._call(lib().nls_set_field, _dptr(a), self.n_local)
+
+    def set_sg_state(self, u, u_past, mfield):
+        a, b, c = self._in(u, np.float64), self._in(u_past, np.float64), self._in(mfield, np.float64)
+        self._call(lib().nls_set_sg_state, _dptr(a), _dptr(b), _dptr(c), self.n_local)
+
+    def step(self, dt, nsteps=1):
+        self._call(lib().nls_step, float(dt), int(nsteps))
+
+    def sync(self):
+        self._call(lib().nls_sync)
+
+    def get_field(self):
+        out = self._out()
+        self._call(lib().nls_get_field, _dptr(out.view(np.float64)), self.n_local)
+        return out
+
+    def get_sg_velocity(self, dt):
+        out = self._out(np.float64)
+        self._call(lib().nls_get_sg_velocity, float(dt), _dptr(out), self.n_local)
+        return out
+
+    def krylov_apply(self, x, t, func):
+        a = self._in(x)
+        out = self._out()
+        t = complex(t)
+        self._call(lib().nls_krylov_apply, _dptr(a), t.real, t.imag, int(func),
+                   _dptr(out.view(np.float64)), self.n_local)
+        return out
+
+    def laplacian(self, x):
+        a = self._in(x)
+        out = self._out()
+        self._call(lib().nls_laplacian_apply, _dptr(a), _dptr(out.view(np.float64)), self.n_local)
+        return out
+
+    def set_timing(self, on=True):
+        self._call(lib().nls_set_timing, 1 if on else 0)
+
+    def reset_timing(self):
+        self._call(lib().nls_reset_timing)
+
+    def timing(self) -> dict:
+        t = Timing()
+        self._call(lib().nls_get_timing, C.byref(t))
+        names = ["alpha", "update", "reduce", "pointwise", "halo"]
+        return {
+            "class_ms": {n: t.class_ms[i] for i, n in enumerate(names)},
+            "class_count": {n: int(t.class_count[i]) for i, n in enumerate(names)},
+            "update_ms": [t.update_ms[j] for j in range(MAX_KRYLOV)],
+            "update_count": [int(t.update_count[j]) for j in range(MAX_KRYLOV)],
+            "steps": int(t.steps),
+        }

@@ -1,0 +1,404 @@
+// nls_oracle.cpp -- TEST INFRASTRUCTURE ONLY.  See nls_oracle.h for scope.
+//
+// CPU restatement of the reference G1 Eigen path, written from the reference
+// source read as text (never compiled: Eigen3 and the libnpy submodule are
+// absent from this image, see DESIGN.md "Oracle").  Every function cites the
+// reference lines it follows.  Compiled with -ffp-contract=off so that, like
+// the reference's x86-64 Eigen build (no FMA), every product is rounded
+// separately.
+#include "nls_oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+using cd = std::complex<double>;
+
+struct Grid {
+  int dim;
+  uint64_t nx, ny, nz, N;
+  double scale;
+};
+
+bool make_grid(const oracle_grid *g, Grid &G) {
+  if (!g || (g->dim != 2 && g->dim != 3) || g->nx < 1 || g->ny < 1) return false;
+  G.dim = g->dim;
+  G.nx = g->nx;
+  G.ny = g->ny;
+  G.nz = g->dim == 3 ? g->nz : 1;
+  if (G.nz < 1) return false;
+  G.N = G.nx * G.ny * G.nz;
+  // laplacians.hpp:49  L *= 1/(dx*dy)   (2D)
+  // laplacians.hpp:102 L *= 1/(dx*dx)   (3D; dy, dz only enter the assert)
+  G.scale = g->dim == 2 ? 1.0 / (g->dx * g->dy) : 1.0 / (g->dx * g->dx);
+  return true;
+}
+
+// Matrix-free restatement of build_laplacian_noflux (laplacians.hpp:10-52)
+// and build_laplacian_noflux_3d (:55-105) applied like Eigen's column-major
+// SpMV: row idx receives its contributions in increasing column order
+// (idx-P, idx-nx, idx-1, idx, idx+1, idx+nx, idx+P), each value pre-scaled.
+//   diag  -4 / -3 (2D, any coordinate on the boundary, :23-30)
+//         -6 / -5 (3D, :69-80)
+//   x     idx+-1 unless the row wraps (:32-37, :82-87)
+//   "y"   idx+-nx whenever inside [0,N)  -> in 3D this couples (i,ny-1,k) with
+//         (i,0,k+1) (:89-92)
+//   z     idx+-nx*ny (:94-97)
+template <class S>
+void lap_apply(const Grid &G, const S *x, S *y) {
+  const uint64_t nx = G.nx, ny = G.ny, nz = G.nz, N = G.N, P = nx * ny;
+  const double s = G.scale;
+  const double d_in = G.dim == 2 ? -4.0 : -6.0;
+  const double d_bd = G.dim == 2 ? -3.0 : -5.0;
+  const double sd_in = d_in * s, sd_bd = d_bd * s;
+  for (uint64_t idx = 0; idx < N; ++idx) {
+    const uint64_t i = idx % nx, j = (idx / nx) % ny, k = idx / P;
+    bool bnd = (i == 0 || i == nx - 1 || j == 0 || j == ny - 1);
+    if (G.dim == 3) bnd = bnd || k == 0 || k == nz - 1;
+    S acc = S(0);
+    if (G.dim == 3 && idx >= P) acc += s * x[idx - P];
+    if (idx >= nx) acc += s * x[idx - nx];
+    if (i > 0) acc += s * x[idx - 1];
+    acc += (bnd ? sd_bd : sd_in) * x[idx];
+    if (i + 1 < nx) acc += s * x[idx + 1];
+    if (idx + nx < N) acc += s * x[idx + nx];
+    if (G.dim == 3 && idx + P < N) acc += s * x[idx + P];
+    y[idx] = acc;
+  }
+}
+
+struct StencilOp {
+  Grid G;
+  uint64_t n() const { return G.N; }
+  template <class S> void apply(const S *x, S *y) const { lap_apply(G, x, y); }
+};
+
+struct CsrOp {
+  uint64_t N;
+  const int64_t *rp, *ci;
+  const double *v;
+  uint64_t n() const { return N; }
+  template <class S> void apply(const S *x, S *y) const {
+    for (uint64_t r = 0; r < N; ++r) {
+      S acc = S(0);
+      for (int64_t q = rp[r]; q < rp[r + 1]; ++q) acc += v[q] * x[ci[q]];
+      y[r] = acc;
+    }
+  }
+};
+
+inline double conj_s(double x) { return x; }
+inline cd conj_s(cd x) { return std::conj(x); }
+inline double abs2_s(double x) { return x * x; }
+inline double abs2_s(cd x) { return x.real() * x.real() + x.imag() * x.imag(); }
+inline double re_s(double x) { return x; }
+inline double re_s(cd x) { return x.real(); }
+
+template <class S> double norm2(const S *x, uint64_t n) {
+  double acc = 0.0;
+  for (uint64_t p = 0; p < n; ++p) acc += abs2_s(x[p]);
+  return std::sqrt(acc);
+}
+
+// <a, b> = a^H b  (Eigen: V.col(i).adjoint() * w, eigen_krylov_complex.hpp:30;
+// for the real path w.dot(V.col(i)) is the same number, eigen_krylov_real.hpp:29)
+template <class S> S dot(const S *a, const S *b, uint64_t n) {
+  S acc = S(0);
+  for (uint64_t p = 0; p < n; ++p) acc += conj_s(a[p]) * b[p];
+  return acc;
+}
+
+// lanczos_L  (eigen_krylov_complex.hpp:10-53, eigen_krylov_real.hpp:5-51)
+// V column-major n x m, T column-major m x m.  Runs m-1 iterations; T(m-1,m-1)
+// is never written and stays 0.  Breakdown (T(j+1,j)==0) divides by zero
+// exactly like the reference (NaN), see eigen_krylov_complex.hpp:47.
+template <class S, class Op>
+void lanczos(const Op &op, const S *u, uint32_t m, std::vector<S> &V,
+             std::vector<S> &T, double &beta) {
+  const uint64_t n = op.n();
+  V.assign(n * m, S(0));
+  T.assign((size_t)m * m, S(0));
+  auto Tm = [&](uint32_t r, uint32_t c) -> S & { return T[(size_t)c * m + r]; };
+  beta = norm2(u, n);
+  for (uint64_t p = 0; p < n; ++p) V[p] = u[p] / beta;
+  std::vector<S> w(n);
+  for (uint32_t j = 0; j + 1 < m; ++j) {
+    const S *vj = &V[(uint64_t)j * n];
+    op.apply(vj, w.data());
+    if (j > 0) {
+      const S b = Tm(j - 1, j);
+      const S *vjm = &V[(uint64_t)(j - 1) * n];
+      for (uint64_t p = 0; p < n; ++p) w[p] -= b * vjm[p];
+    }
+    Tm(j, j) = dot(vj, w.data(), n);
+    {
+      const S a = Tm(j, j);
+      for (uint64_t p = 0; p < n; ++p) w[p] -= a * vj[p];
+    }
+    // full MGS re-orthogonalisation (eigen_krylov_complex.hpp:29-37)
+    for (uint32_t i = 0; i <= j; ++i) {
+      const S *vi = &V[(uint64_t)i * n];
+      const S c = dot(vi, w.data(), n);
+      for (uint64_t p = 0; p < n; ++p) w[p] -= c * vi[p];
+    }
+    const double nb = norm2(w.data(), n);
+    Tm(j + 1, j) = S(nb);
+    Tm(j, j + 1) = S(nb);
+    S *vn = &V[(uint64_t)(j + 1) * n];
+    for (uint64_t p = 0; p < n; ++p) vn[p] = w[p] / nb;
+  }
+}
+
+// Symmetric eigensolver for the real m x m matrix Eigen's SelfAdjointEigenSolver
+// sees: lower triangle of T, real part of the diagonal (Eigen's
+// tridiagonalization reads mat.diagonal().real()).  Cyclic Jacobi: an
+// algorithm independent of the device's implicit-QL, so agreement between
+// the two is a real check.  A (row-major) is overwritten; Q columns = vectors.
+void jacobi_eig(std::vector<double> A, int m, std::vector<double> &lam,
+                std::vector<double> &Q) {
+  Q.assign((size_t)m * m, 0.0);
+  for (int i = 0; i < m; ++i) Q[(size_t)i * m + i] = 1.0;
+  for (int sweep = 0; sweep < 100; ++sweep) {
+    double off = 0.0, tot = 0.0;
+    for (int i = 0; i < m; ++i)
+      for (int j = 0; j < m; ++j) {
+        const double a = A[(size_t)i * m + j] * A[(size_t)i * m + j];
+        tot += a;
+        if (i != j) off += a;
+      }
+    if (off <= 1e-34 * tot || off == 0.0) break;
+    for (int p = 0; p < m - 1; ++p)
+      for (int q = p + 1; q < m; ++q) {
+        const double apq = A[(size_t)p * m + q];
+        if (apq == 0.0) continue;
+        const double app = A[(size_t)p * m + p], aqq = A[(size_t)q * m + q];
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) /
+                         (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < m; ++k) {
+          const double akp = A[(size_t)k * m + p], akq = A[(size_t)k * m + q];
+          A[(size_t)k * m + p] = c * akp - s * akq;
+          A[(size_t)k * m + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < m; ++k) {
+          const double apk = A[(size_t)p * m + k], aqk = A[(size_t)q * m + k];
+          A[(size_t)p * m + k] = c * apk - s * aqk;
+          A[(size_t)q * m + k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < m; ++k) {
+          const double qkp = Q[(size_t)k * m + p], qkq = Q[(size_t)k * m + q];
+          Q[(size_t)k * m + p] = c * qkp - s * qkq;
+          Q[(size_t)k * m + q] = s * qkp + c * qkq;
+        }
+      }
+  }
+  lam.resize(m);
+  for (int i = 0; i < m; ++i) lam[i] = A[(size_t)i * m + i];
+}
+
+inline double sinc_ref(double x) {  // eigen_krylov_real.hpp:95-97
+  return std::fabs(x) < 1e-8 ? 1.0 : std::sin(x) / x;
+}
+
+// f(lambda) for every convention the reference uses.
+cd eval_f(int func, double lam, cd t) {
+  switch (func) {
+    case ORACLE_F_EXP_ABS: return std::exp(t * std::fabs(lam));
+    case ORACLE_F_EXP: return std::exp(t * lam);
+    default: break;
+  }
+  const double x = t.real() * std::sqrt(std::fabs(lam));
+  switch (func) {
+    case ORACLE_F_COS_SQRT: return std::cos(x);
+    case ORACLE_F_SINC_SQRT: return sinc_ref(x);
+    case ORACLE_F_SINC2_SQRT: { const double s = sinc_ref(x); return s * s; }
+    case ORACLE_F_ID_SQRT: return x;
+    case ORACLE_F_SINC2_HALF: {  // eigen_krylov_real.hpp:186-191
+      const double xh = t.real() / 2. * std::sqrt(std::fabs(lam));
+      if (std::fabs(xh) < 1e-8) return 1.0;
+      return (std::sin(xh) / xh) * (std::sin(xh) / xh);
+    }
+    default: return std::nan("");
+  }
+}
+
+inline void assign(double &dst, cd v) { dst = v.real(); }
+inline void assign(cd &dst, cd v) { dst = v; }
+
+// expm_multiply / *_sqrt_multiply: beta * V * Q f(Lambda) Q^H * e1
+// (eigen_krylov_complex.hpp:55-84; eigen_krylov_real.hpp:53-201)
+template <class S, class Op>
+void krylov_apply(const Op &op, const S *u, cd t, uint32_t m, int func, S *out) {
+  const uint64_t n = op.n();
+  std::vector<S> V, T;
+  double beta = 0.0;
+  lanczos(op, u, m, V, T, beta);
+  std::vector<double> A((size_t)m * m, 0.0);
+  for (uint32_t c = 0; c < m; ++c)
+    for (uint32_t r = c; r < m; ++r) {
+      const double v = re_s(T[(size_t)c * m + r]);  // lower triangle
+      A[(size_t)r * m + c] = v;
+      A[(size_t)c * m + r] = v;
+    }
+  std::vector<double> lam, Q;
+  jacobi_eig(A, (int)m, lam, Q);
+  std::vector<cd> coef(m, cd(0));  // (Q f Q^H)[:, 0]
+  for (uint32_t i = 0; i < m; ++i) {
+    cd acc(0);
+    for (uint32_t k = 0; k < m; ++k)
+      acc += Q[(size_t)i * m + k] * eval_f(func, lam[k], t) * Q[(size_t)0 * m + k];
+    coef[i] = acc;
+  }
+  std::vector<S> c(m);
+  for (uint32_t i = 0; i < m; ++i) assign(c[i], coef[i]);
+  for (uint64_t p = 0; p < n; ++p) {
+    S acc = S(0);
+    for (uint32_t k = 0; k < m; ++k) acc += (beta * V[(uint64_t)k * n + p]) * c[k];
+    out[p] = acc;
+  }
+}
+
+const cd *as_c(const double *p) { return reinterpret_cast<const cd *>(p); }
+cd *as_c(double *p) { return reinterpret_cast<cd *>(p); }
+
+// nonlinear half step  out = exp(-0.5*tau*rho(u)) * u,  tau = 1j*dt
+//   cubic (G1 CPU, nlse_solver.hpp:66-69): rho = re^2 + im^2
+//   cubic-quintic (G1 device, device/nlse_cq_solver.hpp:16-39):
+//     d = |u|*|u|, rho = s1*d + s2*d^2 (complex), out = exp(-.5*tau*rho) * u
+void nonlin_half(cd *u, uint64_t n, double dt, int nonlin, const double *sg) {
+  const cd tau(0.0, dt);
+  const cd mt = -.5 * tau;
+  if (nonlin == 0) {
+    for (uint64_t p = 0; p < n; ++p) {
+      const double x = u[p].real() * u[p].real() + u[p].imag() * u[p].imag();
+      u[p] = std::exp(mt * cd(x)) * u[p];
+    }
+  } else {
+    const cd s1(sg[0], sg[1]), s2(sg[2], sg[3]);
+    for (uint64_t p = 0; p < n; ++p) {
+      const double a = std::abs(u[p]);
+      const double d = a * a;
+      const cd rho = s1 * d + s2 * (d * d);
+      u[p] = std::exp(mt * rho) * u[p];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int oracle_laplacian_apply_c(const oracle_grid *g, const double *x, double *y) {
+  Grid G;
+  if (!make_grid(g, G) || !x || !y) return -1;
+  lap_apply(G, as_c(x), as_c(y));
+  return 0;
+}
+
+int oracle_laplacian_apply_r(const oracle_grid *g, const double *x, double *y) {
+  Grid G;
+  if (!make_grid(g, G) || !x || !y) return -1;
+  lap_apply(G, x, y);
+  return 0;
+}
+
+int oracle_lanczos_c(const oracle_grid *g, const double *u, uint32_t m,
+                     double *V, double *T, double *beta) {
+  Grid G;
+  if (!make_grid(g, G) || m < 1) return -1;
+  StencilOp op{G};
+  std::vector<cd> Vv, Tv;
+  lanczos(op, as_c(u), m, Vv, Tv, *beta);
+  std::memcpy(V, Vv.data(), Vv.size() * sizeof(cd));
+  std::memcpy(T, Tv.data(), Tv.size() * sizeof(cd));
+  return 0;
+}
+
+int oracle_krylov_c(const oracle_grid *g, const double *u, double t_re,
+                    double t_im, uint32_t m, int func, double *out) {
+  Grid G;
+  if (!make_grid(g, G) || m < 1) return -1;
+  StencilOp op{G};
+  krylov_apply(op, as_c(u), cd(t_re, t_im), m, func, as_c(out));
+  return 0;
+}
+
+int oracle_krylov_r(const oracle_grid *g, const double *u, double t,
+                    uint32_t m, int func, double *out) {
+  Grid G;
+  if (!make_grid(g, G) || m < 1) return -1;
+  StencilOp op{G};
+  krylov_apply(op, u, cd(t, 0.0), m, func, out);
+  return 0;
+}
+
+int oracle_krylov_csr_c(uint64_t n, const int64_t *rowptr, const int64_t *col,
+                        const double *val, const double *u, double t_re,
+                        double t_im, uint32_t m, int func, double *out) {
+  if (m < 1) return -1;
+  CsrOp op{n, rowptr, col, val};
+  krylov_apply(op, as_c(u), cd(t_re, t_im), m, func, as_c(out));
+  return 0;
+}
+
+int oracle_krylov_csr_r(uint64_t n, const int64_t *rowptr, const int64_t *col,
+                        const double *val, const double *u, double t,
+                        uint32_t m, int func, double *out) {
+  if (m < 1) return -1;
+  CsrOp op{n, rowptr, col, val};
+  krylov_apply(op, u, cd(t, 0.0), m, func, out);
+  return 0;
+}
+
+// NLSESolver::step (nlse_solver.hpp:53-77), tau = 1j*dt, called nsteps times.
+int oracle_nlse_steps(const oracle_grid *g, double *u_, double dt,
+                      uint32_t nsteps, uint32_t m, int nonlin,
+                      const double *sigma) {
+  Grid G;
+  if (!make_grid(g, G) || m < 1 || (nonlin != 0 && nonlin != 1)) return -1;
+  if (nonlin == 1 && !sigma) return -1;
+  StencilOp op{G};
+  const uint64_t n = G.N;
+  cd *u = as_c(u_);
+  std::vector<cd> rho(u, u + n), buf(n);
+  const cd tau(0.0, dt);
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    std::memcpy(rho.data(), u, n * sizeof(cd));
+    nonlin_half(rho.data(), n, dt, nonlin, sigma);
+    krylov_apply(op, rho.data(), -tau, m, ORACLE_F_EXP_ABS, buf.data());
+    nonlin_half(buf.data(), n, dt, nonlin, sigma);
+    std::memcpy(u, buf.data(), n * sizeof(cd));
+  }
+  return 0;
+}
+
+// SGESolver::step (sg_solver.hpp:53-74): Gautschi with the id filter.
+int oracle_sg_steps(const oracle_grid *g, double *u, double *u_past,
+                    const double *mfield, double dt, uint32_t nsteps,
+                    uint32_t m) {
+  Grid G;
+  if (!make_grid(g, G) || m < 1 || !mfield) return -1;
+  StencilOp op{G};
+  const uint64_t n = G.N;
+  std::vector<double> filt(n), gbuf(n), s2(n), cosv(n);
+  const cd t(dt, 0.0);
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    krylov_apply(op, u, t, m, ORACLE_F_ID_SQRT, filt.data());
+    for (uint64_t p = 0; p < n; ++p) gbuf[p] = mfield[p] * (-std::sin(filt[p]));
+    krylov_apply(op, gbuf.data(), t, m, ORACLE_F_SINC2_HALF, s2.data());
+    krylov_apply(op, u, t, m, ORACLE_F_COS_SQRT, cosv.data());
+    for (uint64_t p = 0; p < n; ++p) {
+      const double uc = u[p];
+      u[p] = 2 * cosv[p] - u_past[p] + dt * dt * s2[p];
+      u_past[p] = uc;
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"

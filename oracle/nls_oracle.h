@@ -1,0 +1,81 @@
+/*
+ * nls_oracle.h -- TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * A plain C++17 restatement (no Eigen, no GPU) of the reference's G1 CPU path:
+ *   laplacians.hpp:10-105            (no-flux 2D/3D operators, incl. 3D y-wrap)
+ *   eigen_krylov_complex.hpp:10-84   (MGS Lanczos, T[m-1,m-1]=0, exp(t*|lambda|))
+ *   eigen_krylov_real.hpp:5-201      (real Lanczos, cos/sinc/sinc^2/id of t*sqrt|lambda|)
+ *   nlse_solver.hpp:53-77            (Strang SS2 cubic NLSE step)
+ *   device/nlse_cq_solver.hpp:16-39  (cubic-quintic density, G1 device semantics)
+ *   sg_solver.hpp:53-74              (sine-Gordon Gautschi step)
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library.  The product path (libnls_amd.so) never links it.
+ *
+ * Layout: complex arrays are interleaved doubles (re, im); flat index
+ *   2D: idx = j*nx + i ;  3D: idx = (k*ny + j)*nx + i   (reference: nlse_call.cpp,
+ *   nlse_driver_3d.cpp:12-18).
+ */
+#ifndef NLS_ORACLE_H
+#define NLS_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  int dim;             /* 2 or 3 */
+  uint32_t nx, ny, nz; /* full grid incl. boundary layer; nz ignored for dim 2 */
+  double dx, dy;       /* 2D scale 1/(dx*dy), 3D scale 1/(dx*dx) (laplacians.hpp:49,102) */
+} oracle_grid;
+
+/* Krylov matrix functions (eigen_krylov_real.hpp / eigen_krylov_complex.hpp) */
+enum {
+  ORACLE_F_EXP_ABS = 0,   /* exp(t*|lambda|)           eigen_krylov_complex.hpp:71-77 */
+  ORACLE_F_EXP = 1,       /* exp(t*lambda)  (G2)       nlsolvers/host/include/eigen_krylov_complex.hpp:67-72 */
+  ORACLE_F_COS_SQRT = 2,  /* cos(t*sqrt|lambda|)       eigen_krylov_real.hpp:53-85 */
+  ORACLE_F_SINC_SQRT = 3, /* sinc(t*sqrt|lambda|)      eigen_krylov_real.hpp:87-105 */
+  ORACLE_F_SINC2_SQRT = 4,/* sinc^2(t*sqrt|lambda|)    eigen_krylov_real.hpp:107-141 */
+  ORACLE_F_ID_SQRT = 5,   /* t*sqrt|lambda|            eigen_krylov_real.hpp:143-170 */
+  ORACLE_F_SINC2_HALF = 6 /* sinc^2(t/2*sqrt|lambda|)  eigen_krylov_real.hpp:172-201 */
+};
+
+int oracle_laplacian_apply_c(const oracle_grid *g, const double *x, double *y);
+int oracle_laplacian_apply_r(const oracle_grid *g, const double *x, double *y);
+
+/* V: n*m complex, column-major (V[k*n + p]); T: m*m complex column-major */
+int oracle_lanczos_c(const oracle_grid *g, const double *u, uint32_t m,
+                     double *V, double *T, double *beta);
+
+/* out = f(L) u via m-dim Krylov; t complex for the complex path */
+int oracle_krylov_c(const oracle_grid *g, const double *u, double t_re,
+                    double t_im, uint32_t m, int func, double *out);
+int oracle_krylov_r(const oracle_grid *g, const double *u, double t,
+                    uint32_t m, int func, double *out);
+
+/* Same, for an explicit CSR operator (real values), used by the scipy KAT
+ * (nlsolvers/host/drivers/test_scipy_matfunc.cpp:41-95). */
+int oracle_krylov_csr_c(uint64_t n, const int64_t *rowptr, const int64_t *col,
+                        const double *val, const double *u, double t_re,
+                        double t_im, uint32_t m, int func, double *out);
+int oracle_krylov_csr_r(uint64_t n, const int64_t *rowptr, const int64_t *col,
+                        const double *val, const double *u, double t,
+                        uint32_t m, int func, double *out);
+
+/* NLSE: nsteps Strang SS2 steps with tau = 1j*dt (nlse_solver.hpp:53-77).
+ * nonlin 0 = cubic (G1 CPU), 1 = cubic-quintic (G1 device semantics,
+ * device/nlse_cq_solver.hpp:16-39) with sigma = {s1re, s1im, s2re, s2im}. */
+int oracle_nlse_steps(const oracle_grid *g, double *u, double dt,
+                      uint32_t nsteps, uint32_t m, int nonlin,
+                      const double *sigma);
+
+/* sine-Gordon Gautschi (sg_solver.hpp:53-74); u, u_past updated in place. */
+int oracle_sg_steps(const oracle_grid *g, double *u, double *u_past,
+                    const double *mfield, double dt, uint32_t nsteps,
+                    uint32_t m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

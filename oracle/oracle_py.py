@@ -1,0 +1,118 @@
+"""ctypes binding of liboracle_nls.so -- TEST INFRASTRUCTURE ONLY.
+
+Loaded only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class OracleGrid(C.Structure):
+    _fields_ = [("dim", C.c_int), ("nx", C.c_uint32), ("ny", C.c_uint32), ("nz", C.c_uint32),
+                ("dx", C.c_double), ("dy", C.c_double)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle_nls.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        _LIB = C.CDLL(path)
+        dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+        g = C.POINTER(OracleGrid)
+        L = _LIB
+        L.oracle_laplacian_apply_c.argtypes = [g, dp, dp]
+        L.oracle_laplacian_apply_r.argtypes = [g, dp, dp]
+        L.oracle_lanczos_c.argtypes = [g, dp, C.c_uint32, dp, dp, C.POINTER(C.c_double)]
+        L.oracle_krylov_c.argtypes = [g, dp, C.c_double, C.c_double, C.c_uint32, C.c_int, dp]
+        L.oracle_krylov_r.argtypes = [g, dp, C.c_double, C.c_uint32, C.c_int, dp]
+        ip = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+        L.oracle_krylov_csr_c.argtypes = [C.c_uint64, ip, ip, dp, dp, C.c_double, C.c_double,
+                                          C.c_uint32, C.c_int, dp]
+        L.oracle_krylov_csr_r.argtypes = [C.c_uint64, ip, ip, dp, dp, C.c_double, C.c_uint32,
+                                          C.c_int, dp]
+        L.oracle_nlse_steps.argtypes = [g, dp, C.c_double, C.c_uint32, C.c_uint32, C.c_int,
+                                        C.POINTER(C.c_double)]
+        L.oracle_sg_steps.argtypes = [g, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32]
+    return _LIB
+
+
+def grid(dim, nx, ny, nz, dx, dy):
+    return OracleGrid(dim, nx, ny, nz if dim == 3 else 1, dx, dy)
+
+
+def _c(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.complex128)).view(np.float64).ravel()
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(f"oracle returned {rc}")
+
+
+def laplacian_c(g, x):
+    xi = _c(x)
+    out = np.zeros_like(xi)
+    _check(lib().oracle_laplacian_apply_c(C.byref(g), xi, out))
+    return out.view(np.complex128)
+
+
+def laplacian_r(g, x):
+    xi = np.ascontiguousarray(x, dtype=np.float64).ravel()
+    out = np.zeros_like(xi)
+    _check(lib().oracle_laplacian_apply_r(C.byref(g), xi, out))
+    return out
+
+
+def krylov_c(g, u, t, m, func=0):
+    ui = _c(u)
+    out = np.zeros_like(ui)
+    t = complex(t)
+    _check(lib().oracle_krylov_c(C.byref(g), ui, t.real, t.imag, m, func, out))
+    return out.view(np.complex128)
+
+
+def krylov_r(g, u, t, m, func):
+    ui = np.ascontiguousarray(u, dtype=np.float64).ravel()
+    out = np.zeros_like(ui)
+    _check(lib().oracle_krylov_r(C.byref(g), ui, float(t), m, func, out))
+    return out
+
+
+def krylov_csr(A, u, t, m, func):
+    A = A.tocsr()
+    rp = A.indptr.astype(np.int64)
+    ci = A.indices.astype(np.int64)
+    val = np.ascontiguousarray(A.data, dtype=np.float64)
+    if np.iscomplexobj(u) or isinstance(t, complex):
+        ui = _c(u)
+        out = np.zeros_like(ui)
+        t = complex(t)
+        _check(lib().oracle_krylov_csr_c(A.shape[0], rp, ci, val, ui, t.real, t.imag, m, func, out))
+        return out.view(np.complex128)
+    ui = np.ascontiguousarray(u, dtype=np.float64).ravel()
+    out = np.zeros_like(ui)
+    _check(lib().oracle_krylov_csr_r(A.shape[0], rp, ci, val, ui, float(t), m, func, out))
+    return out
+
+
+def nlse_steps(g, u, dt, nsteps, m, nonlin=0, sigma=(0.0, 0.5, -0.5, 0.0)):
+    ui = _c(u).copy()
+    sg = (C.c_double * 4)(*sigma)
+    _check(lib().oracle_nlse_steps(C.byref(g), ui, dt, nsteps, m, nonlin, sg))
+    return ui.view(np.complex128)
+
+
+def sg_steps(g, u, u_past, mfield, dt, nsteps, m):
+    u = np.ascontiguousarray(u, dtype=np.float64).ravel().copy()
+    up = np.ascontiguousarray(u_past, dtype=np.float64).ravel().copy()
+    mf = np.ascontiguousarray(mfield, dtype=np.float64).ravel()
+    _check(lib().oracle_sg_steps(C.byref(g), u, up, mf, dt, nsteps, m))
+    return u, up
