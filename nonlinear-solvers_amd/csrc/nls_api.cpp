@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -260,13 +261,14 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   int64_t vs = h->vs;
   KState *st = h->B[b].st;
   for (int j = 0; j + 1 < m; ++j) {
+    void *out = vec_ptr(h, b, j + 1);
     if (j >= 1) {
       void *vj = vec_ptr(h, b, j);
       void *args[] = {&vj, &g, &h->partA};
       launch(h, 0, j, fa, h->grid_alpha, args);
       reduce_iter(h, b, j);
     }
-    void *args[] = {&W, &vs, &g, &st, &h->partU};
+    void *args[] = {&W, &out, &vs, &g, &st, &h->partU};
     launch(h, 1, j, kernel_update(h->cplx_, (int)h->cfg.dim, j), h->grid_update[j], args);
     if (j + 1 <= m - 2) halo(h, b, j + 1);
   }
@@ -280,7 +282,9 @@ int occupancy_grid(nls_handle *h, const void *fn, int64_t work_items) {
   int ncu = 0;
   hip_check(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev),
             "hipDeviceGetAttribute");
-  int64_t grid = (int64_t)std::max(per_cu, 1) * std::max(ncu, 1);
+  int mult = 1;
+  if (const char *e = std::getenv("NLS_GRID_MULT")) mult = std::max(1, std::atoi(e));
+  int64_t grid = (int64_t)std::max(per_cu, 1) * std::max(ncu, 1) * mult;
   grid = std::min<int64_t>(grid, std::max<int64_t>(work_items, 1));
   return (int)grid;
 }
@@ -307,16 +311,16 @@ void setup_geometry(nls_handle *h) {
   g.s = c.dim == 2 ? 1.0 / (c.dx * c.dy) : 1.0 / (c.dx * c.dx);
   g.sd_in = (c.dim == 2 ? -4.0 : -6.0) * g.s;
   g.sd_bd = (c.dim == 2 ? -3.0 : -5.0) * g.s;
-  const int BX = c.dim == 3 ? 64 : 256, BY = c.dim == 3 ? 4 : 1;
-  g.ntx = (int32_t)((g.nx + BX - 1) / BX);
-  g.nty = (int32_t)((g.nyp + BY - 1) / BY);
-  int kz = 32;
-  auto tiles = [&](int k) { return (int64_t)g.ntx * g.nty * ((g.nzl + k - 1) / k); };
-  while (kz > 4 && tiles(kz) < 4096) kz /= 2;
-  g.kz = kz;
-  g.ntz = (int32_t)((g.nzl + kz - 1) / kz);
-  g.ntiles = (int64_t)g.ntx * g.nty * g.ntz;
-  h->vs = (g.nzl + 2) * g.P;
+  // tile depth: 3D planes per tile, 2D rows per wave (tile = 4 waves)
+  g.kz = c.dim == 3 ? 32 : 16;
+  if (const char *e = std::getenv("NLS_KZ")) g.kz = std::max(1, std::atoi(e));
+  g.remap = 0;
+  if (const char *e = std::getenv("NLS_TILE_REMAP")) g.remap = std::atoi(e) != 0;
+  // Pad the vector stride so the m streams of one update pass do not start on
+  // the same HBM channel (strides of 2^k * plane bytes camp on one channel).
+  int64_t pad = 256;  // 4 KiB of complex<double>: +15 % on 16-stream passes (tools/bw_probe.hip)
+  if (const char *e = std::getenv("NLS_VEC_PAD")) pad = std::max<int64_t>(0, std::atoll(e));
+  h->vs = (g.nzl + 2) * g.P + pad;
 }
 
 void alloc_all(nls_handle *h) {
@@ -339,11 +343,13 @@ void alloc_all(nls_handle *h) {
   // grid sizes from measured occupancy; partial buffers sized for the largest
   const bool c = h->cplx_;
   const int dim = h->cfg.dim;
-  h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim), g.ntiles);
-  h->grid_lap = occupancy_grid(h, kernel_lap(c, dim), g.ntiles);
+  const int64_t ta = stencil_tiles(g, dim, alpha_rows_per_thread());
+  h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim), ta);
+  h->grid_lap = occupancy_grid(h, kernel_lap(c, dim), ta);
   int64_t cap = 2 * (int64_t)h->grid_alpha;
   for (int j = 0; j + 1 < h->m; ++j) {
-    h->grid_update[j] = occupancy_grid(h, kernel_update(c, dim, j), g.ntiles);
+    h->grid_update[j] = occupancy_grid(h, kernel_update(c, dim, j),
+                                       stencil_tiles(g, dim, update_rows_per_thread(j)));
     cap = std::max<int64_t>(cap, (int64_t)h->grid_update[j] * (j + 2));
   }
   hip_check(h, hipMalloc(&h->partA, 2 * (size_t)h->grid_alpha * sizeof(cplx)), "hipMalloc(partA)");

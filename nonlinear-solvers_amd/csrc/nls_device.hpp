@@ -56,8 +56,8 @@ struct Geo {
   double s;       // off-diagonal value 1/(dx*dy) (2D) or 1/(dx*dx) (3D)
   double sd_in;   // interior diagonal  -4*s / -6*s
   double sd_bd;   // boundary diagonal  -3*s / -5*s
-  int32_t ntx, nty, ntz, kz;  // tiling of the stencil kernels
-  int64_t ntiles;
+  int32_t kz;     // planes (3D) / rows per wave (2D) per tile of the stencil kernels
+  int32_t remap;  // 1: XCD-banded tile order (speed only)
 };
 
 // Device-resident Lanczos state of one Krylov basis (no host round trip in

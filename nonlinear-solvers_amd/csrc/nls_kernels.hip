@@ -30,11 +30,6 @@ template <class S> __device__ __forceinline__ S from_real(double v);
 template <> __device__ __forceinline__ double from_real<double>(double v) { return v; }
 template <> __device__ __forceinline__ cplx from_real<cplx>(double v) { return {v, 0.0}; }
 
-template <int DIM> struct Tile {
-  static constexpr int BX = DIM == 3 ? 64 : 256;
-  static constexpr int BY = DIM == 3 ? 4 : 1;
-};
-
 // ---------------------------------------------------------------------------
 // wave64 + workgroup reduction into one partial per workgroup (fixed order:
 // results are bitwise reproducible run to run)
@@ -44,6 +39,8 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// partials are stored column-major: out[k * gridDim.x + blockIdx.x], so the
+// single-workgroup reduction reads each column with coalesced 1 KiB wave loads.
 template <int NA>
 __device__ __forceinline__ void block_store(cplx (&v)[NA], cplx *__restrict__ out) {
   __shared__ cplx red[NTHREADS / 64][NA];
@@ -62,75 +59,317 @@ __device__ __forceinline__ void block_store(cplx (&v)[NA], cplx *__restrict__ ou
     cplx s = red[0][k];
 #pragma unroll
     for (int q = 1; q < NTHREADS / 64; ++q) s += red[q][k];
-    out[k] = s;
+    out[(int64_t)k * gridDim.x + blockIdx.x] = s;
   }
 }
 
 // ---------------------------------------------------------------------------
-// The stencil march.  fn(p, cur, lap) is called for every local cell p of the
-// workgroup's tiles with cur = V[p] and lap = (L V)[p].
-template <class S, int DIM, class Fn>
+// memory helpers: basis vectors streamed once per pass use non-temporal
+// loads/stores (measured +5-10 % on 16-stream passes, tools/bw_probe.hip);
+// the stencil vector keeps default policy (its neighbours are re-read).
+typedef double v2d __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ cplx ld_nt(const cplx *p) {
+  const v2d v = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p));
+  return {v.x, v.y};
+}
+__device__ __forceinline__ double ld_nt(const double *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_nt(cplx *p, cplx v) {
+  v2d t;
+  t.x = v.re;
+  t.y = v.im;
+  __builtin_nontemporal_store(t, reinterpret_cast<v2d *>(p));
+}
+__device__ __forceinline__ void st_nt(double *p, double v) { __builtin_nontemporal_store(v, p); }
+
+// wave64 cross-lane moves (ds_bpermute)
+__device__ __forceinline__ double shfl_up1(double v) { return __shfl_up(v, 1, 64); }
+__device__ __forceinline__ cplx shfl_up1(cplx v) { return {__shfl_up(v.re, 1, 64), __shfl_up(v.im, 1, 64)}; }
+__device__ __forceinline__ double shfl_dn1(double v) { return __shfl_down(v, 1, 64); }
+__device__ __forceinline__ cplx shfl_dn1(cplx v) { return {__shfl_down(v.re, 1, 64), __shfl_down(v.im, 1, 64)}; }
+__device__ __forceinline__ double bcast(double v, int l) { return __shfl(v, l, 64); }
+__device__ __forceinline__ cplx bcast(cplx v, int l) { return {__shfl(v.re, l, 64), __shfl(v.im, l, 64)}; }
+
+// ---------------------------------------------------------------------------
+// Tiling of the stencil kernels (256 threads = 4 wave64 per workgroup):
+//   3D: tile = 64 x  *  4*RB y-rows  *  kz z-planes; wave w owns RB consecutive
+//       rows, lane = x.  y-neighbours inside the wave's rows come from
+//       registers, x-neighbours from the neighbouring lane (ds_bpermute).
+//   2D: tile = 64*RB x  *  4*kz rows; wave w marches its own kz rows, each lane
+//       owns RB x-positions 64 apart (x-neighbours across the 64-chunk seam
+//       from the neighbouring chunk's lane 0/63).
+// Both march along the slowest dimension with a (prev, cur, next) register
+// queue, so every cell of the stencil vector is fetched from HBM once; only
+// tile-edge neighbours (1 lane of 64, wave-boundary rows) use L1/L2 loads.
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+template <int DIM, int RB> __host__ __device__ inline void tile_counts(const Geo &g, int64_t &ntx,
+                                                                        int64_t &nty, int64_t &ntz) {
+  if (DIM == 3) {
+    ntx = cdiv(g.nx, 64);
+    nty = cdiv(g.nyp, 4 * RB);
+    ntz = cdiv(g.nzl, g.kz);
+  } else {
+    ntx = cdiv(g.nx, 64 * RB);
+    nty = 1;
+    ntz = cdiv(g.nzl, 4 * (int64_t)g.kz);
+  }
+}
+
+// fn(p, cur, lap) for every local cell p of the workgroup's tiles, with
+// cur = V[p] and lap = (L V)[p] (laplacians.hpp:10-105, flat-index form).
+template <class S, int DIM, int RB, class Fn>
 __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn &&fn) {
-  using T = Tile<DIM>;
-  const int tx = threadIdx.x % T::BX, ty = threadIdx.x / T::BX;
-  for (int64_t t = blockIdx.x; t < g.ntiles; t += gridDim.x) {
-    const int64_t it = t % g.ntx;
-    const int64_t rest = t / g.ntx;
-    const int64_t jt = rest % g.nty;
-    const int64_t kt = rest / g.nty;
-    const int64_t x = it * T::BX + tx;
-    const int64_t y = DIM == 3 ? jt * T::BY + ty : 0;
-    if (x >= g.nx || y >= g.nyp) continue;
-    const int64_t q0 = kt * g.kz;
-    const int64_t q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
-    const int64_t r = y * g.nx + x;
-    const bool bxy = (x == 0) || (x == g.nx - 1) || (DIM == 3 && (y == 0 || y == g.nyp - 1));
-    S prev = zero<S>();
-    if (g.z0 + q0 > 0) prev = V[(q0 - 1) * g.P + r];
-    S cur = V[q0 * g.P + r];
-    for (int64_t q = q0; q < q1; ++q) {
-      const int64_t gq = g.z0 + q;
-      const int64_t p = q * g.P + r;
-      const S next = (gq + 1 < g.npl) ? V[p + g.P] : zero<S>();
-      S nb = prev + next;
-      if (x > 0) nb = nb + V[p - 1];
-      if (x + 1 < g.nx) nb = nb + V[p + 1];
-      if constexpr (DIM == 3) {
-        const int64_t pg = gq * g.P + r;
-        if (pg >= g.nx) nb = nb + V[p - g.nx];
-        if (pg + g.nx < g.Ng) nb = nb + V[p + g.nx];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t ntx, nty, ntz;
+  tile_counts<DIM, RB>(g, ntx, nty, ntz);
+  const int64_t tiles = ntx * nty * ntz;
+  const int64_t T8 = tiles / 8;
+  const int64_t P = g.P, nx = g.nx;
+  for (int64_t t0 = blockIdx.x; t0 < tiles; t0 += gridDim.x) {
+    // optional XCD-banded order (workgroups b, b+8 share an XCD): speed only
+    const int64_t t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
+    const int64_t it = t % ntx;
+    const int64_t rest = t / ntx;
+    const int64_t jt = rest % nty;
+    const int64_t kt = rest / nty;
+    if constexpr (DIM == 3) {
+      const int64_t x = it * 64 + lane;
+      const bool xin = x < nx;
+      const int64_t yb = jt * (4 * RB) + (int64_t)w * RB;
+      if (yb >= g.nyp) continue;  // wave-uniform
+      const int64_t q0 = kt * g.kz;
+      const int64_t q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
+      bool rv[RB];
+      int64_t off[RB];
+      S prev[RB], cur[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        rv[r] = yb + r < g.nyp;
+        off[r] = (yb + r) * nx + x;
+        const bool ld = xin && rv[r];
+        prev[r] = (ld && g.z0 + q0 > 0) ? V[(q0 - 1) * P + off[r]] : zero<S>();
+        cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
       }
-      const bool bnd = bxy || gq == 0 || gq == g.npl - 1;
-      const S lap = g.s * nb + (bnd ? g.sd_bd : g.sd_in) * cur;
-      fn(p, cur, lap);
-      prev = cur;
-      cur = next;
+      const bool bx = (x == 0) || (x == nx - 1);
+      for (int64_t q = q0; q < q1; ++q) {
+        const int64_t gq = g.z0 + q;
+        const bool bz = gq == 0 || gq == g.npl - 1;
+        const bool has_next = gq + 1 < g.npl;
+        S next[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          next[r] = (xin && rv[r] && has_next) ? V[(q + 1) * P + off[r]] : zero<S>();
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          if (!rv[r]) continue;  // wave-uniform
+          const int64_t p = q * P + off[r];
+          const int64_t pg = gq * P + off[r];
+          S ym, yp;
+          if (r > 0) ym = cur[r - 1];
+          else ym = (xin && pg >= nx) ? V[p - nx] : zero<S>();
+          if (r + 1 < RB && rv[r + 1 < RB ? r + 1 : r]) yp = cur[r + 1 < RB ? r + 1 : r];
+          else yp = (xin && pg + nx < g.Ng) ? V[p + nx] : zero<S>();
+          S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
+          if (lane == 0) xm = (xin && x > 0) ? V[p - 1] : zero<S>();
+          if (lane == 63) xp = (xin && x + 1 < nx) ? V[p + 1] : zero<S>();
+          if (!(x > 0)) xm = zero<S>();
+          if (!(x + 1 < nx)) xp = zero<S>();
+          const int64_t y = yb + r;
+          const bool bnd = bx || bz || y == 0 || y == g.nyp - 1;
+          const S lap = g.s * (((prev[r] + next[r]) + (xm + xp)) + (ym + yp)) +
+                        (bnd ? g.sd_bd : g.sd_in) * cur[r];
+          if (xin) fn(p, cur[r], lap);
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          prev[r] = cur[r];
+          cur[r] = next[r];
+        }
+      }
+    } else {
+      const int64_t q0 = (kt * 4 + w) * (int64_t)g.kz;
+      if (q0 >= g.nzl) continue;  // wave-uniform
+      const int64_t q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
+      int64_t xr[RB];
+      S prev[RB], cur[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        xr[r] = it * 64 * RB + 64 * r + lane;
+        const bool ld = xr[r] < nx;
+        prev[r] = (ld && g.z0 + q0 > 0) ? V[(q0 - 1) * P + xr[r]] : zero<S>();
+        cur[r] = ld ? V[q0 * P + xr[r]] : zero<S>();
+      }
+      for (int64_t q = q0; q < q1; ++q) {
+        const int64_t gq = g.z0 + q;
+        const bool bz = gq == 0 || gq == g.npl - 1;
+        const bool has_next = gq + 1 < g.npl;
+        S next[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          next[r] = (xr[r] < nx && has_next) ? V[(q + 1) * P + xr[r]] : zero<S>();
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int64_t x = xr[r];
+          const int64_t p = q * P + x;
+          S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
+          const S cm = bcast(cur[r > 0 ? r - 1 : 0], 63);
+          const S cp = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
+          if (lane == 0) xm = r > 0 ? cm : ((x < nx && x > 0) ? V[p - 1] : zero<S>());
+          if (lane == 63) xp = r + 1 < RB ? cp : ((x + 1 < nx) ? V[p + 1] : zero<S>());
+          if (!(x > 0)) xm = zero<S>();
+          if (!(x + 1 < nx)) xp = zero<S>();
+          const bool bnd = x == 0 || x == nx - 1 || bz;
+          const S lap = g.s * ((prev[r] + next[r]) + (xm + xp)) + (bnd ? g.sd_bd : g.sd_in) * cur[r];
+          if (x < nx) fn(p, cur[r], lap);
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          prev[r] = cur[r];
+          cur[r] = next[r];
+        }
+      }
     }
   }
 }
 
+// rows (3D) / x-chunks (2D) per thread: more independent columns per thread
+// for the light kernels, fewer for the register-heavy high-J updates.
+template <int J> struct UpdRB { static constexpr int v = J <= 2 ? 4 : (J <= 6 ? 2 : 1); };
+constexpr int RB_ALPHA = 4;
+
 // y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
 template <class S, int DIM>
 __global__ __launch_bounds__(NTHREADS) void k_lap(const S *__restrict__ V, Geo g, S *__restrict__ out) {
-  march<S, DIM>(V, g, [&](int64_t p, const S &, const S &lap) { out[p] = lap; });
+  march<S, DIM, RB_ALPHA>(V, g, [&](int64_t p, const S &, const S &lap) { out[p] = lap; });
 }
 
-// a = V^H L V and ||V||^2 per workgroup
+// a = V^H L V and ||V||^2 per workgroup, in the symmetric forward-edge form
+//   V^H L V = sum_p d_p |v_p|^2 + 2 s sum_p Re(conj(v_p) (v_{p+1} + v_{p+nx} + v_{p+P}))
+// (each off-diagonal pair of the reference matrix visited once; the matrix is
+// real symmetric, laplacians.hpp:32-37, 89-97, so the form is real).  Only the
+// forward neighbours are needed: x+1 from the next lane, y+1 from the thread's
+// next row, z+1 from the register queue; plane q+2 is prefetched while plane q
+// is reduced.
+template <class S, int DIM, int RB>
+__device__ __forceinline__ void alpha_tiles(const S *__restrict__ V, const Geo &g, double &a, double &n2) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t ntx, nty, ntz;
+  tile_counts<DIM, RB>(g, ntx, nty, ntz);
+  const int64_t tiles = ntx * nty * ntz;
+  const int64_t P = g.P, nx = g.nx;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int64_t it = t % ntx;
+    const int64_t rest = t / ntx;
+    const int64_t jt = rest % nty;
+    const int64_t kt = rest / nty;
+    int64_t q0, q1, yb = 0;
+    int64_t off[RB];
+    bool rv[RB], xin[RB];
+    if constexpr (DIM == 3) {
+      yb = jt * (4 * RB) + (int64_t)w * RB;
+      if (yb >= g.nyp) continue;
+      q0 = kt * g.kz;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        rv[r] = yb + r < g.nyp;
+        off[r] = (yb + r) * nx + it * 64 + lane;
+        xin[r] = it * 64 + lane < nx;
+      }
+    } else {
+      q0 = (kt * 4 + w) * (int64_t)g.kz;
+      if (q0 >= g.nzl) continue;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        rv[r] = true;
+        off[r] = it * 64 * RB + 64 * r + lane;
+        xin[r] = off[r] < nx;
+      }
+    }
+    q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
+    S cur[RB], nxt[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const bool ld = xin[r] && rv[r];
+      cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
+      nxt[r] = (ld && g.z0 + q0 + 1 < g.npl) ? V[(q0 + 1) * P + off[r]] : zero<S>();
+    }
+    for (int64_t q = q0; q < q1; ++q) {
+      const int64_t gq = g.z0 + q;
+      // forward neighbours that live outside this wave's registers
+      S xe[RB], ye = zero<S>();
+#pragma unroll
+      for (int r = 0; r < RB; ++r) xe[r] = shfl_dn1(cur[r]);
+      if constexpr (DIM == 3) {
+        const int rl = RB - 1;
+        // y+1 of the wave's last valid row: flat p + nx (covers the 3D y-wrap)
+        int rlast = 0;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) if (rv[r]) rlast = r;
+        const int64_t p = q * P + off[rlast];
+        const int64_t pg = gq * P + off[rlast];
+        (void)rl;
+        ye = (xin[rlast] && pg + nx < g.Ng) ? V[p + nx] : zero<S>();
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int64_t x = it * 64 + lane;
+          if (lane == 63) xe[r] = (rv[r] && x + 1 < nx) ? V[q * P + off[r] + 1] : zero<S>();
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const S c0 = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
+          if (lane == 63) {
+            if (r + 1 < RB) xe[r] = c0;
+            else xe[r] = (off[r] + 1 < nx) ? V[q * P + off[r] + 1] : zero<S>();
+          }
+        }
+      }
+      // prefetch plane q+2
+      S nn[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        nn[r] = (xin[r] && rv[r] && gq + 2 < g.npl && q + 2 < q1 + 1) ? V[(q + 2) * P + off[r]]
+                                                                        : zero<S>();
+      const bool bz = gq == 0 || gq == g.npl - 1;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        if (!rv[r]) continue;
+        const int64_t x = DIM == 3 ? it * 64 + lane : off[r];
+        if (!xin[r]) continue;
+        const S c = cur[r];
+        S f = (x + 1 < nx) ? xe[r] : zero<S>();
+        if constexpr (DIM == 3) {
+          const bool last = !(r + 1 < RB && rv[r + 1 < RB ? r + 1 : r]);
+          f = f + (last ? ye : cur[r + 1 < RB ? r + 1 : r]);
+        }
+        f = f + nxt[r];
+        const bool bnd = x == 0 || x == nx - 1 || bz ||
+                         (DIM == 3 && (yb + r == 0 || yb + r == g.nyp - 1));
+        const double c2 = abs2(c);
+        n2 += c2;
+        a += (bnd ? g.sd_bd : g.sd_in) * c2 + 2.0 * g.s * to_c(cj_mul(c, f)).re;
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        cur[r] = nxt[r];
+        nxt[r] = nn[r];
+      }
+    }
+  }
+}
+
 template <class S, int DIM>
 __global__ __launch_bounds__(NTHREADS) void k_alpha(const S *__restrict__ V, Geo g, cplx *__restrict__ part) {
-  S a = zero<S>();
-  double n2 = 0.0;
-  march<S, DIM>(V, g, [&](int64_t, const S &cur, const S &lap) {
-    a += cj_mul(cur, lap);
-    n2 += abs2(cur);
-  });
-  cplx v[2] = {to_c(a), {n2, 0.0}};
-  block_store<2>(v, part + (int64_t)blockIdx.x * 2);
+  double a = 0.0, n2 = 0.0;
+  alpha_tiles<S, DIM, RB_ALPHA>(V, g, a, n2);
+  cplx v[2] = {{a, 0.0}, {n2, 0.0}};
+  block_store<2>(v, part);
 }
 
 // W_{J+1} = a * L W_J - sum_{k<=J} b_k W_k ;  partials g_k = W_k^H W_{J+1}, ||W_{J+1}||^2
 template <class S, int DIM, int J>
-__global__ __launch_bounds__(NTHREADS) void k_update(S *__restrict__ W, int64_t vs, Geo g,
+__global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S *__restrict__ out,
+                                                     int64_t vs, Geo g,
                                                      const KState *__restrict__ st,
                                                      cplx *__restrict__ part) {
   constexpr int NA = J + 2;
@@ -142,15 +381,14 @@ __global__ __launch_bounds__(NTHREADS) void k_update(S *__restrict__ W, int64_t 
   for (int k = 0; k <= J; ++k) b[k] = st->coef[k];
   const double a = st->coef[J + 1].re;
   const S *__restrict__ VJ = W + (int64_t)J * vs;
-  S *__restrict__ out = W + (int64_t)(J + 1) * vs;
-  march<S, DIM>(VJ, g, [&](int64_t p, const S &cur, const S &lap) {
+  march<S, DIM, UpdRB<J>::v>(VJ, g, [&](int64_t p, const S &cur, const S &lap) {
     S wk[J > 0 ? J : 1];
 #pragma unroll
-    for (int k = 0; k < J; ++k) wk[k] = W[(int64_t)k * vs + p];
+    for (int k = 0; k < J; ++k) wk[k] = ld_nt(W + (int64_t)k * vs + p);
     S X = a * lap - coef_mul(b[J], cur);
 #pragma unroll
     for (int k = 0; k < J; ++k) X = X - coef_mul(b[k], wk[k]);
-    out[p] = X;
+    st_nt(out + p, X);
 #pragma unroll
     for (int k = 0; k < J; ++k) acc[k] = acc[k] + cj_mul(wk[k], X);
     acc[J] = acc[J] + cj_mul(cur, X);
@@ -159,36 +397,49 @@ __global__ __launch_bounds__(NTHREADS) void k_update(S *__restrict__ W, int64_t 
   cplx v[NA];
 #pragma unroll
   for (int k = 0; k < NA; ++k) v[k] = to_c(acc[k]);
-  block_store<NA>(v, part + (int64_t)blockIdx.x * NA);
+  block_store<NA>(v, part);
 }
+
+// host-side mirror of the tiling, for grid sizes
+int64_t stencil_tiles(const Geo &g, int dim, int rb) {
+  int64_t a, b, c;
+  if (dim == 3) {
+    switch (rb) {
+      case 1: tile_counts<3, 1>(g, a, b, c); break;
+      case 2: tile_counts<3, 2>(g, a, b, c); break;
+      default: tile_counts<3, 4>(g, a, b, c); break;
+    }
+  } else {
+    switch (rb) {
+      case 1: tile_counts<2, 1>(g, a, b, c); break;
+      case 2: tile_counts<2, 2>(g, a, b, c); break;
+      default: tile_counts<2, 4>(g, a, b, c); break;
+    }
+  }
+  return a * b * c;
+}
+int update_rows_per_thread(int J) { return J <= 2 ? 4 : (J <= 6 ? 2 : 1); }
+int alpha_rows_per_thread() { return RB_ALPHA; }
 
 // ---------------------------------------------------------------------------
 // single-workgroup reductions + coefficient math + m x m eigensolve
 
-// Deterministic sum over nb partial rows of width NA, columns [c0, c0+nc) -> dst
-__device__ void sum_partials(const cplx *__restrict__ part, int nb, int NA, int c0, int nc,
-                             cplx *dst) {
-  __shared__ double sre[NTHREADS], sim[NTHREADS];
-  const int t = threadIdx.x;
-  for (int v = c0; v < c0 + nc; ++v) {
-    double a = 0.0, b = 0.0;
-    for (int q = t; q < nb; q += NTHREADS) {
-      const cplx x = part[(int64_t)q * NA + v];
-      a += x.re;
-      b += x.im;
+// Deterministic column sums of column-major partials: dst[v] = sum_q part[v*nb + q],
+// v < nc.  One wave per column, fixed order (bitwise reproducible).
+__device__ void sum_partials(const cplx *__restrict__ part, int nb, int nc, cplx *dst) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int v = w; v < nc; v += NTHREADS / 64) {
+    const cplx *__restrict__ col = part + (int64_t)v * nb;
+    double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
+    int q = lane;
+    for (; q + 64 < nb; q += 128) {
+      const cplx x0 = col[q], x1 = col[q + 64];
+      a0 += x0.re; b0 += x0.im;
+      a1 += x1.re; b1 += x1.im;
     }
-    sre[t] = a;
-    sim[t] = b;
-    __syncthreads();
-    for (int off = NTHREADS / 2; off > 0; off >>= 1) {
-      if (t < off) {
-        sre[t] += sre[t + off];
-        sim[t] += sim[t + off];
-      }
-      __syncthreads();
-    }
-    if (t == 0) dst[v - c0] = {sre[0], sim[0]};
-    __syncthreads();
+    if (q < nb) { const cplx x0 = col[q]; a0 += x0.re; b0 += x0.im; }
+    const double a = wave_sum(a0 + a1), b = wave_sum(b0 + b1);
+    if (lane == 0) dst[v] = {a, b};
   }
 }
 
@@ -205,32 +456,41 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_iter(KState *__restrict__ s
                                                           const cplx *__restrict__ partA, int nbA,
                                                           const cplx *__restrict__ partU, int nbU,
                                                           int j, int do_sum, int do_coef) {
+  __shared__ cplx ssum[2 * MMAX + 8];
+  const int ncols = 2 + (j >= 1 ? j + 1 : 0);
   if (do_sum) {
-    sum_partials(partA, nbA, 2, 0, 2, st->sums);
-    if (j >= 1) sum_partials(partU, nbU, j + 1, 0, j + 1, st->sums + 2);
+    sum_partials(partA, nbA, 2, ssum);
+    if (j >= 1) sum_partials(partU, nbU, j + 1, ssum + 2);
+    __syncthreads();
+    if (!do_coef) {
+      for (int v = threadIdx.x; v < ncols; v += NTHREADS) ssum[v] = ssum[v];
+      return;
+    }
+  } else {
+    for (int v = threadIdx.x; v < ncols; v += NTHREADS) ssum[v] = ssum[v];
     __syncthreads();
   }
   if (!do_coef || threadIdx.x != 0) return;
   double sj;
   if (j == 0) {
-    sj = sqrt(st->sums[1].re);
+    sj = sqrt(ssum[1].re);
     st->s[0] = sj;
     st->G[0][0] = {sj > 0.0 ? 1.0 : 0.0, 0.0};
     st->breakdown = sj > 0.0 ? 0 : 1;
   } else {
-    sj = sqrt(st->sums[2 + j].re);
+    sj = sqrt(ssum[2 + j].re);
     st->s[j] = sj;
     st->To[j - 1] = sj;
     const double isj = inv_or_zero(sj);
     for (int k = 0; k < j; ++k) {
       const double f = inv_or_zero(st->s[k]) * isj;
-      st->G[j][k] = f * st->sums[2 + k];
+      st->G[j][k] = f * ssum[2 + k];
     }
     st->G[j][j] = {sj > 0.0 ? 1.0 : 0.0, 0.0};
     if (!(sj > 0.0) && st->breakdown == 0) st->breakdown = j + 1;
   }
   const double isj = inv_or_zero(sj);
-  const cplx alpha = (isj * isj) * st->sums[0];
+  const cplx alpha = (isj * isj) * ssum[0];
   st->Td[j] = alpha.re;
   st->H[j][j] = alpha;
   for (int k = 0; k < j; ++k) {
@@ -289,13 +549,21 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_final(KState *__restrict__ 
                                                            int m, int do_sum, int do_coef, int nf,
                                                            int f0, int f1, double t_re,
                                                            double t_im) {
+  __shared__ cplx ssum[MMAX];
   if (do_sum && m >= 2) {
-    sum_partials(partU, nbU, m, 0, m, st->sums);
+    sum_partials(partU, nbU, m, ssum);
+    __syncthreads();
+    if (!do_coef) {
+      for (int v = threadIdx.x; v < m; v += NTHREADS) st->sums[v] = ssum[v];
+      return;
+    }
+  } else if (m >= 2) {
+    for (int v = threadIdx.x; v < m; v += NTHREADS) ssum[v] = st->sums[v];
     __syncthreads();
   }
   if (!do_coef) return;
   if (threadIdx.x == 0 && m >= 2) {
-    const double s = sqrt(st->sums[m - 1].re);
+    const double s = sqrt(ssum[m - 1].re);
     st->s[m - 1] = s;
     st->To[m - 2] = s;
     if (!(s > 0.0) && st->breakdown == 0) st->breakdown = m;
@@ -311,9 +579,18 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
                                          double t_re, double t_im) {
   __shared__ double d[MMAX], e[MMAX], Q[MMAX][MMAX + 1];
   const int lane = threadIdx.x;
+  // scale T to max|entry| = 1 (Eigen's SelfAdjointEigenSolver scales the same
+  // way); rotations then use sqrt(f^2 + g^2) without overflow risk.
+  double scl = 0.0;
+  for (int k = 0; k < m; ++k) {
+    scl = fmax(scl, fabs(st->Td[k]));
+    if (k < m - 1) scl = fmax(scl, fabs(st->To[k]));
+  }
+  const double iscl = scl > 0.0 ? 1.0 / scl : 1.0;
+  if (scl == 0.0) scl = 1.0;
   if (lane < m) {
-    d[lane] = st->Td[lane];
-    e[lane] = lane < m - 1 ? st->To[lane] : 0.0;
+    d[lane] = st->Td[lane] * iscl;
+    e[lane] = lane < m - 1 ? st->To[lane] * iscl : 0.0;
     for (int c = 0; c < m; ++c) Q[lane][c] = lane == c ? 1.0 : 0.0;
   }
   __builtin_amdgcn_wave_barrier();
@@ -337,7 +614,7 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
       bool early = false;
       for (int i = mm - 1; i >= l; --i) {
         const double ff = ss * e[i], bb = cc * e[i];
-        rr = hypot(ff, gg);
+        rr = sqrt(ff * ff + gg * gg);
         e[i + 1] = rr;
         if (rr == 0.0) {
           d[i + 1] -= pp;
@@ -345,8 +622,9 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
           early = true;
           break;
         }
-        ss = ff / rr;
-        cc = gg / rr;
+        const double irr = 1.0 / rr;
+        ss = ff * irr;
+        cc = gg * irr;
         gg = d[i + 1] - pp;
         rr = (d[i] - gg) * ss + 2.0 * cc * bb;
         pp = ss * rr;
@@ -364,6 +642,8 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
       e[mm] = 0.0;
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  if (lane < m) d[lane] *= scl;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   if (lane < m) {
     st->lam[lane] = d[lane];
@@ -422,7 +702,7 @@ __global__ __launch_bounds__(NTHREADS) void k_final_nlse(cplx *__restrict__ W, i
        p += (int64_t)gridDim.x * NTHREADS) {
     cplx y = {0.0, 0.0};
 #pragma unroll
-    for (int k = 0; k < M; ++k) y += cmul(c[k], W[(int64_t)k * vs + p]);
+    for (int k = 0; k < M; ++k) y += cmul(c[k], ld_nt(W + (int64_t)k * vs + p));
     const cplx un = nl_half(y, dt, nonlin, s1, s2);
     u[p] = un;
     W[p] = nl_half(un, dt, nonlin, s1, s2);

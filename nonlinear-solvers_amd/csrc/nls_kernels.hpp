@@ -6,12 +6,15 @@
 namespace nls {
 
 // stencil kernels (tiled march), argument lists:
-//   update : (S* W, int64_t vs, Geo g, const KState* st, cplx* part)
+//   update : (const S* W, S* out, int64_t vs, Geo g, const KState* st, cplx* part)
 //   alpha  : (const S* V, Geo g, cplx* part)
 //   lap    : (const S* V, Geo g, S* out)
 const void *kernel_update(bool complex_, int dim, int J);
 const void *kernel_alpha(bool complex_, int dim);
 const void *kernel_lap(bool complex_, int dim);
+int64_t stencil_tiles(const Geo &g, int dim, int rows_per_thread);
+int update_rows_per_thread(int J);
+int alpha_rows_per_thread();
 
 // single workgroup:
 //   reduce_iter  : (KState*, const cplx* partA, int nbA, const cplx* partU, int nbU, int j,
