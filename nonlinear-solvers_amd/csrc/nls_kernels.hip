@@ -234,7 +234,19 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
 
 // rows (3D) / x-chunks (2D) per thread: more independent columns per thread
 // for the light kernels, fewer for the register-heavy high-J updates.
-template <int J> struct UpdRB { static constexpr int v = J <= 2 ? 4 : (J <= 6 ? 2 : 1); };
+#ifndef NLS_UPD_RB_MODE
+#define NLS_UPD_RB_MODE 0
+#endif
+#ifndef NLS_COEF_LDS
+#define NLS_COEF_LDS 0
+#endif
+__host__ __device__ constexpr int upd_rb(int J) {
+  return NLS_UPD_RB_MODE == 0 ? (J <= 2 ? 4 : (J <= 6 ? 2 : 1))
+       : NLS_UPD_RB_MODE == 1 ? (J <= 2 ? 4 : 2)
+       : NLS_UPD_RB_MODE == 2 ? (J <= 6 ? 4 : 2)
+                              : (J <= 2 ? 4 : (J <= 6 ? 2 : (J <= 18 ? 2 : 1)));
+}
+template <int J> struct UpdRB { static constexpr int v = upd_rb(J); };
 constexpr int RB_ALPHA = 4;
 
 // y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
@@ -376,18 +388,29 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
   S acc[NA];
 #pragma unroll
   for (int k = 0; k < NA; ++k) acc[k] = zero<S>();
+#if NLS_COEF_LDS
+  // coefficients broadcast from LDS at every use: keeps ~4(J+1) SGPRs free
+  __shared__ cplx cfs[MMAX + 2];
+  for (int k = threadIdx.x; k <= J + 1; k += NTHREADS) cfs[k] = st->coef[k];
+  __syncthreads();
+  volatile cplx *b = cfs;
+  const double a = cfs[J + 1].re;
+#define NLS_B(k) cplx{b[k].re, b[k].im}
+#else
   cplx b[J + 1];
 #pragma unroll
   for (int k = 0; k <= J; ++k) b[k] = st->coef[k];
   const double a = st->coef[J + 1].re;
+#define NLS_B(k) b[k]
+#endif
   const S *__restrict__ VJ = W + (int64_t)J * vs;
   march<S, DIM, UpdRB<J>::v>(VJ, g, [&](int64_t p, const S &cur, const S &lap) {
     S wk[J > 0 ? J : 1];
 #pragma unroll
     for (int k = 0; k < J; ++k) wk[k] = ld_nt(W + (int64_t)k * vs + p);
-    S X = a * lap - coef_mul(b[J], cur);
+    S X = a * lap - coef_mul(NLS_B(J), cur);
 #pragma unroll
-    for (int k = 0; k < J; ++k) X = X - coef_mul(b[k], wk[k]);
+    for (int k = 0; k < J; ++k) X = X - coef_mul(NLS_B(k), wk[k]);
     st_nt(out + p, X);
 #pragma unroll
     for (int k = 0; k < J; ++k) acc[k] = acc[k] + cj_mul(wk[k], X);
@@ -398,6 +421,7 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
 #pragma unroll
   for (int k = 0; k < NA; ++k) v[k] = to_c(acc[k]);
   block_store<NA>(v, part);
+#undef NLS_B
 }
 
 // host-side mirror of the tiling, for grid sizes
@@ -418,7 +442,7 @@ int64_t stencil_tiles(const Geo &g, int dim, int rb) {
   }
   return a * b * c;
 }
-int update_rows_per_thread(int J) { return J <= 2 ? 4 : (J <= 6 ? 2 : 1); }
+int update_rows_per_thread(int J) { return upd_rb(J); }
 int alpha_rows_per_thread() { return RB_ALPHA; }
 
 // ---------------------------------------------------------------------------

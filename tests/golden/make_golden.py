@@ -1,0 +1,103 @@
+"""Generate the committed golden fixtures (small .npz, no pickles).
+
+Inputs are seeded synthetic fields; expected outputs come from the C oracle
+(oracle/nls_oracle.cpp, a restatement of the reference G1 Eigen path) and are
+cross-checked here against the independent numpy twin (oracle/np_ref.py)
+before being written.  Parity status: the reference itself cannot be built
+in this image (Eigen3 / libnpy absent), so these vectors are restatement
+outputs, pinned by the reference's published scipy known-answer test
+(tests/test_oracle.py::test_scipy_kat) -- see DESIGN.md "Oracle".
+
+Run:  python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import np_ref  # noqa: E402
+import oracle_py as O  # noqa: E402
+
+
+def field(dim, n, L, seed):
+    rng = np.random.default_rng(seed)
+    x = np.linspace(-L, L, n)
+    if dim == 2:
+        Y, X = np.meshgrid(x, x, indexing="ij")
+        u = np.exp(-((X - 1) ** 2 + Y ** 2)) * np.exp(1j * X) + 0.5 * np.exp(-((X + 2) ** 2 + (Y - 1) ** 2))
+    else:
+        Z, Y, X = np.meshgrid(x, x, x, indexing="ij")
+        u = np.exp(-((X - 1) ** 2 + Y ** 2 + Z ** 2)) * np.exp(1j * (X + Z))
+    u = u.ravel() + 1e-3 * (rng.standard_normal(u.size) + 1j * rng.standard_normal(u.size))
+    return u
+
+
+def main():
+    cases = {}
+    # --- cubic NLSE 2D 32^2, m=10, 20 steps (nlse_call defaults) --------------
+    n, L, dt = 32, 10.0, 1e-3
+    dx = 2 * L / (n - 1)
+    u0 = field(2, n, L, 1)
+    u0 /= np.sqrt(np.sum(np.abs(u0) ** 2) * dx * dx)
+    g = O.grid(2, n, n, 1, dx, dx)
+    out = O.nlse_steps(g, u0, dt, 20, 10)
+    tw = np_ref.nlse_steps(2, n, n, 1, dx, dx, u0, dt, 20, 10)
+    assert np.linalg.norm(out - tw) / np.linalg.norm(tw) < 1e-12
+    cases["nlse2d"] = dict(dim=2, n=n, dx=dx, dt=dt, steps=20, m=10, nonlin=0, u0=u0, u=out)
+    # --- cubic-quintic 2D 24^2, m=16, 10 steps ----------------------------------
+    n = 24
+    dx = 2 * L / (n - 1)
+    u0 = field(2, n, L, 2)
+    u0 /= np.sqrt(np.sum(np.abs(u0) ** 2) * dx * dx)
+    g = O.grid(2, n, n, 1, dx, dx)
+    out = O.nlse_steps(g, u0, dt, 10, 16, nonlin=1)
+    tw = np_ref.nlse_steps(2, n, n, 1, dx, dx, u0, dt, 10, 16, nonlin=1)
+    assert np.linalg.norm(out - tw) / np.linalg.norm(tw) < 1e-12
+    cases["cq2d"] = dict(dim=2, n=n, dx=dx, dt=dt, steps=10, m=16, nonlin=1, u0=u0, u=out)
+    # --- cubic NLSE 3D 12^3, m=16, 5 steps --------------------------------------
+    n = 12
+    dx = 2 * L / (n - 1)
+    u0 = field(3, n, L, 3)
+    u0 /= np.sqrt(np.sum(np.abs(u0) ** 2) * dx ** 3)
+    g = O.grid(3, n, n, n, dx, dx)
+    out = O.nlse_steps(g, u0, dt, 5, 16)
+    tw = np_ref.nlse_steps(3, n, n, n, dx, dx, u0, dt, 5, 16)
+    assert np.linalg.norm(out - tw) / np.linalg.norm(tw) < 1e-12
+    cases["nlse3d"] = dict(dim=3, n=n, dx=dx, dt=dt, steps=5, m=16, nonlin=0, u0=u0, u=out)
+    # --- sine-Gordon 2D 32^2, Gautschi m=10, 10 steps ---------------------------
+    n, L = 32, 3.0
+    dx = 2 * L / (n - 1)
+    x = np.linspace(-L, L, n)
+    Y, X = np.meshgrid(x, x, indexing="ij")
+    su0 = (2.0 * np.arctan(np.exp(3.0 - 5.0 * np.sqrt(X * X + Y * Y)))).ravel()
+    sdt = 5.0 / 500
+    sup = su0.copy()
+    mf = -np.ones(su0.size)
+    g = O.grid(2, n, n, 1, dx, dx)
+    su, sup1 = O.sg_steps(g, su0, sup, mf, sdt, 10, 10)
+    tu, tup = np_ref.sg_steps(2, n, n, 1, dx, dx, su0, sup, mf, sdt, 10, 10)
+    assert np.linalg.norm(su - tu) / np.linalg.norm(tu) < 1e-11
+    cases["sg2d"] = dict(dim=2, n=n, dx=dx, dt=sdt, steps=10, m=10, u0=su0, u_past0=sup, mfield=mf,
+                         u=su, u_past=sup1)
+    # --- one Krylov action per matrix function, 3D 10^3 -------------------------
+    n, L = 10, 5.0
+    dx = 2 * L / (n - 1)
+    g = O.grid(3, n, n, n, dx, dx)
+    ur = np.real(field(3, n, L, 4))
+    uc = field(3, n, L, 5)
+    kr = {f"f{f}": O.krylov_r(g, ur, 1e-2, 12, f) for f in (2, 3, 4, 5, 6)}
+    kc = {"f0": O.krylov_c(g, uc, -1e-2j, 12, 0), "f1": O.krylov_c(g, uc, 1e-2j, 12, 1)}
+    lap = O.laplacian_c(g, uc)
+    cases["krylov3d"] = dict(dim=3, n=n, dx=dx, m=12, ur=ur, uc=uc, lap=lap,
+                             **{"r_" + k: v for k, v in kr.items()}, **{"c_" + k: v for k, v in kc.items()})
+    for name, d in cases.items():
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **{k: np.asarray(v) for k, v in d.items()})
+    total = sum(os.path.getsize(os.path.join(HERE, f"{k}.npz")) for k in cases)
+    print(f"wrote {len(cases)} fixtures, {total / 1024:.1f} KiB")
+
+
+if __name__ == "__main__":
+    main()

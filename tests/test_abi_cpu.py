@@ -1,0 +1,119 @@
+"""CPU checks of the drop-in boundary: the C-ABI library loads, exports every
+entry point include/nls.h declares, validates configs before touching a device,
+and the CLI drivers keep the reference's argv/exit-code contract
+(device/nlse_call.cpp:13-24, 51-56)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "nonlinear-solvers_amd", "bin")
+HEADER = os.path.join(ROOT, "include", "nls.h")
+
+nls_amd = pytest.importorskip("nls_amd")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(nls_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = nls_amd.lib()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(nls_amd.EXPORTED_SYMBOLS) == syms
+    assert L.nls_abi_version() == 1
+    out = subprocess.run(["nm", "-D", "--defined-only", nls_amd.lib_path()], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (nls_\w+)", out))
+    assert set(syms) <= exported
+
+
+def test_config_default_matches_reference_defaults():
+    L = nls_amd.lib()
+    c = nls_amd.Config()
+    L.nls_config_default(C.byref(c))
+    assert c.krylov_m == 10                       # device/nlse_solver_dev.hpp:48
+    assert tuple(c.sigma1) == (0.0, 0.5)          # device/nlse_cq_solver.hpp:19
+    assert tuple(c.sigma2) == (-0.5, 0.0)
+    assert c.nranks == 1 and c.rank == 0 and c.device == -1
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(m=0), "krylov_m"), (dict(m=33), "krylov_m"), (dict(dim=4), "dim"),
+    (dict(nx=1), "grid too small"), (dict(dx=0.0), "dx"), (dict(nranks=2), "rccl_id"),
+])
+def test_invalid_config_rejected_before_device(kw, msg):
+    base = dict(dim=2, nx=16, ny=16, nz=1, dx=0.5)
+    base.update(kw)
+    m = base.pop("m", 10)
+    nranks = base.pop("nranks", 1)
+    with pytest.raises(nls_amd.NlsError) as e:
+        nls_amd.Solver(base["dim"], base["nx"], base["ny"], base["nz"], base["dx"], m=m, nranks=nranks)
+    assert e.value.code == -1 and msg in str(e.value)
+
+
+def run(args, **kw):
+    return subprocess.run(args, capture_output=True, text=True, timeout=60, **kw)
+
+
+@pytest.mark.parametrize("prog", ["nlse_call", "nlse_cq_call", "to_nlse_call"])
+def test_driver_usage_exit_code(prog):
+    r = run([os.path.join(BIN, prog)])
+    assert r.returncode == 1 and "Usage:" in r.stderr
+    r = run([os.path.join(BIN, prog)] + ["8"] * 8)
+    assert r.returncode == 1 and "Usage:" in r.stderr
+
+
+def test_driver_shape_mismatch(tmp_path):
+    u = np.zeros((16, 12), complex)
+    f = tmp_path / "u0.npy"
+    np.save(f, u)
+    r = run([os.path.join(BIN, "nlse_call"), "12", "12", "10", "10", str(f), str(tmp_path / "o.npy"),
+             "1.5", "10", "5"])
+    assert r.returncode == 1
+    assert "Input array dimensions mismatch" in r.stderr and "Expected: 12x12" in r.stderr
+
+
+def test_driver_guards_zero_snapshot_frequency(tmp_path):
+    f = tmp_path / "u0.npy"
+    np.save(f, np.ones((8, 8), complex))
+    r = run([os.path.join(BIN, "nlse_call"), "8", "8", "10", "10", str(f), str(tmp_path / "o.npy"),
+             "1.5", "5", "10"])
+    assert r.returncode == 1 and "num_snapshots" in r.stderr
+
+
+def test_sg_driver_rejects_positional():
+    r = run([os.path.join(BIN, "sg_driver_dev"), "256"])
+    assert r.returncode == 1 and "Usage" in r.stderr
+
+
+@pytest.mark.parametrize("shape,dtype", [((7,), complex), ((5, 3), complex), ((2, 3, 4), complex),
+                                         ((4, 2, 3, 2), complex), ((6,), float), ((3, 5), float)])
+def test_npy_codec_roundtrip(tmp_path, shape, dtype):
+    rng = np.random.default_rng(0)
+    a = rng.standard_normal(shape)
+    if dtype is complex:
+        a = a + 1j * rng.standard_normal(shape)
+    f, g = tmp_path / "a.npy", tmp_path / "b.npy"
+    np.save(f, a)
+    mode = "copy-c16" if dtype is complex else "copy-f8"
+    r = run([os.path.join(BIN, "npy_tool"), mode, str(f), str(g)])
+    assert r.returncode == 0, r.stderr
+    b = np.load(g)
+    assert b.dtype == a.dtype and b.shape == a.shape and np.array_equal(a, b)
+    r = run([os.path.join(BIN, "npy_tool"), "shape", str(g)])
+    assert r.stdout.split() == [str(s) for s in shape]
+
+
+def test_npy_codec_rejects_wrong_dtype(tmp_path):
+    f = tmp_path / "a.npy"
+    np.save(f, np.zeros((3, 3), np.float32))
+    r = run([os.path.join(BIN, "npy_tool"), "copy-c16", str(f), str(tmp_path / "b.npy")])
+    assert r.returncode == 1 and "dtype" in r.stderr

@@ -1,0 +1,101 @@
+"""GPU: the drop-in CLI drivers end to end (argv + .npy in, .npy out), checked
+against the oracle driven with the reference drivers' semantics
+(device/nlse_call.cpp:35-82, device/sg_driver_dev.cpp:23-80)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "nonlinear-solvers_amd", "bin")
+
+
+def reference_trajectory(dim, n, L, u0, T, nt, ns, m=10, nonlin=0):
+    dx = 2 * L / (n - 1)
+    dt = T / nt
+    freq = nt // ns
+    u = u0.ravel() / np.sqrt(np.sum(np.abs(u0) ** 2) * dx ** dim)
+    g = O.grid(dim, n, n, n, dx, dx)
+    snaps = [u.copy()]
+    for i in range(1, nt):
+        u = O.nlse_steps(g, u, dt, 1, m, nonlin=nonlin)
+        if i % freq == 0 and len(snaps) < ns:
+            snaps.append(u.copy())
+    return np.array(snaps)
+
+
+def ic(dim, n, L):
+    x = np.linspace(-L, L, n)
+    if dim == 2:
+        Y, X = np.meshgrid(x, x, indexing="ij")
+        return np.exp(-((X - 3) ** 2 + (Y - 3) ** 2) / 0.16) * np.exp(-1j * (X + Y)) + \
+            np.exp(-((X + 3) ** 2 + (Y + 3) ** 2) / 0.16) * np.exp(1j * (X + Y))   # nlse_driver.cpp:52-66
+    Z, Y, X = np.meshgrid(x, x, x, indexing="ij")
+    return np.exp(-(X ** 2 + Y ** 2 + Z ** 2) / 2) * np.exp(1j * X)
+
+
+@pytest.mark.parametrize("prog,nonlin", [("nlse_call", 0), ("nlse_cq_call", 1), ("to_nlse_call", 0)])
+def test_nlse_call_matches_oracle(tmp_path, prog, nonlin):
+    n, L, T, nt, ns = 32, 10.0, 0.02, 20, 4
+    u0 = ic(2, n, L)
+    fi, fo = tmp_path / "u0.npy", tmp_path / "traj.npy"
+    np.save(fi, u0)
+    r = subprocess.run([os.path.join(BIN, prog), str(n), str(n), str(L), str(L), str(fi), str(fo),
+                        str(T), str(nt), str(ns)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert re.match(r"^Trajectory took: \d\.\d{4}e[+-]\d\ds$", r.stdout.strip())
+    out = np.load(fo)
+    assert out.shape == (ns, n, n) and out.dtype == np.complex128
+    ref = reference_trajectory(2, n, L, u0, T, nt, ns, nonlin=nonlin).reshape(ns, n, n)
+    for k in range(ns):
+        assert rel_l2(out[k], ref[k]) <= 1e-10
+
+
+def test_nlse_call_3d_matches_oracle(tmp_path):
+    n, L, T, nt, ns = 12, 5.0, 0.01, 10, 2
+    u0 = ic(3, n, L)
+    fi, fo = tmp_path / "u0.npy", tmp_path / "traj.npy"
+    np.save(fi, u0)
+    r = subprocess.run([os.path.join(BIN, "nlse_call_3d"), str(n), str(n), str(n), str(L), str(L), str(L),
+                        str(fi), str(fo), str(T), str(nt), str(ns), "--m=16"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = np.load(fo)
+    assert out.shape == (ns, n, n, n)
+    ref = reference_trajectory(3, n, L, u0, T, nt, ns, m=16).reshape(ns, n, n, n)
+    for k in range(ns):
+        assert rel_l2(out[k], ref[k]) <= 1e-10
+
+
+def test_sg_driver_matches_oracle(tmp_path):
+    n, L, T, nt, ns = 32, 3.0, 0.2, 20, 4
+    r = subprocess.run([os.path.join(BIN, "sg_driver_dev"), f"--nx={n}", f"--T={T}", f"--nt={nt}",
+                        f"--ns={ns}", f"--prefix={tmp_path}/sg"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    u = np.load(tmp_path / "sg_u_device.npy")
+    v = np.load(tmp_path / "sg_v_device.npy")
+    assert u.shape == (ns, n, n) and v.shape == (ns, n, n)
+    dx = 2 * L / (n - 1)
+    dt = T / nt
+    x = np.linspace(-L, L, n)
+    X, Y = np.meshgrid(x, x, indexing="ij")
+    u0 = (2.0 * np.arctan(np.exp(3.0 - 5.0 * np.sqrt(X * X + Y * Y)))).ravel()
+    g = O.grid(2, n, n, 1, dx, dx)
+    cu, cp = u0.copy(), u0.copy()
+    mf = -np.ones(n * n)
+    ref_u, ref_v = [u0], [np.zeros(n * n)]
+    for i in range(1, nt):
+        cu, cp = O.sg_steps(g, cu, cp, mf, dt, 1, 10)
+        if i % (nt // ns) == 0 and len(ref_u) < ns:
+            ref_u.append(cu.copy())
+            ref_v.append((cu - cp) / dt)
+    for k in range(ns):
+        assert rel_l2(u[k].ravel(), ref_u[k]) <= 1e-10
+        if k:
+            assert rel_l2(v[k].ravel(), ref_v[k]) <= 1e-8

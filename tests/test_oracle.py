@@ -1,0 +1,171 @@
+"""CPU tests of the oracle (test infrastructure) -- pins it before it is trusted.
+
+1. Operator: the matrix-free restatement equals a literal transcription of the
+   reference triplet builders (laplacians.hpp:10-105), entry for entry, and
+   shows the quirks the survey measured (3D y-wrap, non-NSD 3D operator).
+2. Known-answer test from the reference's own published artefact
+   (nlsolvers/scipy-test/data/_comparison_without_lanczos_check.png, setup
+   nlsolvers/host/drivers/test_scipy_matfunc.cpp:41-95 and
+   nlsolvers/scipy-test/check_krylov_compute.py:41-49): Krylov exp action vs
+   scipy.sparse.linalg.expm_multiply, 3D 50^3, L=2, t=1e-2.
+3. Two independent restatements (C oracle, numpy twin with eigh) agree.
+4. Golden fixtures (tests/golden/make_golden.py) are reproduced.
+"""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse.linalg as spla
+
+import np_ref
+import oracle_py as O
+from conftest import rel_l2
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("dim,n", [(2, 2), (2, 5), (2, 12), (3, 2), (3, 4), (3, 7)])
+def test_operator_equals_triplet_builder(dim, n):
+    dx = 0.37
+    A = np_ref.laplacian_triplets(dim, n, dx)
+    N = A.shape[0]
+    g = O.grid(dim, n, n, n, dx, dx)
+    rng = np.random.default_rng(n)
+    for _ in range(2):
+        x = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+        ref = A @ x
+        assert np.array_equal(O.laplacian_c(g, x), ref) or rel_l2(O.laplacian_c(g, x), ref) < 1e-15
+        assert rel_l2(O.laplacian_r(g, x.real), A @ x.real) < 1e-15
+        assert rel_l2(np_ref.laplacian_apply(dim, n, n, n, dx, dx, x), ref) < 1e-15
+    # exact matrix reconstruction from the matrix-free apply (unit vectors)
+    if N <= 400:
+        M = np.column_stack([O.laplacian_r(g, np.eye(N)[:, k]) for k in range(N)])
+        assert np.array_equal(M, A.toarray())
+
+
+def test_operator_quirks():
+    n = 8
+    dx = 1.0
+    A = np_ref.laplacian_triplets(3, n, dx).toarray()
+    assert np.array_equal(A, A.T)
+    # 3D y-wrap couplings (i, n-1, k) <-> (i, 0, k+1) for k < n-1: n*(n-1) of them
+    wrap = 0
+    for k in range(n - 1):
+        for i in range(n):
+            p = k * n * n + (n - 1) * n + i
+            q = (k + 1) * n * n + 0 * n + i
+            wrap += A[p, q] != 0
+    assert wrap == n * (n - 1)
+    # the 3D operator is not negative semi-definite: max eig +0.299/dx^2 at n=8
+    ev = np.linalg.eigvalsh(A)
+    assert 0.29 < ev.max() < 0.31
+    # boundary diagonals -5 (3D) / -3 (2D), not minus the neighbour count
+    assert A[0, 0] == -5.0 and A[n * n * (n // 2) + n * (n // 2) + n // 2, n * n * (n // 2) + n * (n // 2) + n // 2] == -6.0
+    A2 = np_ref.laplacian_triplets(2, n, dx).toarray()
+    assert A2[0, 0] == -3.0 and np.linalg.eigvalsh(A2).max() < 0
+
+
+def _kat_setup():
+    n, L, t = 50, 2.0, 1e-2
+    dx = 2 * L / n
+    A = np_ref.aniso_laplacian_3d(n, dx, np.ones(n ** 3))
+    u0 = np_ref.centered_gaussian_3d(n, L, L / 5)
+    return A, u0, t
+
+
+def test_scipy_kat():
+    """Published accuracy (plot): real m=10 ~5e-10, m>=20 ~2e-15; complex m=10 ~1.2e-9,
+    m>=20 ~3e-13.  The oracle must land on those values (G2 exp(t*lambda) convention)."""
+    A, u0, t = _kat_setup()
+    ys = spla.expm_multiply(A, u0, start=0, stop=t, endpoint=True, num=2)[-1]
+    yc = spla.expm_multiply(1j * A.astype(np.complex128), u0.astype(np.complex128),
+                            start=0, stop=t, endpoint=True, num=2)[-1]
+    er = {m: rel_l2(O.krylov_csr(A, u0, t, m, O_F_EXP), ys) for m in (10, 20, 30)}
+    ec = {m: rel_l2(O.krylov_csr(A, u0.astype(complex), 1j * t, m, O_F_EXP), yc) for m in (10, 20, 30)}
+    assert 3e-10 < er[10] < 9e-10, er
+    assert er[20] < 1e-13 and er[30] < 1e-13, er
+    assert 7e-10 < ec[10] < 2e-9, ec
+    assert 5e-14 < ec[20] < 1e-12 and ec[30] < 1e-12, ec
+
+
+O_F_EXP = 1
+
+
+@pytest.mark.parametrize("dim,n", [(2, 20), (3, 8)])
+def test_oracle_matches_numpy_twin(dim, n):
+    L = 5.0
+    dx = 2 * L / (n - 1)
+    g = O.grid(dim, n, n, n, dx, dx)
+    rng = np.random.default_rng(9)
+    N = n ** dim
+    u = np.exp(-np.linspace(-2, 2, N) ** 2) + 1e-2 * (rng.standard_normal(N) + 1j * rng.standard_normal(N))
+    ap = lambda v: np_ref.laplacian_apply(dim, n, n, n, dx, dx, v)
+    for m in (1, 2, 10, 16):
+        a = O.krylov_c(g, u, -1e-3j, m, 0)
+        b = np_ref.krylov(ap, u, -1e-3j, m, 0)
+        assert rel_l2(a, b) < 1e-13
+    for f in (2, 3, 4, 5, 6):
+        a = O.krylov_r(g, u.real, 1e-2, 10, f)
+        b = np_ref.krylov(ap, u.real, 1e-2, 10, f)
+        assert rel_l2(a, b) < 1e-12
+    a = O.nlse_steps(g, u, 1e-3, 5, 10)
+    b = np_ref.nlse_steps(dim, n, n, n, dx, dx, u, 1e-3, 5, 10)
+    assert rel_l2(a, b) < 1e-13
+    a = O.nlse_steps(g, u, 1e-3, 5, 10, nonlin=1)
+    b = np_ref.nlse_steps(dim, n, n, n, dx, dx, u, 1e-3, 5, 10, nonlin=1)
+    assert rel_l2(a, b) < 1e-13
+
+
+def test_oracle_structural_properties():
+    """exp of a Hermitian T is unitary and the nonlinear phase has unit modulus:
+    the cubic SS2 step conserves the discrete L2 norm."""
+    n, L = 24, 10.0
+    dx = 2 * L / (n - 1)
+    g = O.grid(2, n, n, 1, dx, dx)
+    rng = np.random.default_rng(0)
+    u = rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)
+    out = O.nlse_steps(g, u, 1e-3, 10, 16)
+    assert abs(np.linalg.norm(out) / np.linalg.norm(u) - 1) < 1e-13
+    # m = 1: T = [0] so exp(T) = 1 and the linear part is the identity
+    out1 = O.krylov_c(g, u, -1e-3j, 1, 0)
+    assert rel_l2(out1, u) < 1e-15
+
+
+def test_reference_breakdown_semantics():
+    """The Eigen path divides by beta = 0 (eigen_krylov_complex.hpp:20,47): NaN.
+    The device library follows the device guard instead (tests/test_gpu_parity.py)."""
+    g = O.grid(2, 8, 8, 1, 1.0, 1.0)
+    with np.errstate(all="ignore"):
+        out = O.krylov_c(g, np.zeros(64, complex), -1e-3j, 4, 0)
+    assert np.all(np.isnan(out))
+
+
+@pytest.mark.parametrize("name", ["nlse2d", "cq2d", "nlse3d"])
+def test_golden_nlse(name):
+    d = np.load(os.path.join(GOLD, f"{name}.npz"))
+    n, dim = int(d["n"]), int(d["dim"])
+    g = O.grid(dim, n, n, n, float(d["dx"]), float(d["dx"]))
+    out = O.nlse_steps(g, d["u0"], float(d["dt"]), int(d["steps"]), int(d["m"]), nonlin=int(d["nonlin"]))
+    assert rel_l2(out, d["u"]) < 1e-13
+    tw = np_ref.nlse_steps(dim, n, n, n, float(d["dx"]), float(d["dx"]), d["u0"], float(d["dt"]),
+                           int(d["steps"]), int(d["m"]), nonlin=int(d["nonlin"]))
+    assert rel_l2(tw, d["u"]) < 1e-12
+
+
+def test_golden_sg():
+    d = np.load(os.path.join(GOLD, "sg2d.npz"))
+    n = int(d["n"])
+    g = O.grid(2, n, n, 1, float(d["dx"]), float(d["dx"]))
+    u, up = O.sg_steps(g, d["u0"], d["u_past0"], d["mfield"], float(d["dt"]), int(d["steps"]), int(d["m"]))
+    assert rel_l2(u, d["u"]) < 1e-13 and rel_l2(up, d["u_past"]) < 1e-13
+
+
+def test_golden_krylov_functions():
+    d = np.load(os.path.join(GOLD, "krylov3d.npz"))
+    n, m = int(d["n"]), int(d["m"])
+    g = O.grid(3, n, n, n, float(d["dx"]), float(d["dx"]))
+    for f in (2, 3, 4, 5, 6):
+        assert rel_l2(O.krylov_r(g, d["ur"], 1e-2, m, f), d[f"r_f{f}"]) < 1e-13
+    assert rel_l2(O.krylov_c(g, d["uc"], -1e-2j, m, 0), d["c_f0"]) < 1e-13
+    assert rel_l2(O.krylov_c(g, d["uc"], 1e-2j, m, 1), d["c_f1"]) < 1e-13
+    assert rel_l2(O.laplacian_c(g, d["uc"]), d["lap"]) < 1e-15
