@@ -89,6 +89,7 @@ typedef struct nls_config {
   int32_t nranks;       /* slab decomposition over ranks (1 = single GPU) */
   int32_t rank;         /* this rank, 0..nranks-1 */
   const void *rccl_id;  /* 128-byte RCCL unique id (nls_rccl_unique_id on rank 0), NULL if nranks == 1 */
+  void *local_group;    /* in-process rank group (nls_group_create); replaces RCCL when non-NULL */
 } nls_config;
 
 typedef struct nls_handle nls_handle;
@@ -129,6 +130,17 @@ int nls_laplacian_apply(nls_handle *h, const double *x, double *y, uint64_t n_lo
 
 /* Multi-GPU: 128-byte RCCL unique id, created on rank 0 and broadcast by the caller. */
 int nls_rccl_unique_id(void *out128);
+
+/* In-process rank group: the ranks of one slab decomposition are handles of
+ * ONE process, each driven by its own host thread (the reference's
+ * one-solver-per-OpenMP-thread model, device/nlse_driver_omp.cpp:103-121).
+ * Halo planes move by device-to-device copies and the Lanczos sums are
+ * reduced in fixed rank order on the device -- the same kernels and slab
+ * layout as the RCCL path, usable on a single GPU.  Pass the group as
+ * nls_config.local_group (rccl_id is then ignored). */
+typedef struct nls_group nls_group;
+int nls_group_create(int32_t nranks, nls_group **out);
+int nls_group_destroy(nls_group *g);
 
 /* Instrumentation: HIP-event timing around every launch on the handle's
  * stream.  Classes: 0 alpha (stencil + dot), 1 update (stencil + CGS +

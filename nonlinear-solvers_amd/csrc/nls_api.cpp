@@ -10,7 +10,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -42,7 +45,24 @@ struct Fail {
   int code;
 };
 
+constexpr int NSUM = 2 * MMAX + 8;  // cplx words of KState::sums
+constexpr int EVRING = 8;            // events per handle for the local transport
+
 }  // namespace
+
+// In-process rank group (local transport): a host-side rendezvous per exchange
+// plus device buffers for the fixed-order all-reduce.
+struct nls_group {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t gen = 0;
+  int arrived = 0;
+  bool aborted = false;
+  std::vector<std::vector<uint64_t>> slots, done;
+  cplx *pub = nullptr;  // [rank][parity][NSUM]
+  int dev = -1;
+};
 
 struct nls_handle {
   nls_config cfg{};
@@ -74,6 +94,10 @@ struct nls_handle {
   // multi-rank
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
+  nls_group *group = nullptr;  // local transport when non-NULL
+  bool collective = false;     // split reductions + exchanges (nranks > 1, or NLS_FORCE_RCCL=1)
+  hipEvent_t evring[EVRING] = {};
+  uint64_t evnext = 0, ar_count = 0;
 };
 
 namespace {
@@ -166,10 +190,54 @@ void launch(nls_handle *h, int cls, int j, const void *fn, int grid, void **args
 
 // ---- multi-rank plumbing ---------------------------------------------------
 
+// Host rendezvous of the local transport: every rank deposits a payload, the
+// last arrival publishes the round; bounded wait (a failed rank aborts all).
+std::vector<std::vector<uint64_t>> rendezvous(nls_handle *h, std::vector<uint64_t> payload) {
+  nls_group *g = h->group;
+  std::unique_lock<std::mutex> lk(g->mu);
+  if (g->aborted) fail(h, NLS_ERR_RCCL, "local group aborted by another rank");
+  const uint64_t my_gen = g->gen;
+  g->slots[h->rank] = std::move(payload);
+  if (++g->arrived == g->n) {
+    g->done = g->slots;
+    g->arrived = 0;
+    ++g->gen;
+    g->cv.notify_all();
+  } else if (!g->cv.wait_for(lk, std::chrono::seconds(300),
+                             [&] { return g->gen != my_gen || g->aborted; })) {
+    g->aborted = true;
+    g->cv.notify_all();
+    fail(h, NLS_ERR_RCCL, "local group rendezvous timed out");
+  }
+  if (g->aborted) fail(h, NLS_ERR_RCCL, "local group aborted by another rank");
+  return g->done;
+}
+
+hipEvent_t next_event(nls_handle *h) { return h->evring[h->evnext++ % EVRING]; }
+
+void halo_local(nls_handle *h, char *first, char *last, char *gbelow, char *gabove, size_t bytes) {
+  hipEvent_t ev = next_event(h);
+  hip_check(h, hipEventRecord(ev, h->stream), "hipEventRecord");
+  auto all = rendezvous(h, {(uint64_t)(uintptr_t)first, (uint64_t)(uintptr_t)last,
+                            (uint64_t)(uintptr_t)ev});
+  if (h->rank > 0) {
+    const auto &nb = all[h->rank - 1];
+    hip_check(h, hipStreamWaitEvent(h->stream, (hipEvent_t)(uintptr_t)nb[2], 0), "hipStreamWaitEvent");
+    hip_check(h, hipMemcpyAsync(gbelow, (const void *)(uintptr_t)nb[1], bytes, hipMemcpyDeviceToDevice,
+                                h->stream), "hipMemcpyAsync(halo)");
+  }
+  if (h->rank < h->nranks - 1) {
+    const auto &nb = all[h->rank + 1];
+    hip_check(h, hipStreamWaitEvent(h->stream, (hipEvent_t)(uintptr_t)nb[2], 0), "hipStreamWaitEvent");
+    hip_check(h, hipMemcpyAsync(gabove, (const void *)(uintptr_t)nb[0], bytes, hipMemcpyDeviceToDevice,
+                                h->stream), "hipMemcpyAsync(halo)");
+  }
+}
+
 // Exchange the boundary planes of vector k of basis b into the neighbours'
 // ghost planes (z-slab decomposition; one plane covers the 3D y-wrap too).
 void halo(nls_handle *h, int b, int k) {
-  if (h->nranks == 1) return;
+  if (!h->collective) return;
   const int64_t P = h->geo.P;
   const size_t cnt = (size_t)P * (h->cplx_ ? 2 : 1);
   char *v = vec_ptr(h, b, k);
@@ -181,6 +249,14 @@ void halo(nls_handle *h, int b, int k) {
     rec.a = get_event(h);
     rec.b = get_event(h);
     hip_check(h, hipEventRecord(rec.a, h->stream), "hipEventRecord");
+  }
+  if (h->group) {
+    halo_local(h, first, last, gbelow, gabove, (size_t)P * h->esize);
+    if (h->timing) {
+      hip_check(h, hipEventRecord(rec.b, h->stream), "hipEventRecord");
+      h->recs.push_back(rec);
+    }
+    return;
   }
   rccl_check(h, ncclGroupStart(), "ncclGroupStart");
   if (h->rank > 0) {
@@ -200,6 +276,36 @@ void halo(nls_handle *h, int b, int k) {
 
 void allreduce_sums(nls_handle *h, int b, int ncplx) {
   void *p = &h->B[b].st->sums[0];
+  if (h->group) {
+    // publish my partial sums, rendezvous, then every rank sums all ranks'
+    // publications in rank order (identical result on every rank)
+    nls_group *g = h->group;
+    const int parity = (int)(h->ar_count++ & 1);
+    cplx *mine = g->pub + ((int64_t)h->rank * 2 + parity) * NSUM;
+    hip_check(h, hipMemcpyAsync(mine, p, (size_t)ncplx * sizeof(cplx), hipMemcpyDeviceToDevice,
+                                h->stream), "hipMemcpyAsync(pub)");
+    hipEvent_t ev = next_event(h);
+    hip_check(h, hipEventRecord(ev, h->stream), "hipEventRecord");
+    auto all = rendezvous(h, {(uint64_t)(uintptr_t)ev});
+    for (int r = 0; r < h->nranks; ++r)
+      if (r != h->rank)
+        hip_check(h, hipStreamWaitEvent(h->stream, (hipEvent_t)(uintptr_t)all[r][0], 0),
+                  "hipStreamWaitEvent");
+    cplx *dst = static_cast<cplx *>(p);
+    int nr = h->nranks, par = parity, cnt = ncplx, stride = NSUM;
+    void *args[] = {&dst, &g->pub, &nr, &par, &cnt, &stride};
+    launch(h, 2, -1, kernel_sum_ranks(), 1, args);
+    if (std::getenv("NLS_DEBUG_SUMS")) {
+      std::vector<cplx> hv(ncplx), hp(ncplx);
+      hip_check(h, hipStreamSynchronize(h->stream), "sync");
+      hip_check(h, hipMemcpy(hv.data(), p, ncplx * sizeof(cplx), hipMemcpyDeviceToHost), "d2h");
+      hip_check(h, hipMemcpy(hp.data(), mine, ncplx * sizeof(cplx), hipMemcpyDeviceToHost), "d2h");
+      std::fprintf(stderr, "[rank %d ar %llu n %d] pub0 %.6e sum0 %.6e | pub1 %.6e sum1 %.6e\n", h->rank,
+                   (unsigned long long)h->ar_count, ncplx, hp[0].re, hv[0].re, ncplx > 1 ? hp[1].re : 0.0,
+                   ncplx > 1 ? hv[1].re : 0.0);
+    }
+    return;
+  }
   rccl_check(h, ncclAllReduce(p, p, (size_t)ncplx * 2, ncclDouble, ncclSum, h->comm, h->stream),
              "ncclAllReduce");
 }
@@ -210,7 +316,7 @@ void reduce_iter(nls_handle *h, int b, int j) {
   KState *st = h->B[b].st;
   int nbA = h->grid_alpha, nbU = j >= 1 ? h->grid_update[j - 1] : 0;
   const void *fn = kernel_reduce_iter();
-  if (h->nranks == 1) {
+  if (!h->collective) {
     int ds = 1, dc = 1;
     void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc};
     launch(h, 2, j, fn, 1, args);
@@ -230,7 +336,7 @@ void reduce_final(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
   KState *st = h->B[b].st;
   int m = h->m, nbU = m >= 2 ? h->grid_update[m - 2] : 0;
   const void *fn = kernel_reduce_final();
-  if (h->nranks == 1) {
+  if (!h->collective) {
     int ds = 1, dc = 1;
     void *args[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti};
     launch(h, 2, m, fn, 1, args);
@@ -426,7 +532,9 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   else if (!(c.dx > 0.0) || !(c.dy > 0.0)) why = "dx, dy must be > 0";
   else if (c.krylov_m < 1 || c.krylov_m > NLS_MAX_KRYLOV) why = "krylov_m must be in 1..32";
   else if (c.nranks < 1 || c.rank < 0 || c.rank >= c.nranks) why = "bad rank/nranks";
-  else if (c.nranks > 1 && !c.rccl_id) why = "nranks > 1 needs rccl_id";
+  else if (c.nranks > 1 && !c.rccl_id && !c.local_group) why = "nranks > 1 needs rccl_id or local_group";
+  else if (c.local_group && static_cast<nls_group *>(c.local_group)->n != c.nranks)
+    why = "local_group size != nranks";
   else if ((uint32_t)c.nranks > (c.dim == 3 ? c.nz : c.ny)) why = "more ranks than planes";
   if (!why.empty()) {
     g_create_error = why;
@@ -458,11 +566,29 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
     hip_check(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
     setup_geometry(h);
     alloc_all(h);
-    if (h->nranks > 1) {
+    if (h->nranks > 1 && c.local_group) {
+      h->group = static_cast<nls_group *>(c.local_group);
+      for (auto &e : h->evring)
+        hip_check(h, hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+      std::lock_guard<std::mutex> lk(h->group->mu);
+      if (!h->group->pub) {
+        hip_check(h, hipMalloc(&h->group->pub, (size_t)h->nranks * 2 * NSUM * sizeof(cplx)),
+                  "hipMalloc(group)");
+        hip_check(h, hipMemset(h->group->pub, 0, (size_t)h->nranks * 2 * NSUM * sizeof(cplx)),
+                  "hipMemset(group)");
+        h->group->dev = h->dev;
+      }
+    } else if (h->nranks > 1) {
       ncclUniqueId id;
       std::memcpy(&id, c.rccl_id, sizeof(id));
       rccl_check(h, ncclCommInitRank(&h->comm, h->nranks, id, h->rank), "ncclCommInitRank");
+    } else if (const char *e = std::getenv("NLS_FORCE_RCCL"); e && std::atoi(e)) {
+      // debug: run the collective code path through a 1-rank RCCL communicator
+      ncclUniqueId id;
+      rccl_check(h, ncclGetUniqueId(&id), "ncclGetUniqueId");
+      rccl_check(h, ncclCommInitRank(&h->comm, 1, id, 0), "ncclCommInitRank");
     }
+    h->collective = h->nranks > 1 || h->comm != nullptr;
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
   });
   if (rc != NLS_OK) {
@@ -486,6 +612,8 @@ int nls_destroy(nls_handle *h) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : h->evpool) (void)hipEventDestroy(e);
+  for (auto e : h->evring)
+    if (e) (void)hipEventDestroy(e);
   free_all(h);
   if (h->comm) ncclCommDestroy(h->comm);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -672,6 +800,27 @@ int nls_rccl_unique_id(void *out128) {
   }
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
   std::memcpy(out128, &id, sizeof(id));
+  return NLS_OK;
+}
+
+int nls_group_create(int32_t nranks, nls_group **out) {
+  if (!out || nranks < 1) return NLS_ERR_ARG;
+  nls_group *g = new (std::nothrow) nls_group();
+  if (!g) return NLS_ERR_OOM;
+  g->n = nranks;
+  g->slots.resize(nranks);
+  g->done.resize(nranks);
+  *out = g;
+  return NLS_OK;
+}
+
+int nls_group_destroy(nls_group *g) {
+  if (!g) return NLS_ERR_ARG;
+  if (g->pub) {
+    (void)hipSetDevice(g->dev);
+    (void)hipFree(g->pub);
+  }
+  delete g;
   return NLS_OK;
 }
 

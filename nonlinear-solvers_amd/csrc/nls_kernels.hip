@@ -487,11 +487,11 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_iter(KState *__restrict__ s
     if (j >= 1) sum_partials(partU, nbU, j + 1, ssum + 2);
     __syncthreads();
     if (!do_coef) {
-      for (int v = threadIdx.x; v < ncols; v += NTHREADS) ssum[v] = ssum[v];
+      for (int v = threadIdx.x; v < ncols; v += NTHREADS) st->sums[v] = ssum[v];
       return;
     }
   } else {
-    for (int v = threadIdx.x; v < ncols; v += NTHREADS) ssum[v] = ssum[v];
+    for (int v = threadIdx.x; v < ncols; v += NTHREADS) ssum[v] = st->sums[v];
     __syncthreads();
   }
   if (!do_coef || threadIdx.x != 0) return;
@@ -847,6 +847,17 @@ const void *kernel_lap(bool cplx_, int dim) {
   return dim == 3 ? reinterpret_cast<const void *>(&k_lap<double, 3>)
                   : reinterpret_cast<const void *>(&k_lap<double, 2>);
 }
+
+// local-transport all-reduce: dst[v] = sum_r pub[r][parity][v] in rank order
+__global__ __launch_bounds__(NTHREADS) void k_sum_ranks(cplx *__restrict__ dst, const cplx *__restrict__ pub,
+                                                        int nranks, int parity, int n, int stride) {
+  for (int v = threadIdx.x; v < n; v += NTHREADS) {
+    cplx s = {0.0, 0.0};
+    for (int r = 0; r < nranks; ++r) s += pub[((int64_t)r * 2 + parity) * stride + v];
+    dst[v] = s;
+  }
+}
+const void *kernel_sum_ranks() { return reinterpret_cast<const void *>(&k_sum_ranks); }
 
 const void *kernel_reduce_iter() { return reinterpret_cast<const void *>(&k_reduce_iter); }
 const void *kernel_reduce_final() { return reinterpret_cast<const void *>(&k_reduce_final); }

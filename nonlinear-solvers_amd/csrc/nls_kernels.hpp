@@ -22,6 +22,8 @@ int alpha_rows_per_thread();
 //   reduce_final : (KState*, const cplx* partU, int nbU, int m, int do_sum, int do_coef,
 //                   int nf, int f0, int f1, double t_re, double t_im)
 const void *kernel_reduce_iter();
+//   sum_ranks    : (cplx* dst, const cplx* pub, int nranks, int parity, int n, int stride)
+const void *kernel_sum_ranks();
 const void *kernel_reduce_final();
 
 // pointwise (grid-stride):

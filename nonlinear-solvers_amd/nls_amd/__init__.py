@@ -27,7 +27,8 @@ EXPORTED_SYMBOLS = (
     "nls_abi_version", "nls_config_default", "nls_create", "nls_destroy", "nls_last_error",
     "nls_local_planes", "nls_set_field", "nls_set_sg_state", "nls_step", "nls_sync",
     "nls_get_field", "nls_get_sg_velocity", "nls_krylov_apply", "nls_laplacian_apply",
-    "nls_rccl_unique_id", "nls_set_timing", "nls_get_timing", "nls_reset_timing",
+    "nls_rccl_unique_id", "nls_group_create", "nls_group_destroy", "nls_set_timing",
+    "nls_get_timing", "nls_reset_timing",
 )
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -46,7 +47,7 @@ class Config(C.Structure):
         ("krylov_m", C.c_uint32),
         ("sigma1", C.c_double * 2), ("sigma2", C.c_double * 2),
         ("device", C.c_int32), ("nranks", C.c_int32), ("rank", C.c_int32),
-        ("rccl_id", C.c_void_p),
+        ("rccl_id", C.c_void_p), ("local_group", C.c_void_p),
     ]
 
 
@@ -96,6 +97,8 @@ def lib():
     L.nls_krylov_apply.argtypes = [H, dp, C.c_double, C.c_double, C.c_int32, dp, C.c_uint64]
     L.nls_laplacian_apply.argtypes = [H, dp, dp, C.c_uint64]
     L.nls_rccl_unique_id.argtypes = [C.c_void_p]
+    L.nls_group_create.argtypes = [C.c_int32, C.POINTER(C.c_void_p)]
+    L.nls_group_destroy.argtypes = [C.c_void_p]
     L.nls_set_timing.argtypes = [H, C.c_int32]
     L.nls_get_timing.argtypes = [H, C.POINTER(Timing)]
     L.nls_reset_timing.argtypes = [H]
@@ -113,6 +116,31 @@ def rccl_unique_id() -> bytes:
     return buf.raw
 
 
+class Group:
+    """In-process rank group (nls_group_create): ranks are Solver handles of this
+    process driven from separate host threads; halo by D2D copies, fixed-order
+    device all-reduce.  Same slab layout and kernels as the RCCL path."""
+
+    def __init__(self, nranks: int):
+        g = C.c_void_p()
+        rc = lib().nls_group_create(int(nranks), C.byref(g))
+        if rc != 0:
+            raise NlsError(rc, "nls_group_create failed")
+        self._g = g
+        self.nranks = nranks
+
+    def close(self):
+        if getattr(self, "_g", None):
+            lib().nls_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def _dptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
@@ -127,7 +155,7 @@ class Solver:
 
     def __init__(self, dim, nx, ny, nz=1, dx=1.0, dy=None, equation=NLSE_CUBIC, m=10,
                  sigma1=(0.0, 0.5), sigma2=(-0.5, 0.0), device=-1, nranks=1, rank=0,
-                 rccl_id: bytes | None = None):
+                 rccl_id: bytes | None = None, group: "Group | None" = None):
         L = lib()
         cfg = Config()
         L.nls_config_default(C.byref(cfg))
@@ -141,6 +169,8 @@ class Solver:
         cfg.device, cfg.nranks, cfg.rank = device, nranks, rank
         self._id = C.create_string_buffer(rccl_id, 128) if rccl_id else None
         cfg.rccl_id = C.cast(self._id, C.c_void_p) if self._id is not None else None
+        self._group = group
+        cfg.local_group = group._g if group is not None else None
         self.cfg = cfg
         self.complex = equation != SG_GAUTSCHI
         self.dtype = np.complex128 if self.complex else np.float64
