@@ -158,7 +158,7 @@ def main():
     ap.add_argument("--workload", default="nlse3d_512", choices=sorted(WORKLOADS))
     ap.add_argument("--n", type=int, default=None, help="override grid side (testing only)")
     ap.add_argument("--m", type=int, default=None, help="override Krylov dim (testing only)")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

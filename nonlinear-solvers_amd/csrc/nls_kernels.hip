@@ -117,44 +117,49 @@ template <int DIM, int RB> __host__ __device__ inline void tile_counts(const Geo
 
 // fn(p, cur, lap) for every local cell p of the workgroup's tiles, with
 // cur = V[p] and lap = (L V)[p] (laplacians.hpp:10-105, flat-index form).
+// Local indices are 32-bit (the host guarantees (nzl+2)*P < 2^31); the flat
+// range tests of the reference (idx-nx >= 0, idx+nx < N) are evaluated on
+// (plane, row) coordinates so they never need 64-bit global indices.
 template <class S, int DIM, int RB, class Fn>
 __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn &&fn) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int64_t ntx, nty, ntz;
-  tile_counts<DIM, RB>(g, ntx, nty, ntz);
-  const int64_t tiles = ntx * nty * ntz;
-  const int64_t T8 = tiles / 8;
-  const int64_t P = g.P, nx = g.nx;
-  for (int64_t t0 = blockIdx.x; t0 < tiles; t0 += gridDim.x) {
+  int64_t ntx64, nty64, ntz64;
+  tile_counts<DIM, RB>(g, ntx64, nty64, ntz64);
+  const int ntx = (int)ntx64, nty = (int)nty64;
+  const int tiles = (int)(ntx64 * nty64 * ntz64);
+  const int T8 = tiles / 8;
+  const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, nzl = (int)g.nzl, kz = g.kz;
+  const int z0 = (int)g.z0, npl = (int)g.npl;
+  for (int t0 = blockIdx.x; t0 < tiles; t0 += gridDim.x) {
     // optional XCD-banded order (workgroups b, b+8 share an XCD): speed only
-    const int64_t t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
-    const int64_t it = t % ntx;
-    const int64_t rest = t / ntx;
-    const int64_t jt = rest % nty;
-    const int64_t kt = rest / nty;
+    const int t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
+    const int it = t % ntx;
+    const int rest = t / ntx;
+    const int jt = rest % nty;
+    const int kt = rest / nty;
     if constexpr (DIM == 3) {
-      const int64_t x = it * 64 + lane;
+      const int x = it * 64 + lane;
       const bool xin = x < nx;
-      const int64_t yb = jt * (4 * RB) + (int64_t)w * RB;
-      if (yb >= g.nyp) continue;  // wave-uniform
-      const int64_t q0 = kt * g.kz;
-      const int64_t q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
+      const int yb = jt * (4 * RB) + w * RB;
+      if (yb >= nyp) continue;  // wave-uniform
+      const int q0 = kt * kz;
+      const int q1 = q0 + kz < nzl ? q0 + kz : nzl;
       bool rv[RB];
-      int64_t off[RB];
+      int off[RB];
       S prev[RB], cur[RB];
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
-        rv[r] = yb + r < g.nyp;
+        rv[r] = yb + r < nyp;
         off[r] = (yb + r) * nx + x;
         const bool ld = xin && rv[r];
-        prev[r] = (ld && g.z0 + q0 > 0) ? V[(q0 - 1) * P + off[r]] : zero<S>();
+        prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + off[r]] : zero<S>();
         cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
       }
       const bool bx = (x == 0) || (x == nx - 1);
-      for (int64_t q = q0; q < q1; ++q) {
-        const int64_t gq = g.z0 + q;
-        const bool bz = gq == 0 || gq == g.npl - 1;
-        const bool has_next = gq + 1 < g.npl;
+      for (int q = q0; q < q1; ++q) {
+        const int gq = z0 + q;
+        const bool bz = gq == 0 || gq == npl - 1;
+        const bool has_next = gq + 1 < npl;
         S next[RB];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
@@ -162,20 +167,21 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           if (!rv[r]) continue;  // wave-uniform
-          const int64_t p = q * P + off[r];
-          const int64_t pg = gq * P + off[r];
+          const int p = q * P + off[r];
+          const int y = yb + r;
           S ym, yp;
           if (r > 0) ym = cur[r - 1];
-          else ym = (xin && pg >= nx) ? V[p - nx] : zero<S>();
+          else ym = (xin && (gq > 0 || y > 0)) ? V[p - nx] : zero<S>();            // idx - nx >= 0
           if (r + 1 < RB && rv[r + 1 < RB ? r + 1 : r]) yp = cur[r + 1 < RB ? r + 1 : r];
-          else yp = (xin && pg + nx < g.Ng) ? V[p + nx] : zero<S>();
+          else yp = (xin && (gq < npl - 1 || y < nyp - 1)) ? V[p + nx] : zero<S>();  // idx + nx < N
           S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
-          if (lane == 0) xm = (xin && x > 0) ? V[p - 1] : zero<S>();
-          if (lane == 63) xp = (xin && x + 1 < nx) ? V[p + 1] : zero<S>();
+          const S xe = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin
+                           ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
+          if (lane == 0) xm = xe;
+          if (lane == 63) xp = xe;
           if (!(x > 0)) xm = zero<S>();
           if (!(x + 1 < nx)) xp = zero<S>();
-          const int64_t y = yb + r;
-          const bool bnd = bx || bz || y == 0 || y == g.nyp - 1;
+          const bool bnd = bx || bz || y == 0 || y == nyp - 1;
           const S lap = g.s * (((prev[r] + next[r]) + (xm + xp)) + (ym + yp)) +
                         (bnd ? g.sd_bd : g.sd_in) * cur[r];
           if (xin) fn(p, cur[r], lap);
@@ -187,35 +193,38 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
         }
       }
     } else {
-      const int64_t q0 = (kt * 4 + w) * (int64_t)g.kz;
-      if (q0 >= g.nzl) continue;  // wave-uniform
-      const int64_t q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
-      int64_t xr[RB];
+      const int q0 = (kt * 4 + w) * kz;
+      if (q0 >= nzl) continue;  // wave-uniform
+      const int q1 = q0 + kz < nzl ? q0 + kz : nzl;
+      int xr[RB];
       S prev[RB], cur[RB];
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         xr[r] = it * 64 * RB + 64 * r + lane;
         const bool ld = xr[r] < nx;
-        prev[r] = (ld && g.z0 + q0 > 0) ? V[(q0 - 1) * P + xr[r]] : zero<S>();
+        prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + xr[r]] : zero<S>();
         cur[r] = ld ? V[q0 * P + xr[r]] : zero<S>();
       }
-      for (int64_t q = q0; q < q1; ++q) {
-        const int64_t gq = g.z0 + q;
-        const bool bz = gq == 0 || gq == g.npl - 1;
-        const bool has_next = gq + 1 < g.npl;
+      for (int q = q0; q < q1; ++q) {
+        const int gq = z0 + q;
+        const bool bz = gq == 0 || gq == npl - 1;
+        const bool has_next = gq + 1 < npl;
         S next[RB];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
           next[r] = (xr[r] < nx && has_next) ? V[(q + 1) * P + xr[r]] : zero<S>();
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
-          const int64_t x = xr[r];
-          const int64_t p = q * P + x;
+          const int x = xr[r];
+          const int p = q * P + x;
           S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
           const S cm = bcast(cur[r > 0 ? r - 1 : 0], 63);
           const S cp = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
-          if (lane == 0) xm = r > 0 ? cm : ((x < nx && x > 0) ? V[p - 1] : zero<S>());
-          if (lane == 63) xp = r + 1 < RB ? cp : ((x + 1 < nx) ? V[p + 1] : zero<S>());
+          const bool edge_ld = (lane == 0 && r == 0 && x < nx && x > 0) ||
+                               (lane == 63 && r + 1 == RB && x + 1 < nx);
+          const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
+          if (lane == 0) xm = r > 0 ? cm : xe;
+          if (lane == 63) xp = r + 1 < RB ? cp : xe;
           if (!(x > 0)) xm = zero<S>();
           if (!(x + 1 < nx)) xp = zero<S>();
           const bool bnd = x == 0 || x == nx - 1 || bz;
@@ -232,13 +241,11 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
   }
 }
 
-// rows (3D) / x-chunks (2D) per thread: more independent columns per thread
-// for the light kernels, fewer for the register-heavy high-J updates.
 #ifndef NLS_UPD_RB_MODE
 #define NLS_UPD_RB_MODE 0
 #endif
 #ifndef NLS_COEF_LDS
-#define NLS_COEF_LDS 0
+#define NLS_COEF_LDS 1
 #endif
 __host__ __device__ constexpr int upd_rb(int J) {
   return NLS_UPD_RB_MODE == 0 ? (J <= 2 ? 4 : (J <= 6 ? 2 : 1))
@@ -252,7 +259,7 @@ constexpr int RB_ALPHA = 4;
 // y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
 template <class S, int DIM>
 __global__ __launch_bounds__(NTHREADS) void k_lap(const S *__restrict__ V, Geo g, S *__restrict__ out) {
-  march<S, DIM, RB_ALPHA>(V, g, [&](int64_t p, const S &, const S &lap) { out[p] = lap; });
+  march<S, DIM, RB_ALPHA>(V, g, [&](int p, const S &, const S &lap) { out[p] = lap; });
 }
 
 // a = V^H L V and ||V||^2 per workgroup, in the symmetric forward-edge form
@@ -389,25 +396,34 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
 #pragma unroll
   for (int k = 0; k < NA; ++k) acc[k] = zero<S>();
 #if NLS_COEF_LDS
-  // coefficients broadcast from LDS at every use: keeps ~4(J+1) SGPRs free
+  // Coefficients broadcast from LDS at every use (ds_read_b128, one address per
+  // wave): keeps 4(J+1) SGPRs free, which otherwise spill to VGPR lanes and cost
+  // ~90 v_readlane per cell row in the hot loop.  The empty asm with a memory
+  // clobber stops the compiler from hoisting the LDS reads back into registers.
   __shared__ cplx cfs[MMAX + 2];
   for (int k = threadIdx.x; k <= J + 1; k += NTHREADS) cfs[k] = st->coef[k];
   __syncthreads();
-  volatile cplx *b = cfs;
   const double a = cfs[J + 1].re;
-#define NLS_B(k) cplx{b[k].re, b[k].im}
+#define NLS_B(k) cfs[k]
+#define NLS_RELOAD() asm volatile("" ::: "memory")
 #else
   cplx b[J + 1];
 #pragma unroll
   for (int k = 0; k <= J; ++k) b[k] = st->coef[k];
   const double a = st->coef[J + 1].re;
 #define NLS_B(k) b[k]
+#define NLS_RELOAD() ((void)0)
 #endif
   const S *__restrict__ VJ = W + (int64_t)J * vs;
-  march<S, DIM, UpdRB<J>::v>(VJ, g, [&](int64_t p, const S &cur, const S &lap) {
+  march<S, DIM, UpdRB<J>::v>(VJ, g, [&](int p, const S &cur, const S &lap) {
     S wk[J > 0 ? J : 1];
+    const S *__restrict__ src = W + p;
 #pragma unroll
-    for (int k = 0; k < J; ++k) wk[k] = ld_nt(W + (int64_t)k * vs + p);
+    for (int k = 0; k < J; ++k) {
+      wk[k] = ld_nt(src);
+      src += vs;
+    }
+    NLS_RELOAD();
     S X = a * lap - coef_mul(NLS_B(J), cur);
 #pragma unroll
     for (int k = 0; k < J; ++k) X = X - coef_mul(NLS_B(k), wk[k]);
@@ -422,6 +438,7 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
   for (int k = 0; k < NA; ++k) v[k] = to_c(acc[k]);
   block_store<NA>(v, part);
 #undef NLS_B
+#undef NLS_RELOAD
 }
 
 // host-side mirror of the tiling, for grid sizes
