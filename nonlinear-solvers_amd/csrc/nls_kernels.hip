@@ -120,7 +120,11 @@ template <int DIM, int RB> __host__ __device__ inline void tile_counts(const Geo
 // Local indices are 32-bit (the host guarantees (nzl+2)*P < 2^31); the flat
 // range tests of the reference (idx-nx >= 0, idx+nx < N) are evaluated on
 // (plane, row) coordinates so they never need 64-bit global indices.
-template <class S, int DIM, int RB, class Fn>
+//
+// PLANE = true: fn(p[RB], cur[RB], lap[RB], ok[RB]) is called once per plane
+// with all rows of the thread, so the caller can issue every streamed load of
+// all its rows before the first use (more loads in flight per accumulator set).
+template <class S, int DIM, int RB, bool PLANE = false, class Fn>
 __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn &&fn) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int64_t ntx64, nty64, ntz64;
@@ -160,12 +164,17 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
         const int gq = z0 + q;
         const bool bz = gq == 0 || gq == npl - 1;
         const bool has_next = gq + 1 < npl;
-        S next[RB];
+        S next[RB], lapv[RB];
+        int pv[RB];
+        bool okv[RB];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
           next[r] = (xin && rv[r] && has_next) ? V[(q + 1) * P + off[r]] : zero<S>();
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
+          pv[r] = q * P + off[r];
+          okv[r] = false;
+          lapv[r] = zero<S>();
           if (!rv[r]) continue;  // wave-uniform
           const int p = q * P + off[r];
           const int y = yb + r;
@@ -184,8 +193,14 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
           const bool bnd = bx || bz || y == 0 || y == nyp - 1;
           const S lap = g.s * (((prev[r] + next[r]) + (xm + xp)) + (ym + yp)) +
                         (bnd ? g.sd_bd : g.sd_in) * cur[r];
-          if (xin) fn(p, cur[r], lap);
+          if constexpr (PLANE) {
+            okv[r] = xin;
+            lapv[r] = lap;
+          } else {
+            if (xin) fn(p, cur[r], lap);
+          }
         }
+        if constexpr (PLANE) fn(pv, cur, lapv, okv);
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           prev[r] = cur[r];
@@ -209,7 +224,9 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
         const int gq = z0 + q;
         const bool bz = gq == 0 || gq == npl - 1;
         const bool has_next = gq + 1 < npl;
-        S next[RB];
+        S next[RB], lapv[RB];
+        int pv[RB];
+        bool okv[RB];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
           next[r] = (xr[r] < nx && has_next) ? V[(q + 1) * P + xr[r]] : zero<S>();
@@ -217,6 +234,7 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
         for (int r = 0; r < RB; ++r) {
           const int x = xr[r];
           const int p = q * P + x;
+          pv[r] = p;
           S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
           const S cm = bcast(cur[r > 0 ? r - 1 : 0], 63);
           const S cp = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
@@ -229,8 +247,14 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
           if (!(x + 1 < nx)) xp = zero<S>();
           const bool bnd = x == 0 || x == nx - 1 || bz;
           const S lap = g.s * ((prev[r] + next[r]) + (xm + xp)) + (bnd ? g.sd_bd : g.sd_in) * cur[r];
-          if (x < nx) fn(p, cur[r], lap);
+          if constexpr (PLANE) {
+            okv[r] = x < nx;
+            lapv[r] = lap;
+          } else {
+            if (x < nx) fn(p, cur[r], lap);
+          }
         }
+        if constexpr (PLANE) fn(pv, cur, lapv, okv);
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           prev[r] = cur[r];
@@ -242,7 +266,7 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
 }
 
 #ifndef NLS_UPD_RB_MODE
-#define NLS_UPD_RB_MODE 0
+#define NLS_UPD_RB_MODE 1
 #endif
 #ifndef NLS_COEF_LDS
 #define NLS_COEF_LDS 1
@@ -415,23 +439,33 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
 #define NLS_RELOAD() ((void)0)
 #endif
   const S *__restrict__ VJ = W + (int64_t)J * vs;
-  march<S, DIM, UpdRB<J>::v>(VJ, g, [&](int p, const S &cur, const S &lap) {
-    S wk[J > 0 ? J : 1];
-    const S *__restrict__ src = W + p;
+  constexpr int RB = UpdRB<J>::v;
+  march<S, DIM, RB, true>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
+    // every streamed load of every row first ...
+    S wk[RB][J > 0 ? J : 1];
 #pragma unroll
-    for (int k = 0; k < J; ++k) {
-      wk[k] = ld_nt(src);
-      src += vs;
+    for (int r = 0; r < RB; ++r) {
+      const S *__restrict__ src = W + p[r];
+#pragma unroll
+      for (int k = 0; k < J; ++k) {
+        wk[r][k] = ok[r] ? ld_nt(src) : zero<S>();
+        src += vs;
+      }
     }
     NLS_RELOAD();
-    S X = a * lap - coef_mul(NLS_B(J), cur);
+    // ... then the CGS update, the store and the Gram / norm partial sums
 #pragma unroll
-    for (int k = 0; k < J; ++k) X = X - coef_mul(NLS_B(k), wk[k]);
-    st_nt(out + p, X);
+    for (int r = 0; r < RB; ++r) {
+      if (!ok[r]) continue;
+      S X = a * lap[r] - coef_mul(NLS_B(J), cur[r]);
 #pragma unroll
-    for (int k = 0; k < J; ++k) acc[k] = acc[k] + cj_mul(wk[k], X);
-    acc[J] = acc[J] + cj_mul(cur, X);
-    acc[J + 1] = acc[J + 1] + from_real<S>(abs2(X));
+      for (int k = 0; k < J; ++k) X = X - coef_mul(NLS_B(k), wk[r][k]);
+      st_nt(out + p[r], X);
+#pragma unroll
+      for (int k = 0; k < J; ++k) acc[k] = acc[k] + cj_mul(wk[r][k], X);
+      acc[J] = acc[J] + cj_mul(cur[r], X);
+      acc[J + 1] = acc[J + 1] + from_real<S>(abs2(X));
+    }
   });
   cplx v[NA];
 #pragma unroll
@@ -511,37 +545,53 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_iter(KState *__restrict__ s
     for (int v = threadIdx.x; v < ncols; v += NTHREADS) ssum[v] = st->sums[v];
     __syncthreads();
   }
-  if (!do_coef || threadIdx.x != 0) return;
-  double sj;
-  if (j == 0) {
-    sj = sqrt(ssum[1].re);
-    st->s[0] = sj;
-    st->G[0][0] = {sj > 0.0 ? 1.0 : 0.0, 0.0};
-    st->breakdown = sj > 0.0 ? 0 : 1;
-  } else {
-    sj = sqrt(ssum[2 + j].re);
-    st->s[j] = sj;
-    st->To[j - 1] = sj;
-    const double isj = inv_or_zero(sj);
-    for (int k = 0; k < j; ++k) {
-      const double f = inv_or_zero(st->s[k]) * isj;
-      st->G[j][k] = f * ssum[2 + k];
-    }
-    st->G[j][j] = {sj > 0.0 ? 1.0 : 0.0, 0.0};
-    if (!(sj > 0.0) && st->breakdown == 0) st->breakdown = j + 1;
+  if (!do_coef) return;
+  // Coefficient math, parallel over k: the previous Hessenberg columns, norms
+  // and the new Gram column are staged in LDS (one coalesced read of the state)
+  // instead of a serial chain of dependent global loads.
+  __shared__ double s_s[MMAX + 1];
+  __shared__ cplx s_G[MMAX];
+  __shared__ cplx s_H[MMAX][MMAX];
+  const int t = threadIdx.x;
+  for (int k = t; k < j; k += NTHREADS) s_s[k] = st->s[k];
+  for (int e = t; e < j * MMAX; e += NTHREADS) {
+    const int k = e / MMAX, l = e % MMAX;
+    if (l <= k) s_H[k][l] = st->H[k][l];
   }
+  const double sj = sqrt(j == 0 ? ssum[1].re : ssum[2 + j].re);
   const double isj = inv_or_zero(sj);
+  if (t == 0) s_s[j] = sj;
+  __syncthreads();
+  for (int k = t; k < j; k += NTHREADS) s_G[k] = (inv_or_zero(s_s[k]) * isj) * ssum[2 + k];
+  if (t == 0) s_G[j] = {sj > 0.0 ? 1.0 : 0.0, 0.0};
+  __syncthreads();
   const cplx alpha = (isj * isj) * ssum[0];
-  st->Td[j] = alpha.re;
-  st->H[j][j] = alpha;
-  for (int k = 0; k < j; ++k) {
-    cplx acc = {0.0, 0.0};
-    for (int l = 0; l <= k; ++l) acc += cmul(cconj(st->H[k][l]), st->G[j][l]);
-    acc += st->s[k + 1] * st->G[j][k + 1];
-    st->H[j][k] = acc;
+  for (int k = t; k <= j; k += NTHREADS) {
+    cplx h;
+    if (k == j) {
+      h = alpha;
+    } else {
+      //   H[j][k] = sum_{l<=k} conj(H[k][l]) G[j][l] + s_{k+1} G[j][k+1]
+      cplx acc = {0.0, 0.0};
+      for (int l = 0; l <= k; ++l) acc += cmul(cconj(s_H[k][l]), s_G[l]);
+      acc += s_s[k + 1] * s_G[k + 1];
+      h = acc;
+    }
+    st->H[j][k] = h;
+    st->G[j][k] = s_G[k];
+    st->coef[k] = inv_or_zero(s_s[k]) * h;
   }
-  for (int k = 0; k <= j; ++k) st->coef[k] = inv_or_zero(st->s[k]) * st->H[j][k];
-  st->coef[j + 1] = {isj, 0.0};
+  if (t == 0) {
+    st->s[j] = sj;
+    st->Td[j] = alpha.re;
+    st->coef[j + 1] = {isj, 0.0};
+    if (j == 0) {
+      st->breakdown = sj > 0.0 ? 0 : 1;
+    } else {
+      st->To[j - 1] = sj;
+      if (!(sj > 0.0) && st->breakdown == 0) st->breakdown = j + 1;
+    }
+  }
 }
 
 __device__ __forceinline__ double sinc_ref(double x) {  // eigen_krylov_real.hpp:95-97
@@ -614,62 +664,69 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_final(KState *__restrict__ 
   if (threadIdx.x < 64) eigen_phase(st, m, nf, f0, f1, t_re, t_im);
 }
 
-// Wave-0 part of k_reduce_final (no workgroup barriers inside: one wave's LDS
-// accesses complete in program order).
+// Wave-0 part of k_reduce_final.  Lane k holds d[k] and e[k] in registers; the
+// implicit-shift QL recurrence (uniform across lanes) reads them with
+// v_readlane and writes them back with a lane-select, so its dependency chain
+// never waits on LDS.  Lane r applies every Givens rotation to row r of Q (LDS).
+__device__ __forceinline__ double rdlane(double v, int i) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), i);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), i);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf, int f0, int f1,
                                          double t_re, double t_im) {
-  __shared__ double d[MMAX], e[MMAX], Q[MMAX][MMAX + 1];
+  __shared__ double Q[MMAX][MMAX + 1];
   const int lane = threadIdx.x;
-  // scale T to max|entry| = 1 (Eigen's SelfAdjointEigenSolver scales the same
-  // way); rotations then use sqrt(f^2 + g^2) without overflow risk.
-  double scl = 0.0;
-  for (int k = 0; k < m; ++k) {
-    scl = fmax(scl, fabs(st->Td[k]));
-    if (k < m - 1) scl = fmax(scl, fabs(st->To[k]));
-  }
+  // scale T to max|entry| = 1 (as Eigen's SelfAdjointEigenSolver does)
+  double dl = lane < m ? st->Td[lane] : 0.0;
+  double el = lane < m - 1 ? st->To[lane] : 0.0;
+  double scl = fmax(fabs(dl), fabs(el));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) scl = fmax(scl, __shfl_xor(scl, off, 64));
   const double iscl = scl > 0.0 ? 1.0 / scl : 1.0;
   if (scl == 0.0) scl = 1.0;
-  if (lane < m) {
-    d[lane] = st->Td[lane] * iscl;
-    e[lane] = lane < m - 1 ? st->To[lane] * iscl : 0.0;
+  dl *= iscl;
+  el *= iscl;
+  if (lane < m)
     for (int c = 0; c < m; ++c) Q[lane][c] = lane == c ? 1.0 : 0.0;
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  // implicit-shift QL on the symmetric tridiagonal (d, e); every lane runs the
-  // scalar recurrence redundantly, lane r applies the rotations to row r.
+  auto setd = [&](int i, double v) { if (lane == i) dl = v; };
+  auto sete = [&](int i, double v) { if (lane == i) el = v; };
   for (int l = 0; l < m; ++l) {
     int iter = 0;
     for (;;) {
       int mm;
       for (mm = l; mm < m - 1; ++mm) {
-        const double dd = fabs(d[mm]) + fabs(d[mm + 1]);
-        if (fabs(e[mm]) <= 2.220446049250313e-16 * dd) break;
+        const double dd = fabs(rdlane(dl, mm)) + fabs(rdlane(dl, mm + 1));
+        if (fabs(rdlane(el, mm)) <= 2.220446049250313e-16 * dd) break;
       }
       if (mm == l) break;
       if (++iter > 64) break;
-      double gg = (d[l + 1] - d[l]) / (2.0 * e[l]);
+      const double dlv = rdlane(dl, l), el_l = rdlane(el, l);
+      double gg = (rdlane(dl, l + 1) - dlv) / (2.0 * el_l);
       double rr = hypot(gg, 1.0);
-      gg = d[mm] - d[l] + e[l] / (gg + (gg >= 0.0 ? fabs(rr) : -fabs(rr)));
+      gg = rdlane(dl, mm) - dlv + el_l / (gg + (gg >= 0.0 ? fabs(rr) : -fabs(rr)));
       double ss = 1.0, cc = 1.0, pp = 0.0;
       bool early = false;
       for (int i = mm - 1; i >= l; --i) {
-        const double ff = ss * e[i], bb = cc * e[i];
+        const double ei = rdlane(el, i);
+        const double ff = ss * ei, bb = cc * ei;
         rr = sqrt(ff * ff + gg * gg);
-        e[i + 1] = rr;
+        sete(i + 1, rr);
         if (rr == 0.0) {
-          d[i + 1] -= pp;
-          e[mm] = 0.0;
+          setd(i + 1, rdlane(dl, i + 1) - pp);
+          sete(mm, 0.0);
           early = true;
           break;
         }
         const double irr = 1.0 / rr;
         ss = ff * irr;
         cc = gg * irr;
-        gg = d[i + 1] - pp;
-        rr = (d[i] - gg) * ss + 2.0 * cc * bb;
+        gg = rdlane(dl, i + 1) - pp;
+        rr = (rdlane(dl, i) - gg) * ss + 2.0 * cc * bb;
         pp = ss * rr;
-        d[i + 1] = gg + pp;
+        setd(i + 1, gg + pp);
         gg = cc * rr - bb;
         if (lane < m) {
           const double fq = Q[lane][i + 1];
@@ -678,22 +735,21 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
         }
       }
       if (early) continue;
-      d[l] -= pp;
-      e[l] = gg;
-      e[mm] = 0.0;
+      setd(l, rdlane(dl, l) - pp);
+      sete(l, gg);
+      sete(mm, 0.0);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  if (lane < m) d[lane] *= scl;
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const double lam_l = dl * scl;
   if (lane < m) {
-    st->lam[lane] = d[lane];
+    st->lam[lane] = lam_l;
     const double s0 = st->s[0];
     const double isr = inv_or_zero(st->s[lane]);
     for (int fi = 0; fi < nf; ++fi) {
       const int func = fi == 0 ? f0 : f1;
       cplx c = {0.0, 0.0};
-      for (int k = 0; k < m; ++k) c += (Q[lane][k] * Q[0][k]) * eval_f(func, d[k], t_re, t_im);
+      for (int k = 0; k < m; ++k) c += (Q[lane][k] * Q[0][k]) * eval_f(func, rdlane(lam_l, k), t_re, t_im);
       st->fin[fi][lane] = (s0 * isr) * c;
     }
   }
@@ -736,17 +792,37 @@ __global__ __launch_bounds__(NTHREADS) void k_final_nlse(cplx *__restrict__ W, i
                                                          const KState *__restrict__ st,
                                                          cplx *__restrict__ u, double dt,
                                                          int nonlin, cplx s1, cplx s2) {
-  cplx c[M];
+  // two cells per thread, all 2M basis loads issued before the first use;
+  // combination coefficients broadcast from LDS
+  constexpr int U = 2;
+  __shared__ cplx cf[MMAX];
+  for (int k = threadIdx.x; k < M; k += NTHREADS) cf[k] = st->fin[0][k];
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * NTHREADS * U;
+  for (int64_t base = (int64_t)blockIdx.x * NTHREADS * U + threadIdx.x; base < n; base += stride) {
+    cplx w[U][M];
 #pragma unroll
-  for (int k = 0; k < M; ++k) c[k] = st->fin[0][k];
-  for (int64_t p = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; p < n;
-       p += (int64_t)gridDim.x * NTHREADS) {
-    cplx y = {0.0, 0.0};
+    for (int q = 0; q < U; ++q) {
+      const int64_t p = base + q * NTHREADS;
+      const cplx *__restrict__ src = W + p;
 #pragma unroll
-    for (int k = 0; k < M; ++k) y += cmul(c[k], ld_nt(W + (int64_t)k * vs + p));
-    const cplx un = nl_half(y, dt, nonlin, s1, s2);
-    u[p] = un;
-    W[p] = nl_half(un, dt, nonlin, s1, s2);
+      for (int k = 0; k < M; ++k) {
+        w[q][k] = p < n ? ld_nt(src) : cplx{0.0, 0.0};
+        src += vs;
+      }
+    }
+    asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int64_t p = base + q * NTHREADS;
+      if (p >= n) continue;
+      cplx y = {0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < M; ++k) y += cmul(cf[k], w[q][k]);
+      const cplx un = nl_half(y, dt, nonlin, s1, s2);
+      st_nt(u + p, un);
+      st_nt(W + p, nl_half(un, dt, nonlin, s1, s2));
+    }
   }
 }
 
@@ -787,12 +863,12 @@ __global__ __launch_bounds__(NTHREADS) void k_sg_mid(const double *__restrict__ 
     double yi = 0.0, yc = 0.0;
 #pragma unroll
     for (int k = 0; k < M; ++k) {
-      const double w = W[(int64_t)k * vs + p];
+      const double w = ld_nt(W + (int64_t)k * vs + p);
       yi += ci[k] * w;
       yc += cc[k] * w;
     }
-    g0[p] = mf[p] * (-sin(yi));
-    up[p] = 2 * yc - up[p];
+    st_nt(g0 + p, mf[p] * (-sin(yi)));
+    st_nt(up + p, 2 * yc - up[p]);
   }
 }
 
@@ -809,7 +885,7 @@ __global__ __launch_bounds__(NTHREADS) void k_sg_end(const double *__restrict__ 
        p += (int64_t)gridDim.x * NTHREADS) {
     double ys = 0.0;
 #pragma unroll
-    for (int k = 0; k < M; ++k) ys += c[k] * W2[(int64_t)k * vs + p];
+    for (int k = 0; k < M; ++k) ys += c[k] * ld_nt(W2 + (int64_t)k * vs + p);
     const double uo = u[p];
     u[p] = up[p] + (dt * dt) * ys;
     up[p] = uo;
