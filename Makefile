@@ -11,15 +11,22 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wal
 LDFLAGS  := -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 LIB      := $(LIBDIR)/libnls_amd.so
-OBJS     := $(BUILD)/nls_kernels.o $(BUILD)/nls_api.o
+STENCIL  := iso2 iso3 ani2 ani3
+OBJS     := $(BUILD)/nls_kernels.o $(BUILD)/nls_api.o $(STENCIL:%=$(BUILD)/nls_stencil_%.o)
+DEVHDR   := $(CSRC)/nls_device.hpp $(CSRC)/nls_kernels.hpp $(CSRC)/nls_stencil.hpp
 
 all: $(LIB) drivers oracle
 
 $(BUILD) $(LIBDIR) $(BINDIR):
 	mkdir -p $@
 
-$(BUILD)/nls_kernels.o: $(CSRC)/nls_kernels.hip $(CSRC)/nls_device.hpp $(CSRC)/nls_kernels.hpp | $(BUILD)
+$(BUILD)/nls_kernels.o: $(CSRC)/nls_kernels.hip $(DEVHDR) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the stencil tables, one object per operator variant x dimension (parallel build)
+$(BUILD)/nls_stencil_%.o: $(CSRC)/nls_stencil.hip $(DEVHDR) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DNLS_ANI=$(if $(findstring ani,$*),1,0) -DNLS_DIM=$(subst ani,,$(subst iso,,$*)) \
+	  -DNLS_TABLE=stencil_table_$* -c $< -o $@
 
 $(BUILD)/nls_api.o: $(CSRC)/nls_api.cpp $(CSRC)/nls_device.hpp $(CSRC)/nls_kernels.hpp include/nls.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@

@@ -16,8 +16,13 @@
  *                       (the operator is described by grid parameters, not by a CSR matrix)
  *   nls_set_field    <- cudaMemcpy H2D of host_u0 in the ctors above       device/nlse_solver_dev.hpp:63-64
  *   nls_set_sg_state <- SGESolverDevice ctor u0/u_past/m uploads           device/sg_solver_dev.hpp:118-135
+ *   nls_set_coefficients <- NLSESolverDevice(L, u0, m, ...) (G2) m upload  nlsolvers/device/include/nlse_dev.hpp:66-130
+ *                       build_anisotropic_laplacian_noflux{,_3d}(.., c)   nlsolvers/common/include/laplacians.hpp:54-103,158-218
+ *   nls_apply_bc     <- NLSESolverDevice::apply_bc() (G2)                  nlsolvers/device/include/nlse_dev.hpp:178-185,
+ *                       neumann_bc_no_velocity_blocking{,_3d}             nlsolvers/device/include/boundaries.cuh:10-81
  *   nls_step         <- NLSESolverDevice::step(tau=1j*dt, i)               device/nlse_solver_dev.hpp:94-111
  *                       SGESolverDevice::step(tau=dt, i)                   device/sg_solver_dev.hpp:168-193
+ *                       G2 NLSESolverDevice::step(tau=1j*dt, i)            nlsolvers/device/include/nlse_dev.hpp:187-203
  *   nls_get_field    <- transfer_snapshots(dst) / store_snapshot D2D+D2H   device/nlse_solver_dev.hpp:113-124
  *   nls_get_sg_velocity <- transfer_snapshots(dst, 'v')                    device/sg_solver_dev.hpp:195-222
  *   nls_krylov_apply <- MatrixFunctionApplicator{Complex,Real}::apply(out, in, t[, type])
@@ -63,7 +68,11 @@ enum nls_status {
 enum nls_equation {
   NLS_NLSE_CUBIC = 0,   /* i u_t + Lap u + |u|^2 u = 0, SS2 (nlse_solver.hpp:53-77) */
   NLS_NLSE_CQ = 1,      /* rho = s1|u|^2 + s2|u|^4 (device/nlse_cq_solver.hpp:16-39) */
-  NLS_SG_GAUTSCHI = 2   /* u_tt = Lap u + m sin u, Gautschi (sg_solver.hpp:53-74) */
+  NLS_SG_GAUTSCHI = 2,  /* u_tt = Lap u + m sin u, Gautschi (sg_solver.hpp:53-74) */
+  NLS_NLSE_G2 = 3       /* G2 cubic NLSE with focusing field m(x) and anisotropic operator
+                           div(c grad): SS2 with exp(+tau/2 m|u|^2) and exp(tau*lambda)
+                           (nlsolvers/device/include/nlse_dev.hpp:187-203,
+                           nlsolvers/device/drivers/nlse_cubic_driver_{2d,3d}.cpp) */
 };
 
 /* Krylov matrix functions f, applied as f(L) u (nls_krylov_apply) */
@@ -106,11 +115,25 @@ const char *nls_last_error(const nls_handle *h); /* h == NULL: last nls_create e
  * (3D: z, 2D: y); n_local = nzl * plane size. */
 int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t *n_local);
 
-/* NLSE: u (complex interleaved, 2*n_local doubles).  SG: u (n_local doubles). */
+/* NLSE: u (complex interleaved, 2*n_local doubles).  SG: u (n_local doubles).
+ * (The G2 drivers do not normalise u0, nlse_cubic_driver_3d.cpp:54-65; the G1
+ * drivers do, nlse_call.cpp:41-49 -- the caller decides.) */
 int nls_set_field(nls_handle *h, const double *u, uint64_t n_local);
 /* SG only: u, u_past = u0 - dt*v0 (sg_driver_dev.cpp:64,106) and the m(x) field. */
 int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past,
                      const double *mfield, uint64_t n_local);
+
+/* G2 only (NLS_NLSE_G2): the focusing field m(x) and the anisotropy c(x) of the
+ * operator div(c grad u) (face weights (c_a + c_b)/2, diagonal -sum of weights,
+ * scale 1/(dx*dy) in 2D and 1/(dx*dx) in 3D), both real, local slab.  Must be
+ * called before the first nls_step. */
+int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfield,
+                         uint64_t n_local);
+/* Neumann "copy" boundary condition of the G2 drivers, applied after every step
+ * (boundaries.cuh:10-81): every boundary cell takes the value of the cell with
+ * all coordinates clamped into [1, n-2].  Complex (NLSE) handles; needs >= 3
+ * cells per dimension.  Like nls_step it is enqueued asynchronously. */
+int nls_apply_bc(nls_handle *h);
 
 /* Enqueue nsteps time steps (NLSE: tau = 1j*dt; SG: tau = dt) on the handle's
  * stream and return.  Errors of asynchronous execution surface at nls_sync /

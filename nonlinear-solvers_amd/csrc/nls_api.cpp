@@ -77,12 +77,16 @@ struct nls_handle {
   Basis B[2];
   void *u = nullptr;        // NLSE state u (nloc complex)
   double *up = nullptr;     // SG u_past
-  double *mf = nullptr;     // SG m(x)
+  double *mf = nullptr;     // SG m(x), G2 NLSE focusing field m(x)
+  double *cfb = nullptr;    // G2 anisotropy c(x): (nzl + 2) planes, local plane 0 at +P
+  bool ani = false;         // G2 operator div(c grad) (laplacians.hpp:54-218)
+  bool coef_set = false;
   void *scratch = nullptr;  // nloc elements
   cplx *partA = nullptr, *partU = nullptr;
   int grid_alpha = 1, grid_lap = 1, grid_pw = 1;
   int grid_update[MMAX] = {};
   bool field_set = false, w0_ready = false;
+  double w0_dt = 0.0;  // dt the live start vector W_0 = N(u) was built with
   int nonlin = 0;
   cplx s1{0.0, 0.5}, s2{-0.5, 0.0};
   std::string err;
@@ -234,14 +238,13 @@ void halo_local(nls_handle *h, char *first, char *last, char *gbelow, char *gabo
   }
 }
 
-// Exchange the boundary planes of vector k of basis b into the neighbours'
-// ghost planes (z-slab decomposition; one plane covers the 3D y-wrap too).
-void halo(nls_handle *h, int b, int k) {
+// Exchange the boundary planes of a slab-stored array (local plane 0 at v,
+// ghost planes at -P and nzl*P) into the neighbours' ghost planes (z-slab
+// decomposition; one plane covers the 3D y-wrap too).
+void halo_planes(nls_handle *h, char *v, int64_t es) {
   if (!h->collective) return;
   const int64_t P = h->geo.P;
-  const size_t cnt = (size_t)P * (h->cplx_ ? 2 : 1);
-  char *v = vec_ptr(h, b, k);
-  const int64_t es = (int64_t)h->esize;
+  const size_t cnt = (size_t)P * (size_t)(es / 8);
   char *first = v, *last = v + (h->geo.nzl - 1) * P * es;
   char *gbelow = v - P * es, *gabove = v + h->geo.nzl * P * es;
   TimingRec rec{4, -1, nullptr, nullptr};
@@ -251,7 +254,7 @@ void halo(nls_handle *h, int b, int k) {
     hip_check(h, hipEventRecord(rec.a, h->stream), "hipEventRecord");
   }
   if (h->group) {
-    halo_local(h, first, last, gbelow, gabove, (size_t)P * h->esize);
+    halo_local(h, first, last, gbelow, gabove, (size_t)P * es);
     if (h->timing) {
       hip_check(h, hipEventRecord(rec.b, h->stream), "hipEventRecord");
       h->recs.push_back(rec);
@@ -273,6 +276,9 @@ void halo(nls_handle *h, int b, int k) {
     h->recs.push_back(rec);
   }
 }
+
+// vector k of basis b
+void halo(nls_handle *h, int b, int k) { halo_planes(h, vec_ptr(h, b, k), (int64_t)h->esize); }
 
 void allreduce_sums(nls_handle *h, int b, int ncplx) {
   void *p = &h->B[b].st->sums[0];
@@ -356,7 +362,7 @@ void reduce_final(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
 void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
   const int m = h->m;
   Geo g = h->geo;
-  const void *fa = kernel_alpha(h->cplx_, (int)h->cfg.dim);
+  const void *fa = kernel_alpha(h->cplx_, (int)h->cfg.dim, h->ani);
   {
     void *v0 = vec_ptr(h, b, 0);
     void *args[] = {&v0, &g, &h->partA};
@@ -375,7 +381,7 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
       reduce_iter(h, b, j);
     }
     void *args[] = {&W, &out, &vs, &g, &st, &h->partU};
-    launch(h, 1, j, kernel_update(h->cplx_, (int)h->cfg.dim, j), h->grid_update[j], args);
+    launch(h, 1, j, kernel_update(h->cplx_, (int)h->cfg.dim, j, h->ani), h->grid_update[j], args);
     if (j + 1 <= m - 2) halo(h, b, j + 1);
   }
   reduce_final(h, b, nf, f0, f1, tr, ti);
@@ -441,6 +447,13 @@ void alloc_all(nls_handle *h) {
   const size_t nbytes = (size_t)g.nloc * h->esize;
   if (h->cplx_) {
     hip_check(h, hipMalloc(&h->u, nbytes), "hipMalloc(u)");
+    if (h->ani) {
+      const size_t cbytes = (size_t)(g.nzl + 2) * g.P * sizeof(double);
+      hip_check(h, hipMalloc(&h->mf, (size_t)g.nloc * sizeof(double)), "hipMalloc(m)");
+      hip_check(h, hipMalloc(&h->cfb, cbytes), "hipMalloc(c)");
+      hip_check(h, hipMemsetAsync(h->cfb, 0, cbytes, h->stream), "hipMemset");
+      h->geo.cf = h->cfb + g.P;
+    }
   } else {
     hip_check(h, hipMalloc(&h->up, nbytes), "hipMalloc(u_past)");
     hip_check(h, hipMalloc(&h->mf, nbytes), "hipMalloc(m)");
@@ -449,12 +462,13 @@ void alloc_all(nls_handle *h) {
   // grid sizes from measured occupancy; partial buffers sized for the largest
   const bool c = h->cplx_;
   const int dim = h->cfg.dim;
+  const bool ani = h->ani;
   const int64_t ta = stencil_tiles(g, dim, alpha_rows_per_thread());
-  h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim), ta);
-  h->grid_lap = occupancy_grid(h, kernel_lap(c, dim), ta);
+  h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim, ani), ta);
+  h->grid_lap = occupancy_grid(h, kernel_lap(c, dim, ani), ta);
   int64_t cap = 2 * (int64_t)h->grid_alpha;
   for (int j = 0; j + 1 < h->m; ++j) {
-    h->grid_update[j] = occupancy_grid(h, kernel_update(c, dim, j),
+    h->grid_update[j] = occupancy_grid(h, kernel_update(c, dim, j, ani),
                                        stencil_tiles(g, dim, update_rows_per_thread(j)));
     cap = std::max<int64_t>(cap, (int64_t)h->grid_update[j] * (j + 2));
   }
@@ -469,11 +483,11 @@ void free_all(nls_handle *h) {
     if (h->B[b].st) (void)hipFree(h->B[b].st);
     h->B[b] = Basis{};
   }
-  for (void *p : {h->u, (void *)h->up, (void *)h->mf, h->scratch, (void *)h->partA,
-                  (void *)h->partU})
+  for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch,
+                  (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
   h->u = h->scratch = nullptr;
-  h->up = h->mf = nullptr;
+  h->up = h->mf = h->cfb = nullptr;
   h->partA = h->partU = nullptr;
 }
 
@@ -526,7 +540,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   const nls_config &c = *cfg;
   std::string why;
   if (c.dim != 2 && c.dim != 3) why = "dim must be 2 or 3";
-  else if (c.equation < 0 || c.equation > 2) why = "unknown equation";
+  else if (c.equation < 0 || c.equation > 3) why = "unknown equation";
   else if (c.equation == NLS_SG_GAUTSCHI && c.dim != 2 && c.dim != 3) why = "bad dim";
   else if (c.nx < 2 || c.ny < 2 || (c.dim == 3 && c.nz < 2)) why = "grid too small (need >= 2 per dimension)";
   else if (!(c.dx > 0.0) || !(c.dy > 0.0)) why = "dx, dy must be > 0";
@@ -536,6 +550,10 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   else if (c.local_group && static_cast<nls_group *>(c.local_group)->n != c.nranks)
     why = "local_group size != nranks";
   else if ((uint32_t)c.nranks > (c.dim == 3 ? c.nz : c.ny)) why = "more ranks than planes";
+  else if (c.equation == NLS_NLSE_G2 && (c.nx < 3 || c.ny < 3 || (c.dim == 3 && c.nz < 3)))
+    why = "G2 NLSE needs >= 3 cells per dimension (Neumann copy boundary)";
+  else if (c.equation == NLS_NLSE_G2 && (uint32_t)(2 * c.nranks) > (c.dim == 3 ? c.nz : c.ny))
+    why = "G2 NLSE needs >= 2 planes per rank";
   if (!why.empty()) {
     g_create_error = why;
     return NLS_ERR_ARG;
@@ -550,7 +568,8 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   h->esize = h->cplx_ ? 16 : 8;
   h->m = (int)c.krylov_m;
   h->nbasis = h->cplx_ ? 1 : 2;
-  h->nonlin = c.equation == NLS_NLSE_CQ ? 1 : 0;
+  h->nonlin = c.equation == NLS_NLSE_CQ ? 1 : (c.equation == NLS_NLSE_G2 ? 2 : 0);
+  h->ani = c.equation == NLS_NLSE_G2;
   h->s1 = {c.sigma1[0], c.sigma1[1]};
   h->s2 = {c.sigma2[0], c.sigma2[1]};
   h->rank = c.rank;
@@ -666,9 +685,51 @@ int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past, const
   });
 }
 
+int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfield, uint64_t n) {
+  return guarded(h, [&] {
+    if (!h->ani) fail(h, NLS_ERR_STATE, "nls_set_coefficients on a non-G2 handle");
+    if (!mfield || !cfield) fail(h, NLS_ERR_ARG, "NULL input");
+    check_len(h, n);
+    const size_t bytes = (size_t)n * sizeof(double);
+    hip_check(h, hipMemcpyAsync(h->mf, mfield, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    hip_check(h, hipMemcpyAsync(h->cfb + h->geo.P, cfield, bytes, hipMemcpyHostToDevice, h->stream),
+              "H2D");
+    halo_planes(h, reinterpret_cast<char *>(h->cfb + h->geo.P), (int64_t)sizeof(double));
+    h->coef_set = true;
+    h->w0_ready = false;  // the start vector depends on m
+    hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+}
+
+int nls_apply_bc(nls_handle *h) {
+  return guarded(h, [&] {
+    if (!h->cplx_) fail(h, NLS_ERR_STATE, "nls_apply_bc on a sine-Gordon handle");
+    if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
+    const Geo &g = h->geo;
+    if (g.nx < 3 || g.npl < 3 || (h->cfg.dim == 3 && g.nyp < 3))
+      fail(h, NLS_ERR_ARG, "Neumann copy boundary needs >= 3 cells per dimension");
+    if ((g.z0 == 0 || g.z0 + g.nzl == g.npl) && g.nzl < 2)
+      fail(h, NLS_ERR_ARG, "Neumann copy boundary needs >= 2 planes on the boundary slabs");
+    // the start vector of the next step (N(u) with the last step's dt, kept
+    // from the final pass) is refreshed on the same boundary cells
+    const bool refresh = h->w0_ready;
+    double dt = h->w0_dt;
+    void *w0 = vec_ptr(h, 0, 0);
+    Geo gg = g;
+    int wr = refresh ? 1 : 0, nl = h->nonlin;
+    const int64_t cells = neumann_bc_cells(g);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((cells + NTHREADS - 1) / NTHREADS, 4096));
+    void *args[] = {&h->u, &w0, &h->mf, &gg, &wr, &dt, &nl, &h->s1, &h->s2};
+    launch(h, 3, -1, kernel_neumann_bc(), grid, args);
+    if (refresh) halo(h, 0, 0);
+    hip_check(h, hipGetLastError(), "kernel launch");
+  });
+}
+
 int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
   return guarded(h, [&] {
     if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
+    if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");
     const int m = h->m;
     const int64_t n = h->geo.nloc;
@@ -677,21 +738,26 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
       if (h->cplx_) {
         // NLSESolverDevice::step (device/nlse_solver_dev.hpp:94-111), tau = 1j*dt:
         //   N(1/2) -> exp(L*dt) via exp(t|lambda|), t = -tau -> N(1/2)
-        if (!h->w0_ready) {
+        // G2 (nlsolvers/device/include/nlse_dev.hpp:187-203): N uses +tau/2 m|u|^2
+        // and the linear flow is exp(t*lambda) with t = +tau
+        // (nlsolvers/device/include/matfunc_complex.hpp:281-287).
+        if (!h->w0_ready || h->w0_dt != dt) {
           void *w0 = vec_ptr(h, 0, 0);
           int nl = h->nonlin;
-          void *args[] = {&h->u, &w0, (void *)&n, &dt, &nl, &h->s1, &h->s2};
+          void *args[] = {&h->u, &w0, &h->mf, (void *)&n, &dt, &nl, &h->s1, &h->s2};
           pw_launch(h, 3, kernel_nl_init(), args);
           halo(h, 0, 0);
         }
-        run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt);
+        if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt);
+        else run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt);
         void *W = vec_ptr(h, 0, 0);
         KState *st = h->B[0].st;
         int nl = h->nonlin;
-        void *args[] = {&W, &vs, (void *)&n, &st, &h->u, &dt, &nl, &h->s1, &h->s2};
+        void *args[] = {&W, &vs, (void *)&n, &st, &h->u, &h->mf, &dt, &nl, &h->s1, &h->s2};
         pw_launch(h, 3, kernel_final_nlse(m), args);
         halo(h, 0, 0);
         h->w0_ready = true;
+        h->w0_dt = dt;
       } else {
         // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u
         run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0);
@@ -754,6 +820,7 @@ int nls_krylov_apply(nls_handle *h, const double *in, double t_re, double t_im, 
   return guarded(h, [&] {
     if (!in || !out) fail(h, NLS_ERR_ARG, "NULL buffer");
     if (func < 0 || func > 6) fail(h, NLS_ERR_ARG, "unknown func");
+    if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     check_len(h, n);
     const int b = h->cplx_ ? 0 : 1;  // SG: the scratch basis keeps u intact
     copy_in_vector(h, b, 0, in);
@@ -775,6 +842,7 @@ int nls_krylov_apply(nls_handle *h, const double *in, double t_re, double t_im, 
 int nls_laplacian_apply(nls_handle *h, const double *x, double *y, uint64_t n) {
   return guarded(h, [&] {
     if (!x || !y) fail(h, NLS_ERR_ARG, "NULL buffer");
+    if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     check_len(h, n);
     const int b = h->cplx_ ? 0 : 1;
     copy_in_vector(h, b, 0, x);
@@ -783,7 +851,7 @@ int nls_laplacian_apply(nls_handle *h, const double *x, double *y, uint64_t n) {
     void *v0 = vec_ptr(h, b, 0);
     Geo g = h->geo;
     void *args[] = {&v0, &g, &h->scratch};
-    launch(h, 0, -1, kernel_lap(h->cplx_, (int)h->cfg.dim), h->grid_lap, args);
+    launch(h, 0, -1, kernel_lap(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_lap, args);
     hip_check(h, hipMemcpyAsync(y, h->scratch, (size_t)n * h->esize, hipMemcpyDeviceToHost,
                                 h->stream),
               "hipMemcpy D2H");

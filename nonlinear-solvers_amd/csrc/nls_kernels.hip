@@ -14,466 +14,18 @@
 //                and reduces g_k = W_k^H W_{j+1} and ||W_{j+1}||^2
 //                                                        j+1 reads + 1 write
 // The stencil is the reference's assembled CSR restated matrix-free
-// (laplacians.hpp:10-105): per point, the column's z (3D) / y (2D)
+// (laplacians.hpp:10-105; G2 anisotropic nlsolvers/common/include/laplacians.hpp:54-218): per point, the column's z (3D) / y (2D)
 // neighbours come from a register queue while the workgroup marches along the
 // slowest dimension; x and (3D) y neighbours are neighbouring lanes' loads
 // served from L1/L2.  The 3D "y-wrap" (i,ny-1,k)<->(i,0,k+1) falls out of
 // flat-index neighbours p +- nx over contiguous plane storage.
-#include <utility>
-
-#include "nls_device.hpp"
+//
+// This file holds the reductions, the eigensolve and the pointwise kernels;
+// the stencil passes are in nls_stencil.hpp / nls_stencil.hip.
+#include "nls_stencil.hpp"
 #include "nls_kernels.hpp"
 
 namespace nls {
-
-template <class S> __device__ __forceinline__ S from_real(double v);
-template <> __device__ __forceinline__ double from_real<double>(double v) { return v; }
-template <> __device__ __forceinline__ cplx from_real<cplx>(double v) { return {v, 0.0}; }
-
-// ---------------------------------------------------------------------------
-// wave64 + workgroup reduction into one partial per workgroup (fixed order:
-// results are bitwise reproducible run to run)
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// partials are stored column-major: out[k * gridDim.x + blockIdx.x], so the
-// single-workgroup reduction reads each column with coalesced 1 KiB wave loads.
-template <int NA>
-__device__ __forceinline__ void block_store(cplx (&v)[NA], cplx *__restrict__ out) {
-  __shared__ cplx red[NTHREADS / 64][NA];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < NA; ++k) {
-    v[k].re = wave_sum(v[k].re);
-    v[k].im = wave_sum(v[k].im);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < NA; ++k) red[w][k] = v[k];
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < NA; k += NTHREADS) {
-    cplx s = red[0][k];
-#pragma unroll
-    for (int q = 1; q < NTHREADS / 64; ++q) s += red[q][k];
-    out[(int64_t)k * gridDim.x + blockIdx.x] = s;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// memory helpers: basis vectors streamed once per pass use non-temporal
-// loads/stores (measured +5-10 % on 16-stream passes, tools/bw_probe.hip);
-// the stencil vector keeps default policy (its neighbours are re-read).
-typedef double v2d __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ cplx ld_nt(const cplx *p) {
-  const v2d v = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p));
-  return {v.x, v.y};
-}
-__device__ __forceinline__ double ld_nt(const double *p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ void st_nt(cplx *p, cplx v) {
-  v2d t;
-  t.x = v.re;
-  t.y = v.im;
-  __builtin_nontemporal_store(t, reinterpret_cast<v2d *>(p));
-}
-__device__ __forceinline__ void st_nt(double *p, double v) { __builtin_nontemporal_store(v, p); }
-
-// wave64 cross-lane moves (ds_bpermute)
-__device__ __forceinline__ double shfl_up1(double v) { return __shfl_up(v, 1, 64); }
-__device__ __forceinline__ cplx shfl_up1(cplx v) { return {__shfl_up(v.re, 1, 64), __shfl_up(v.im, 1, 64)}; }
-__device__ __forceinline__ double shfl_dn1(double v) { return __shfl_down(v, 1, 64); }
-__device__ __forceinline__ cplx shfl_dn1(cplx v) { return {__shfl_down(v.re, 1, 64), __shfl_down(v.im, 1, 64)}; }
-__device__ __forceinline__ double bcast(double v, int l) { return __shfl(v, l, 64); }
-__device__ __forceinline__ cplx bcast(cplx v, int l) { return {__shfl(v.re, l, 64), __shfl(v.im, l, 64)}; }
-
-// ---------------------------------------------------------------------------
-// Tiling of the stencil kernels (256 threads = 4 wave64 per workgroup):
-//   3D: tile = 64 x  *  4*RB y-rows  *  kz z-planes; wave w owns RB consecutive
-//       rows, lane = x.  y-neighbours inside the wave's rows come from
-//       registers, x-neighbours from the neighbouring lane (ds_bpermute).
-//   2D: tile = 64*RB x  *  4*kz rows; wave w marches its own kz rows, each lane
-//       owns RB x-positions 64 apart (x-neighbours across the 64-chunk seam
-//       from the neighbouring chunk's lane 0/63).
-// Both march along the slowest dimension with a (prev, cur, next) register
-// queue, so every cell of the stencil vector is fetched from HBM once; only
-// tile-edge neighbours (1 lane of 64, wave-boundary rows) use L1/L2 loads.
-__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
-
-template <int DIM, int RB> __host__ __device__ inline void tile_counts(const Geo &g, int64_t &ntx,
-                                                                        int64_t &nty, int64_t &ntz) {
-  if (DIM == 3) {
-    ntx = cdiv(g.nx, 64);
-    nty = cdiv(g.nyp, 4 * RB);
-    ntz = cdiv(g.nzl, g.kz);
-  } else {
-    ntx = cdiv(g.nx, 64 * RB);
-    nty = 1;
-    ntz = cdiv(g.nzl, 4 * (int64_t)g.kz);
-  }
-}
-
-// fn(p, cur, lap) for every local cell p of the workgroup's tiles, with
-// cur = V[p] and lap = (L V)[p] (laplacians.hpp:10-105, flat-index form).
-// Local indices are 32-bit (the host guarantees (nzl+2)*P < 2^31); the flat
-// range tests of the reference (idx-nx >= 0, idx+nx < N) are evaluated on
-// (plane, row) coordinates so they never need 64-bit global indices.
-//
-// PLANE = true: fn(p[RB], cur[RB], lap[RB], ok[RB]) is called once per plane
-// with all rows of the thread, so the caller can issue every streamed load of
-// all its rows before the first use (more loads in flight per accumulator set).
-template <class S, int DIM, int RB, bool PLANE = false, class Fn>
-__device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn &&fn) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int64_t ntx64, nty64, ntz64;
-  tile_counts<DIM, RB>(g, ntx64, nty64, ntz64);
-  const int ntx = (int)ntx64, nty = (int)nty64;
-  const int tiles = (int)(ntx64 * nty64 * ntz64);
-  const int T8 = tiles / 8;
-  const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, nzl = (int)g.nzl, kz = g.kz;
-  const int z0 = (int)g.z0, npl = (int)g.npl;
-  for (int t0 = blockIdx.x; t0 < tiles; t0 += gridDim.x) {
-    // optional XCD-banded order (workgroups b, b+8 share an XCD): speed only
-    const int t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
-    const int it = t % ntx;
-    const int rest = t / ntx;
-    const int jt = rest % nty;
-    const int kt = rest / nty;
-    if constexpr (DIM == 3) {
-      const int x = it * 64 + lane;
-      const bool xin = x < nx;
-      const int yb = jt * (4 * RB) + w * RB;
-      if (yb >= nyp) continue;  // wave-uniform
-      const int q0 = kt * kz;
-      const int q1 = q0 + kz < nzl ? q0 + kz : nzl;
-      bool rv[RB];
-      int off[RB];
-      S prev[RB], cur[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        rv[r] = yb + r < nyp;
-        off[r] = (yb + r) * nx + x;
-        const bool ld = xin && rv[r];
-        prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + off[r]] : zero<S>();
-        cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
-      }
-      const bool bx = (x == 0) || (x == nx - 1);
-      for (int q = q0; q < q1; ++q) {
-        const int gq = z0 + q;
-        const bool bz = gq == 0 || gq == npl - 1;
-        const bool has_next = gq + 1 < npl;
-        S next[RB], lapv[RB];
-        int pv[RB];
-        bool okv[RB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-          next[r] = (xin && rv[r] && has_next) ? V[(q + 1) * P + off[r]] : zero<S>();
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          pv[r] = q * P + off[r];
-          okv[r] = false;
-          lapv[r] = zero<S>();
-          if (!rv[r]) continue;  // wave-uniform
-          const int p = q * P + off[r];
-          const int y = yb + r;
-          S ym, yp;
-          if (r > 0) ym = cur[r - 1];
-          else ym = (xin && (gq > 0 || y > 0)) ? V[p - nx] : zero<S>();            // idx - nx >= 0
-          if (r + 1 < RB && rv[r + 1 < RB ? r + 1 : r]) yp = cur[r + 1 < RB ? r + 1 : r];
-          else yp = (xin && (gq < npl - 1 || y < nyp - 1)) ? V[p + nx] : zero<S>();  // idx + nx < N
-          S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
-          const S xe = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin
-                           ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
-          if (lane == 0) xm = xe;
-          if (lane == 63) xp = xe;
-          if (!(x > 0)) xm = zero<S>();
-          if (!(x + 1 < nx)) xp = zero<S>();
-          const bool bnd = bx || bz || y == 0 || y == nyp - 1;
-          const S lap = g.s * (((prev[r] + next[r]) + (xm + xp)) + (ym + yp)) +
-                        (bnd ? g.sd_bd : g.sd_in) * cur[r];
-          if constexpr (PLANE) {
-            okv[r] = xin;
-            lapv[r] = lap;
-          } else {
-            if (xin) fn(p, cur[r], lap);
-          }
-        }
-        if constexpr (PLANE) fn(pv, cur, lapv, okv);
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          prev[r] = cur[r];
-          cur[r] = next[r];
-        }
-      }
-    } else {
-      const int q0 = (kt * 4 + w) * kz;
-      if (q0 >= nzl) continue;  // wave-uniform
-      const int q1 = q0 + kz < nzl ? q0 + kz : nzl;
-      int xr[RB];
-      S prev[RB], cur[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        xr[r] = it * 64 * RB + 64 * r + lane;
-        const bool ld = xr[r] < nx;
-        prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + xr[r]] : zero<S>();
-        cur[r] = ld ? V[q0 * P + xr[r]] : zero<S>();
-      }
-      for (int q = q0; q < q1; ++q) {
-        const int gq = z0 + q;
-        const bool bz = gq == 0 || gq == npl - 1;
-        const bool has_next = gq + 1 < npl;
-        S next[RB], lapv[RB];
-        int pv[RB];
-        bool okv[RB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-          next[r] = (xr[r] < nx && has_next) ? V[(q + 1) * P + xr[r]] : zero<S>();
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const int x = xr[r];
-          const int p = q * P + x;
-          pv[r] = p;
-          S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
-          const S cm = bcast(cur[r > 0 ? r - 1 : 0], 63);
-          const S cp = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
-          const bool edge_ld = (lane == 0 && r == 0 && x < nx && x > 0) ||
-                               (lane == 63 && r + 1 == RB && x + 1 < nx);
-          const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
-          if (lane == 0) xm = r > 0 ? cm : xe;
-          if (lane == 63) xp = r + 1 < RB ? cp : xe;
-          if (!(x > 0)) xm = zero<S>();
-          if (!(x + 1 < nx)) xp = zero<S>();
-          const bool bnd = x == 0 || x == nx - 1 || bz;
-          const S lap = g.s * ((prev[r] + next[r]) + (xm + xp)) + (bnd ? g.sd_bd : g.sd_in) * cur[r];
-          if constexpr (PLANE) {
-            okv[r] = x < nx;
-            lapv[r] = lap;
-          } else {
-            if (x < nx) fn(p, cur[r], lap);
-          }
-        }
-        if constexpr (PLANE) fn(pv, cur, lapv, okv);
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          prev[r] = cur[r];
-          cur[r] = next[r];
-        }
-      }
-    }
-  }
-}
-
-#ifndef NLS_UPD_RB_MODE
-#define NLS_UPD_RB_MODE 1
-#endif
-#ifndef NLS_COEF_LDS
-#define NLS_COEF_LDS 1
-#endif
-__host__ __device__ constexpr int upd_rb(int J) {
-  return NLS_UPD_RB_MODE == 0 ? (J <= 2 ? 4 : (J <= 6 ? 2 : 1))
-       : NLS_UPD_RB_MODE == 1 ? (J <= 2 ? 4 : 2)
-       : NLS_UPD_RB_MODE == 2 ? (J <= 6 ? 4 : 2)
-                              : (J <= 2 ? 4 : (J <= 6 ? 2 : (J <= 18 ? 2 : 1)));
-}
-template <int J> struct UpdRB { static constexpr int v = upd_rb(J); };
-constexpr int RB_ALPHA = 4;
-
-// y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
-template <class S, int DIM>
-__global__ __launch_bounds__(NTHREADS) void k_lap(const S *__restrict__ V, Geo g, S *__restrict__ out) {
-  march<S, DIM, RB_ALPHA>(V, g, [&](int p, const S &, const S &lap) { out[p] = lap; });
-}
-
-// a = V^H L V and ||V||^2 per workgroup, in the symmetric forward-edge form
-//   V^H L V = sum_p d_p |v_p|^2 + 2 s sum_p Re(conj(v_p) (v_{p+1} + v_{p+nx} + v_{p+P}))
-// (each off-diagonal pair of the reference matrix visited once; the matrix is
-// real symmetric, laplacians.hpp:32-37, 89-97, so the form is real).  Only the
-// forward neighbours are needed: x+1 from the next lane, y+1 from the thread's
-// next row, z+1 from the register queue; plane q+2 is prefetched while plane q
-// is reduced.
-template <class S, int DIM, int RB>
-__device__ __forceinline__ void alpha_tiles(const S *__restrict__ V, const Geo &g, double &a, double &n2) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int64_t ntx, nty, ntz;
-  tile_counts<DIM, RB>(g, ntx, nty, ntz);
-  const int64_t tiles = ntx * nty * ntz;
-  const int64_t P = g.P, nx = g.nx;
-  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-    const int64_t it = t % ntx;
-    const int64_t rest = t / ntx;
-    const int64_t jt = rest % nty;
-    const int64_t kt = rest / nty;
-    int64_t q0, q1, yb = 0;
-    int64_t off[RB];
-    bool rv[RB], xin[RB];
-    if constexpr (DIM == 3) {
-      yb = jt * (4 * RB) + (int64_t)w * RB;
-      if (yb >= g.nyp) continue;
-      q0 = kt * g.kz;
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        rv[r] = yb + r < g.nyp;
-        off[r] = (yb + r) * nx + it * 64 + lane;
-        xin[r] = it * 64 + lane < nx;
-      }
-    } else {
-      q0 = (kt * 4 + w) * (int64_t)g.kz;
-      if (q0 >= g.nzl) continue;
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        rv[r] = true;
-        off[r] = it * 64 * RB + 64 * r + lane;
-        xin[r] = off[r] < nx;
-      }
-    }
-    q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
-    S cur[RB], nxt[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const bool ld = xin[r] && rv[r];
-      cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
-      nxt[r] = (ld && g.z0 + q0 + 1 < g.npl) ? V[(q0 + 1) * P + off[r]] : zero<S>();
-    }
-    for (int64_t q = q0; q < q1; ++q) {
-      const int64_t gq = g.z0 + q;
-      // forward neighbours that live outside this wave's registers
-      S xe[RB], ye = zero<S>();
-#pragma unroll
-      for (int r = 0; r < RB; ++r) xe[r] = shfl_dn1(cur[r]);
-      if constexpr (DIM == 3) {
-        const int rl = RB - 1;
-        // y+1 of the wave's last valid row: flat p + nx (covers the 3D y-wrap)
-        int rlast = 0;
-#pragma unroll
-        for (int r = 0; r < RB; ++r) if (rv[r]) rlast = r;
-        const int64_t p = q * P + off[rlast];
-        const int64_t pg = gq * P + off[rlast];
-        (void)rl;
-        ye = (xin[rlast] && pg + nx < g.Ng) ? V[p + nx] : zero<S>();
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const int64_t x = it * 64 + lane;
-          if (lane == 63) xe[r] = (rv[r] && x + 1 < nx) ? V[q * P + off[r] + 1] : zero<S>();
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const S c0 = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
-          if (lane == 63) {
-            if (r + 1 < RB) xe[r] = c0;
-            else xe[r] = (off[r] + 1 < nx) ? V[q * P + off[r] + 1] : zero<S>();
-          }
-        }
-      }
-      // prefetch plane q+2
-      S nn[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r)
-        nn[r] = (xin[r] && rv[r] && gq + 2 < g.npl && q + 2 < q1 + 1) ? V[(q + 2) * P + off[r]]
-                                                                        : zero<S>();
-      const bool bz = gq == 0 || gq == g.npl - 1;
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        if (!rv[r]) continue;
-        const int64_t x = DIM == 3 ? it * 64 + lane : off[r];
-        if (!xin[r]) continue;
-        const S c = cur[r];
-        S f = (x + 1 < nx) ? xe[r] : zero<S>();
-        if constexpr (DIM == 3) {
-          const bool last = !(r + 1 < RB && rv[r + 1 < RB ? r + 1 : r]);
-          f = f + (last ? ye : cur[r + 1 < RB ? r + 1 : r]);
-        }
-        f = f + nxt[r];
-        const bool bnd = x == 0 || x == nx - 1 || bz ||
-                         (DIM == 3 && (yb + r == 0 || yb + r == g.nyp - 1));
-        const double c2 = abs2(c);
-        n2 += c2;
-        a += (bnd ? g.sd_bd : g.sd_in) * c2 + 2.0 * g.s * to_c(cj_mul(c, f)).re;
-      }
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        cur[r] = nxt[r];
-        nxt[r] = nn[r];
-      }
-    }
-  }
-}
-
-template <class S, int DIM>
-__global__ __launch_bounds__(NTHREADS) void k_alpha(const S *__restrict__ V, Geo g, cplx *__restrict__ part) {
-  double a = 0.0, n2 = 0.0;
-  alpha_tiles<S, DIM, RB_ALPHA>(V, g, a, n2);
-  cplx v[2] = {{a, 0.0}, {n2, 0.0}};
-  block_store<2>(v, part);
-}
-
-// W_{J+1} = a * L W_J - sum_{k<=J} b_k W_k ;  partials g_k = W_k^H W_{J+1}, ||W_{J+1}||^2
-template <class S, int DIM, int J>
-__global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S *__restrict__ out,
-                                                     int64_t vs, Geo g,
-                                                     const KState *__restrict__ st,
-                                                     cplx *__restrict__ part) {
-  constexpr int NA = J + 2;
-  S acc[NA];
-#pragma unroll
-  for (int k = 0; k < NA; ++k) acc[k] = zero<S>();
-#if NLS_COEF_LDS
-  // Coefficients broadcast from LDS at every use (ds_read_b128, one address per
-  // wave): keeps 4(J+1) SGPRs free, which otherwise spill to VGPR lanes and cost
-  // ~90 v_readlane per cell row in the hot loop.  The empty asm with a memory
-  // clobber stops the compiler from hoisting the LDS reads back into registers.
-  __shared__ cplx cfs[MMAX + 2];
-  for (int k = threadIdx.x; k <= J + 1; k += NTHREADS) cfs[k] = st->coef[k];
-  __syncthreads();
-  const double a = cfs[J + 1].re;
-#define NLS_B(k) cfs[k]
-#define NLS_RELOAD() asm volatile("" ::: "memory")
-#else
-  cplx b[J + 1];
-#pragma unroll
-  for (int k = 0; k <= J; ++k) b[k] = st->coef[k];
-  const double a = st->coef[J + 1].re;
-#define NLS_B(k) b[k]
-#define NLS_RELOAD() ((void)0)
-#endif
-  const S *__restrict__ VJ = W + (int64_t)J * vs;
-  constexpr int RB = UpdRB<J>::v;
-  march<S, DIM, RB, true>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
-    // every streamed load of every row first ...
-    S wk[RB][J > 0 ? J : 1];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const S *__restrict__ src = W + p[r];
-#pragma unroll
-      for (int k = 0; k < J; ++k) {
-        wk[r][k] = ok[r] ? ld_nt(src) : zero<S>();
-        src += vs;
-      }
-    }
-    NLS_RELOAD();
-    // ... then the CGS update, the store and the Gram / norm partial sums
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      if (!ok[r]) continue;
-      S X = a * lap[r] - coef_mul(NLS_B(J), cur[r]);
-#pragma unroll
-      for (int k = 0; k < J; ++k) X = X - coef_mul(NLS_B(k), wk[r][k]);
-      st_nt(out + p[r], X);
-#pragma unroll
-      for (int k = 0; k < J; ++k) acc[k] = acc[k] + cj_mul(wk[r][k], X);
-      acc[J] = acc[J] + cj_mul(cur[r], X);
-      acc[J + 1] = acc[J + 1] + from_real<S>(abs2(X));
-    }
-  });
-  cplx v[NA];
-#pragma unroll
-  for (int k = 0; k < NA; ++k) v[k] = to_c(acc[k]);
-  block_store<NA>(v, part);
-#undef NLS_B
-#undef NLS_RELOAD
-}
 
 // host-side mirror of the tiling, for grid sizes
 int64_t stencil_tiles(const Geo &g, int dim, int rb) {
@@ -758,14 +310,17 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
 // ---------------------------------------------------------------------------
 // pointwise kernels
 
-// Nonlinear half step out = exp(-0.5*tau*rho(u)) u, tau = 1j*dt
-//  cubic (nlse_solver.hpp:66-69): rho = re^2 + im^2
-//  cubic-quintic (device/nlse_cq_solver.hpp:16-39): d = |u|*|u|, rho = s1 d + s2 d^2
-__device__ __forceinline__ cplx nl_half(cplx u, double dt, int nonlin, cplx s1, cplx s2) {
-  if (nonlin == 0) {
+// Nonlinear half step, tau = 1j*dt
+//  0 cubic (nlse_solver.hpp:66-69): out = exp(-0.5*tau*rho) u, rho = re^2 + im^2
+//  1 cubic-quintic (device/nlse_cq_solver.hpp:16-39): d = |u|*|u|, rho = s1 d + s2 d^2
+//  2 G2 cubic with focusing field (nlsolvers/device/include/nlse_dev.hpp:20-40):
+//    out = u * exp(0.5*tau * m|u|^2)   (note the sign: G2 integrates with +tau)
+__device__ __forceinline__ cplx nl_half(cplx u, double mval, double dt, int nonlin, cplx s1, cplx s2) {
+  if (nonlin == 0 || nonlin == 2) {
     const double x = u.re * u.re + u.im * u.im;
+    const double ph = nonlin == 0 ? (-0.5 * dt) * x : (0.5 * dt) * (mval * x);
     double sn, cs;
-    sincos((-0.5 * dt) * x, &sn, &cs);
+    sincos(ph, &sn, &cs);
     return {cs * u.re - sn * u.im, cs * u.im + sn * u.re};
   }
   const double a = hypot(u.re, u.im);
@@ -779,18 +334,19 @@ __device__ __forceinline__ cplx nl_half(cplx u, double dt, int nonlin, cplx s1, 
 }
 
 __global__ __launch_bounds__(NTHREADS) void k_nl_init(const cplx *__restrict__ u, cplx *__restrict__ w0,
-                                                      int64_t n, double dt, int nonlin, cplx s1,
-                                                      cplx s2) {
+                                                      const double *__restrict__ mf, int64_t n,
+                                                      double dt, int nonlin, cplx s1, cplx s2) {
   for (int64_t p = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; p < n;
        p += (int64_t)gridDim.x * NTHREADS)
-    w0[p] = nl_half(u[p], dt, nonlin, s1, s2);
+    w0[p] = nl_half(u[p], nonlin == 2 ? mf[p] : 0.0, dt, nonlin, s1, s2);
 }
 
 // u = N(sum_k fin_k W_k) ; W_0 <- N(u) for the next step (fused start of step)
 template <int M>
 __global__ __launch_bounds__(NTHREADS) void k_final_nlse(cplx *__restrict__ W, int64_t vs, int64_t n,
                                                          const KState *__restrict__ st,
-                                                         cplx *__restrict__ u, double dt,
+                                                         cplx *__restrict__ u,
+                                                         const double *__restrict__ mf, double dt,
                                                          int nonlin, cplx s1, cplx s2) {
   // two cells per thread, all 2M basis loads issued before the first use;
   // combination coefficients broadcast from LDS
@@ -819,10 +375,76 @@ __global__ __launch_bounds__(NTHREADS) void k_final_nlse(cplx *__restrict__ W, i
       cplx y = {0.0, 0.0};
 #pragma unroll
       for (int k = 0; k < M; ++k) y += cmul(cf[k], w[q][k]);
-      const cplx un = nl_half(y, dt, nonlin, s1, s2);
+      const double mv = nonlin == 2 ? mf[p] : 0.0;
+      const cplx un = nl_half(y, mv, dt, nonlin, s1, s2);
       st_nt(u + p, un);
-      st_nt(W + p, nl_half(un, dt, nonlin, s1, s2));
+      st_nt(W + p, nl_half(un, mv, dt, nonlin, s1, s2));
     }
+  }
+}
+
+// Neumann "copy" boundary condition of the G2 drivers (boundaries.cuh:10-19
+// for 2D, :24-81 for 3D).  The reference's sequence of strided copies
+// (faces of the slowest axis from their inner neighbour plane, then the next
+// axis over the full extent of the previous, ...) leaves every boundary cell
+// equal to the cell with all coordinates clamped into [1, n-2]; interior
+// cells are never written, so the gather is race-free in place.  Only the
+// boundary shell is visited: the perimeter of every local plane plus the full
+// global first/last plane.  When the start vector of the next step is live
+// (w0_ready), its boundary cells are refreshed with N(u) at the same time.
+__host__ __device__ inline int64_t bc_perimeter(const Geo &g) {
+  return g.nyp == 1 ? 2 : 2 * g.nx + 2 * (g.nyp - 2);
+}
+__host__ __device__ inline int64_t bc_cells(const Geo &g) {
+  const int64_t full = (g.z0 == 0 ? 1 : 0) + (g.z0 + g.nzl == g.npl ? 1 : 0);
+  return g.nzl * bc_perimeter(g) + full * g.P;
+}
+int64_t neumann_bc_cells(const Geo &g) { return bc_cells(g); }
+
+__global__ __launch_bounds__(NTHREADS) void k_neumann_bc(cplx *__restrict__ u, cplx *__restrict__ w0,
+                                                         const double *__restrict__ mf, Geo g,
+                                                         int w0_ready, double dt, int nonlin,
+                                                         cplx s1, cplx s2) {
+  const int64_t per = bc_perimeter(g);
+  const int64_t nper = g.nzl * per;
+  const int64_t total = bc_cells(g);
+  const int64_t nx = g.nx, nyp = g.nyp;
+  for (int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * NTHREADS) {
+    int64_t q, x, y;
+    if (t < nper) {  // perimeter of local plane q
+      q = t / per;
+      const int64_t k = t % per;
+      if (nyp == 1) {
+        x = k == 0 ? 0 : nx - 1;
+        y = 0;
+      } else if (k < nx) {
+        x = k; y = 0;
+      } else if (k < 2 * nx) {
+        x = k - nx; y = nyp - 1;
+      } else if (k < 2 * nx + nyp - 2) {
+        x = 0; y = 1 + (k - 2 * nx);
+      } else {
+        x = nx - 1; y = 1 + (k - 2 * nx - (nyp - 2));
+      }
+    } else {  // full global boundary plane(s) owned by this slab
+      const int64_t k = t - nper;
+      const int64_t which = k / g.P, c = k % g.P;
+      const bool has_first = g.z0 == 0;
+      q = (which == 0 && has_first) ? 0 : g.nzl - 1;
+      x = c % nx;
+      y = c / nx;
+    }
+    const int64_t gq = g.z0 + q;
+    const int64_t xs = x < 1 ? 1 : (x > nx - 2 ? nx - 2 : x);
+    const int64_t ys = nyp == 1 ? 0 : (y < 1 ? 1 : (y > nyp - 2 ? nyp - 2 : y));
+    const int64_t gs = gq < 1 ? 1 : (gq > g.npl - 2 ? g.npl - 2 : gq);
+    const int64_t src = (gs - g.z0) * g.P + ys * nx + xs;
+    const int64_t dst = q * g.P + y * nx + x;
+    if (src == dst) continue;
+    const cplx v = u[src];
+    u[dst] = v;
+    if (w0_ready) w0[dst] = nl_half(v, nonlin == 2 ? mf[dst] : 0.0, dt, nonlin, s1, s2);
   }
 }
 
@@ -904,42 +526,17 @@ __global__ __launch_bounds__(NTHREADS) void k_sg_velocity(const double *__restri
 // ---------------------------------------------------------------------------
 // kernel tables (host side)
 
-#define NLS_J_LIST(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
-  X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) \
-  X(28) X(29) X(30)
-#define NLS_M_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) \
-  X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) \
-  X(29) X(30) X(31) X(32)
-
-template <class S, int DIM> const void *update_fn(int J) {
-  switch (J) {
-#define X(J) case J: return reinterpret_cast<const void *>(&k_update<S, DIM, J>);
-    NLS_J_LIST(X)
-#undef X
-    default: return nullptr;
-  }
+namespace {
+using Table = const void *(*)(int, bool, int);
+Table table(int dim, bool ani) {
+  return ani ? (dim == 3 ? &stencil_table_ani3 : &stencil_table_ani2)
+             : (dim == 3 ? &stencil_table_iso3 : &stencil_table_iso2);
 }
+}  // namespace
 
-const void *kernel_update(bool cplx_, int dim, int J) {
-  if (cplx_) return dim == 3 ? update_fn<cplx, 3>(J) : update_fn<cplx, 2>(J);
-  return dim == 3 ? update_fn<double, 3>(J) : update_fn<double, 2>(J);
-}
-
-const void *kernel_alpha(bool cplx_, int dim) {
-  if (cplx_)
-    return dim == 3 ? reinterpret_cast<const void *>(&k_alpha<cplx, 3>)
-                    : reinterpret_cast<const void *>(&k_alpha<cplx, 2>);
-  return dim == 3 ? reinterpret_cast<const void *>(&k_alpha<double, 3>)
-                  : reinterpret_cast<const void *>(&k_alpha<double, 2>);
-}
-
-const void *kernel_lap(bool cplx_, int dim) {
-  if (cplx_)
-    return dim == 3 ? reinterpret_cast<const void *>(&k_lap<cplx, 3>)
-                    : reinterpret_cast<const void *>(&k_lap<cplx, 2>);
-  return dim == 3 ? reinterpret_cast<const void *>(&k_lap<double, 3>)
-                  : reinterpret_cast<const void *>(&k_lap<double, 2>);
-}
+const void *kernel_update(bool cplx_, int dim, int J, bool ani) { return table(dim, ani)(NLS_KIND_UPDATE, cplx_, J); }
+const void *kernel_alpha(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_ALPHA, cplx_, 0); }
+const void *kernel_lap(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_LAP, cplx_, 0); }
 
 // local-transport all-reduce: dst[v] = sum_r pub[r][parity][v] in rank order
 __global__ __launch_bounds__(NTHREADS) void k_sum_ranks(cplx *__restrict__ dst, const cplx *__restrict__ pub,
@@ -956,6 +553,7 @@ const void *kernel_reduce_iter() { return reinterpret_cast<const void *>(&k_redu
 const void *kernel_reduce_final() { return reinterpret_cast<const void *>(&k_reduce_final); }
 const void *kernel_nl_init() { return reinterpret_cast<const void *>(&k_nl_init); }
 const void *kernel_sg_velocity() { return reinterpret_cast<const void *>(&k_sg_velocity); }
+const void *kernel_neumann_bc() { return reinterpret_cast<const void *>(&k_neumann_bc); }
 
 const void *kernel_final_nlse(int M) {
   switch (M) {
@@ -996,3 +594,4 @@ const void *kernel_sg_end(int M) {
 }
 
 }  // namespace nls
+

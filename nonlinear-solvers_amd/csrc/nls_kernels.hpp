@@ -9,12 +9,20 @@ namespace nls {
 //   update : (const S* W, S* out, int64_t vs, Geo g, const KState* st, cplx* part)
 //   alpha  : (const S* V, Geo g, cplx* part)
 //   lap    : (const S* V, Geo g, S* out)
-const void *kernel_update(bool complex_, int dim, int J);
-const void *kernel_alpha(bool complex_, int dim);
-const void *kernel_lap(bool complex_, int dim);
+// ani = true: the G2 anisotropic operator (complex only; Geo::cf = c field)
+const void *kernel_update(bool complex_, int dim, int J, bool ani);
+const void *kernel_alpha(bool complex_, int dim, bool ani);
+const void *kernel_lap(bool complex_, int dim, bool ani);
 int64_t stencil_tiles(const Geo &g, int dim, int rows_per_thread);
 int update_rows_per_thread(int J);
 int alpha_rows_per_thread();
+
+// per-variant tables (nls_stencil.hip, one object per operator x dimension)
+enum { NLS_KIND_UPDATE = 0, NLS_KIND_ALPHA = 1, NLS_KIND_LAP = 2 };
+const void *stencil_table_iso2(int kind, bool complex_, int J);
+const void *stencil_table_iso3(int kind, bool complex_, int J);
+const void *stencil_table_ani2(int kind, bool complex_, int J);
+const void *stencil_table_ani3(int kind, bool complex_, int J);
 
 // single workgroup:
 //   reduce_iter  : (KState*, const cplx* partA, int nbA, const cplx* partU, int nbU, int j,
@@ -27,9 +35,12 @@ const void *kernel_sum_ranks();
 const void *kernel_reduce_final();
 
 // pointwise (grid-stride):
-//   nl_init   : (const cplx* u, cplx* w0, int64_t n, double dt, int nonlin, cplx s1, cplx s2)
-//   final_nlse: (cplx* W, int64_t vs, int64_t n, const KState*, cplx* u, double dt, int nonlin,
+//   nl_init   : (const cplx* u, cplx* w0, const double* mf, int64_t n, double dt, int nonlin,
 //                cplx s1, cplx s2)
+//   final_nlse: (cplx* W, int64_t vs, int64_t n, const KState*, cplx* u, const double* mf,
+//                double dt, int nonlin, cplx s1, cplx s2)
+//   neumann_bc: (cplx* u, cplx* w0, const double* mf, Geo g, int w0_ready, double dt, int nonlin,
+//                cplx s1, cplx s2)   -- boundary cells only (grid over neumann_bc_cells())
 //   combine   : (const S* W, int64_t vs, int64_t n, const KState*, S* out)
 //   sg_mid    : (const double* W, int64_t vs, int64_t n, const KState*, const double* mf,
 //                double* up, double* g0)
@@ -42,5 +53,7 @@ const void *kernel_combine(bool complex_, int M);
 const void *kernel_sg_mid(int M);
 const void *kernel_sg_end(int M);
 const void *kernel_sg_velocity();
+const void *kernel_neumann_bc();
+int64_t neumann_bc_cells(const Geo &g);
 
 }  // namespace nls

@@ -1,0 +1,593 @@
+// nls_stencil.hpp -- device-side building blocks of the stencil kernels
+// (included by nls_stencil.hip, which is compiled once per operator variant
+// and dimension, and by nls_kernels.hip for the shared helpers).
+//
+// Two operators share one tiled march:
+//   iso  (G1, laplacians.hpp:10-105): constant 5/7-point stencil, diagonal
+//        -4/-3 (2D) or -6/-5 (3D) times the scale.
+//   ani  (G2, nlsolvers/common/include/laplacians.hpp:54-103, 158-218):
+//        div(c grad u) with face weights w = (c_a + c_b)/2 on every coupling
+//        of the same flat-index pattern (incl. the 3D y-wrap) and diagonal
+//        -sum(w), i.e.  (L v)_p = s * sum_{q ~ p} w_pq (v_q - v_p).
+//        c is marched alongside the vector (one extra f64 stream per pass).
+#pragma once
+#include <utility>
+
+#include "nls_device.hpp"
+
+namespace nls {
+
+template <class S> __device__ __forceinline__ S from_real(double v);
+template <> __device__ __forceinline__ double from_real<double>(double v) { return v; }
+template <> __device__ __forceinline__ cplx from_real<cplx>(double v) { return {v, 0.0}; }
+
+// ---------------------------------------------------------------------------
+// wave64 + workgroup reduction into one partial per workgroup (fixed order:
+// results are bitwise reproducible run to run)
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// partials are stored column-major: out[k * gridDim.x + blockIdx.x], so the
+// single-workgroup reduction reads each column with coalesced 1 KiB wave loads.
+template <int NA>
+__device__ __forceinline__ void block_store(cplx (&v)[NA], cplx *__restrict__ out) {
+  __shared__ cplx red[NTHREADS / 64][NA];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    v[k].re = wave_sum(v[k].re);
+    v[k].im = wave_sum(v[k].im);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) red[w][k] = v[k];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < NA; k += NTHREADS) {
+    cplx s = red[0][k];
+#pragma unroll
+    for (int q = 1; q < NTHREADS / 64; ++q) s += red[q][k];
+    out[(int64_t)k * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// memory helpers: basis vectors streamed once per pass use non-temporal
+// loads/stores (measured +5-10 % on 16-stream passes, tools/bw_probe.hip);
+// the stencil vector keeps default policy (its neighbours are re-read).
+typedef double v2d __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ cplx ld_nt(const cplx *p) {
+  const v2d v = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p));
+  return {v.x, v.y};
+}
+__device__ __forceinline__ double ld_nt(const double *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_nt(cplx *p, cplx v) {
+  v2d t;
+  t.x = v.re;
+  t.y = v.im;
+  __builtin_nontemporal_store(t, reinterpret_cast<v2d *>(p));
+}
+__device__ __forceinline__ void st_nt(double *p, double v) { __builtin_nontemporal_store(v, p); }
+
+// wave64 cross-lane moves (ds_bpermute)
+__device__ __forceinline__ double shfl_up1(double v) { return __shfl_up(v, 1, 64); }
+__device__ __forceinline__ cplx shfl_up1(cplx v) { return {__shfl_up(v.re, 1, 64), __shfl_up(v.im, 1, 64)}; }
+__device__ __forceinline__ double shfl_dn1(double v) { return __shfl_down(v, 1, 64); }
+__device__ __forceinline__ cplx shfl_dn1(cplx v) { return {__shfl_down(v.re, 1, 64), __shfl_down(v.im, 1, 64)}; }
+__device__ __forceinline__ double bcast(double v, int l) { return __shfl(v, l, 64); }
+__device__ __forceinline__ cplx bcast(cplx v, int l) { return {__shfl(v.re, l, 64), __shfl(v.im, l, 64)}; }
+
+
+// ---------------------------------------------------------------------------
+// Tiling of the stencil kernels (256 threads = 4 wave64 per workgroup):
+//   3D: tile = 64 x  *  4*RB y-rows  *  kz z-planes; wave w owns RB consecutive
+//       rows, lane = x.  y-neighbours inside the wave's rows come from
+//       registers, x-neighbours from the neighbouring lane (ds_bpermute).
+//   2D: tile = 64*RB x  *  4*kz rows; wave w marches its own kz rows, each lane
+//       owns RB x-positions 64 apart (x-neighbours across the 64-chunk seam
+//       from the neighbouring chunk's lane 0/63).
+// Both march along the slowest dimension with a (prev, cur, next) register
+// queue, so every cell of the stencil vector is fetched from HBM once; only
+// tile-edge neighbours (1 lane of 64, wave-boundary rows) use L1/L2 loads.
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+template <int DIM, int RB> __host__ __device__ inline void tile_counts(const Geo &g, int64_t &ntx,
+                                                                        int64_t &nty, int64_t &ntz) {
+  if (DIM == 3) {
+    ntx = cdiv(g.nx, 64);
+    nty = cdiv(g.nyp, 4 * RB);
+    ntz = cdiv(g.nzl, g.kz);
+  } else {
+    ntx = cdiv(g.nx, 64 * RB);
+    nty = 1;
+    ntz = cdiv(g.nzl, 4 * (int64_t)g.kz);
+  }
+}
+
+// weight of one anisotropic coupling, (c_a + c_b) / 2 (laplacians.hpp:181-209),
+// zero when the neighbour is not coupled
+__device__ __forceinline__ double face_w(bool e, double ca, double cb) { return e ? 0.5 * (ca + cb) : 0.0; }
+
+// fn(p, cur, lap) for every local cell p of the workgroup's tiles, with
+// cur = V[p] and lap = (L V)[p] (laplacians.hpp:10-105, flat-index form).
+// Local indices are 32-bit (the host guarantees (nzl+2)*P < 2^31); the flat
+// range tests of the reference (idx-nx >= 0, idx+nx < N) are evaluated on
+// (plane, row) coordinates so they never need 64-bit global indices.
+//
+// PLANE = true: fn(p[RB], cur[RB], lap[RB], ok[RB]) is called once per plane
+// with all rows of the thread, so the caller can issue every streamed load of
+// all its rows before the first use (more loads in flight per accumulator set).
+// ANI = true: the G2 operator; the coefficient field g.cf (same layout and
+// ghost planes as a basis vector) is marched with the same register queue.
+template <class S, int DIM, int RB, bool PLANE = false, bool ANI = false, class Fn>
+__device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn &&fn) {
+  const double *__restrict__ C = g.cf;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t ntx64, nty64, ntz64;
+  tile_counts<DIM, RB>(g, ntx64, nty64, ntz64);
+  const int ntx = (int)ntx64, nty = (int)nty64;
+  const int tiles = (int)(ntx64 * nty64 * ntz64);
+  const int T8 = tiles / 8;
+  const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, nzl = (int)g.nzl, kz = g.kz;
+  const int z0 = (int)g.z0, npl = (int)g.npl;
+  for (int t0 = blockIdx.x; t0 < tiles; t0 += gridDim.x) {
+    // optional XCD-banded order (workgroups b, b+8 share an XCD): speed only
+    const int t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
+    const int it = t % ntx;
+    const int rest = t / ntx;
+    const int jt = rest % nty;
+    const int kt = rest / nty;
+    if constexpr (DIM == 3) {
+      const int x = it * 64 + lane;
+      const bool xin = x < nx;
+      const int yb = jt * (4 * RB) + w * RB;
+      if (yb >= nyp) continue;  // wave-uniform
+      const int q0 = kt * kz;
+      const int q1 = q0 + kz < nzl ? q0 + kz : nzl;
+      bool rv[RB];
+      int off[RB];
+      S prev[RB], cur[RB];
+      double cprv[RB], ccur[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        rv[r] = yb + r < nyp;
+        off[r] = (yb + r) * nx + x;
+        const bool ld = xin && rv[r];
+        prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + off[r]] : zero<S>();
+        cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
+        if constexpr (ANI) {
+          cprv[r] = (ld && z0 + q0 > 0) ? C[(q0 - 1) * P + off[r]] : 0.0;
+          ccur[r] = ld ? C[q0 * P + off[r]] : 0.0;
+        }
+      }
+      const bool bx = (x == 0) || (x == nx - 1);
+      for (int q = q0; q < q1; ++q) {
+        const int gq = z0 + q;
+        const bool bz = gq == 0 || gq == npl - 1;
+        const bool has_next = gq + 1 < npl;
+        S next[RB], lapv[RB];
+        double cnxt[RB];
+        int pv[RB];
+        bool okv[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const bool ld = xin && rv[r] && has_next;
+          next[r] = ld ? V[(q + 1) * P + off[r]] : zero<S>();
+          if constexpr (ANI) cnxt[r] = ld ? C[(q + 1) * P + off[r]] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          pv[r] = q * P + off[r];
+          okv[r] = false;
+          lapv[r] = zero<S>();
+          if (!rv[r]) continue;  // wave-uniform
+          const int p = q * P + off[r];
+          const int y = yb + r;
+          const bool eym = gq > 0 || y > 0;            // idx - nx >= 0
+          const bool eyp = gq < npl - 1 || y < nyp - 1;  // idx + nx < N
+          const bool inner_yp = r + 1 < RB && rv[r + 1 < RB ? r + 1 : r];
+          S ym, yp;
+          if (r > 0) ym = cur[r - 1];
+          else ym = (xin && eym) ? V[p - nx] : zero<S>();
+          if (inner_yp) yp = cur[r + 1 < RB ? r + 1 : r];
+          else yp = (xin && eyp) ? V[p + nx] : zero<S>();
+          S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
+          const bool edge_ld = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin;
+          const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
+          if (lane == 0) xm = xe;
+          if (lane == 63) xp = xe;
+          if (!(x > 0)) xm = zero<S>();
+          if (!(x + 1 < nx)) xp = zero<S>();
+          S lap;
+          if constexpr (ANI) {
+            const double cc = ccur[r];
+            double cym, cyp;
+            if (r > 0) cym = ccur[r - 1];
+            else cym = (xin && eym) ? C[p - nx] : 0.0;
+            if (inner_yp) cyp = ccur[r + 1 < RB ? r + 1 : r];
+            else cyp = (xin && eyp) ? C[p + nx] : 0.0;
+            double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
+            const double cxe = edge_ld ? C[p + (lane == 0 ? -1 : 1)] : 0.0;
+            if (lane == 0) cxm = cxe;
+            if (lane == 63) cxp = cxe;
+            const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
+            const double wym = face_w(eym, cc, cym), wyp = face_w(eyp, cc, cyp);
+            const double wzm = face_w(gq > 0, cc, cprv[r]), wzp = face_w(has_next, cc, cnxt[r]);
+            lap = g.s * ((((wzm * prev[r] + wzp * next[r]) + (wxm * xm + wxp * xp)) +
+                          (wym * ym + wyp * yp)) -
+                         (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * cur[r]);
+          } else {
+            const bool bnd = bx || bz || y == 0 || y == nyp - 1;
+            lap = g.s * (((prev[r] + next[r]) + (xm + xp)) + (ym + yp)) +
+                  (bnd ? g.sd_bd : g.sd_in) * cur[r];
+          }
+          if constexpr (PLANE) {
+            okv[r] = xin;
+            lapv[r] = lap;
+          } else {
+            if (xin) fn(p, cur[r], lap);
+          }
+        }
+        if constexpr (PLANE) fn(pv, cur, lapv, okv);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          prev[r] = cur[r];
+          cur[r] = next[r];
+          if constexpr (ANI) {
+            cprv[r] = ccur[r];
+            ccur[r] = cnxt[r];
+          }
+        }
+      }
+    } else {
+      const int q0 = (kt * 4 + w) * kz;
+      if (q0 >= nzl) continue;  // wave-uniform
+      const int q1 = q0 + kz < nzl ? q0 + kz : nzl;
+      int xr[RB];
+      S prev[RB], cur[RB];
+      double cprv[RB], ccur[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        xr[r] = it * 64 * RB + 64 * r + lane;
+        const bool ld = xr[r] < nx;
+        prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + xr[r]] : zero<S>();
+        cur[r] = ld ? V[q0 * P + xr[r]] : zero<S>();
+        if constexpr (ANI) {
+          cprv[r] = (ld && z0 + q0 > 0) ? C[(q0 - 1) * P + xr[r]] : 0.0;
+          ccur[r] = ld ? C[q0 * P + xr[r]] : 0.0;
+        }
+      }
+      for (int q = q0; q < q1; ++q) {
+        const int gq = z0 + q;
+        const bool bz = gq == 0 || gq == npl - 1;
+        const bool has_next = gq + 1 < npl;
+        S next[RB], lapv[RB];
+        double cnxt[RB];
+        int pv[RB];
+        bool okv[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const bool ld = xr[r] < nx && has_next;
+          next[r] = ld ? V[(q + 1) * P + xr[r]] : zero<S>();
+          if constexpr (ANI) cnxt[r] = ld ? C[(q + 1) * P + xr[r]] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int x = xr[r];
+          const int p = q * P + x;
+          pv[r] = p;
+          S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
+          const S cm = bcast(cur[r > 0 ? r - 1 : 0], 63);
+          const S cp = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
+          const bool edge_ld = (lane == 0 && r == 0 && x < nx && x > 0) ||
+                               (lane == 63 && r + 1 == RB && x + 1 < nx);
+          const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
+          if (lane == 0) xm = r > 0 ? cm : xe;
+          if (lane == 63) xp = r + 1 < RB ? cp : xe;
+          if (!(x > 0)) xm = zero<S>();
+          if (!(x + 1 < nx)) xp = zero<S>();
+          S lap;
+          if constexpr (ANI) {
+            const double cc = ccur[r];
+            double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
+            const double ccm = bcast(ccur[r > 0 ? r - 1 : 0], 63);
+            const double ccp = bcast(ccur[r + 1 < RB ? r + 1 : r], 0);
+            const double cxe = edge_ld ? C[p + (lane == 0 ? -1 : 1)] : 0.0;
+            if (lane == 0) cxm = r > 0 ? ccm : cxe;
+            if (lane == 63) cxp = r + 1 < RB ? ccp : cxe;
+            const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
+            const double wzm = face_w(gq > 0, cc, cprv[r]), wzp = face_w(has_next, cc, cnxt[r]);
+            lap = g.s * (((wzm * prev[r] + wzp * next[r]) + (wxm * xm + wxp * xp)) -
+                         ((wzm + wzp) + (wxm + wxp)) * cur[r]);
+          } else {
+            const bool bnd = x == 0 || x == nx - 1 || bz;
+            lap = g.s * ((prev[r] + next[r]) + (xm + xp)) + (bnd ? g.sd_bd : g.sd_in) * cur[r];
+          }
+          if constexpr (PLANE) {
+            okv[r] = x < nx;
+            lapv[r] = lap;
+          } else {
+            if (x < nx) fn(p, cur[r], lap);
+          }
+        }
+        if constexpr (PLANE) fn(pv, cur, lapv, okv);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          prev[r] = cur[r];
+          cur[r] = next[r];
+          if constexpr (ANI) {
+            cprv[r] = ccur[r];
+            ccur[r] = cnxt[r];
+          }
+        }
+      }
+    }
+  }
+}
+
+#ifndef NLS_UPD_RB_MODE
+#define NLS_UPD_RB_MODE 1
+#endif
+#ifndef NLS_COEF_LDS
+#define NLS_COEF_LDS 1
+#endif
+__host__ __device__ constexpr int upd_rb(int J) {
+  return NLS_UPD_RB_MODE == 0 ? (J <= 2 ? 4 : (J <= 6 ? 2 : 1))
+       : NLS_UPD_RB_MODE == 1 ? (J <= 2 ? 4 : 2)
+       : NLS_UPD_RB_MODE == 2 ? (J <= 6 ? 4 : 2)
+                              : (J <= 2 ? 4 : (J <= 6 ? 2 : (J <= 18 ? 2 : 1)));
+}
+template <int J> struct UpdRB { static constexpr int v = upd_rb(J); };
+constexpr int RB_ALPHA = 4;
+
+// y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
+template <class S, int DIM, bool ANI>
+__global__ __launch_bounds__(NTHREADS) void k_lap(const S *__restrict__ V, Geo g, S *__restrict__ out) {
+  march<S, DIM, RB_ALPHA, false, ANI>(V, g, [&](int p, const S &, const S &lap) { out[p] = lap; });
+}
+
+// a = V^H L V and ||V||^2 per workgroup, from forward couplings only (each
+// off-diagonal pair of the reference matrix visited once; the matrices are
+// real symmetric, laplacians.hpp:32-37, 89-97, 181-209, so the form is real):
+//   iso:  V^H L V = sum_p d_p |v_p|^2 + 2 s sum_p Re(conj(v_p) (v_{p+1} + v_{p+nx} + v_{p+P}))
+//   ani:  V^H L V = -s sum_{forward pairs (p,q)} w_pq |v_p - v_q|^2   (diag = -sum w)
+// Only the forward neighbours are needed: x+1 from the next lane, y+1 from the
+// thread's next row, z+1 from the register queue; plane q+2 is prefetched
+// while plane q is reduced.
+template <class S, int DIM, int RB, bool ANI>
+__device__ __forceinline__ void alpha_tiles(const S *__restrict__ V, const Geo &g, double &a, double &n2) {
+  const double *__restrict__ C = g.cf;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t ntx, nty, ntz;
+  tile_counts<DIM, RB>(g, ntx, nty, ntz);
+  const int64_t tiles = ntx * nty * ntz;
+  const int64_t P = g.P, nx = g.nx;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int64_t it = t % ntx;
+    const int64_t rest = t / ntx;
+    const int64_t jt = rest % nty;
+    const int64_t kt = rest / nty;
+    int64_t q0, q1, yb = 0;
+    int64_t off[RB];
+    bool rv[RB], xin[RB];
+    if constexpr (DIM == 3) {
+      yb = jt * (4 * RB) + (int64_t)w * RB;
+      if (yb >= g.nyp) continue;
+      q0 = kt * g.kz;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        rv[r] = yb + r < g.nyp;
+        off[r] = (yb + r) * nx + it * 64 + lane;
+        xin[r] = it * 64 + lane < nx;
+      }
+    } else {
+      q0 = (kt * 4 + w) * (int64_t)g.kz;
+      if (q0 >= g.nzl) continue;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        rv[r] = true;
+        off[r] = it * 64 * RB + 64 * r + lane;
+        xin[r] = off[r] < nx;
+      }
+    }
+    q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
+    S cur[RB], nxt[RB];
+    double ccu[RB], cnx[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const bool ld = xin[r] && rv[r];
+      const bool ldn = ld && g.z0 + q0 + 1 < g.npl;
+      cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
+      nxt[r] = ldn ? V[(q0 + 1) * P + off[r]] : zero<S>();
+      if constexpr (ANI) {
+        ccu[r] = ld ? C[q0 * P + off[r]] : 0.0;
+        cnx[r] = ldn ? C[(q0 + 1) * P + off[r]] : 0.0;
+      }
+    }
+    for (int64_t q = q0; q < q1; ++q) {
+      const int64_t gq = g.z0 + q;
+      // forward neighbours that live outside this wave's registers
+      S xe[RB], ye = zero<S>();
+      double cxe[RB], cye = 0.0;
+      bool eye = false;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        xe[r] = shfl_dn1(cur[r]);
+        if constexpr (ANI) cxe[r] = shfl_dn1(ccu[r]);
+      }
+      if constexpr (DIM == 3) {
+        // y+1 of the wave's last valid row: flat p + nx (covers the 3D y-wrap)
+        int rlast = 0;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) if (rv[r]) rlast = r;
+        const int64_t p = q * P + off[rlast];
+        const int64_t pg = gq * P + off[rlast];
+        eye = xin[rlast] && pg + nx < g.Ng;
+        ye = eye ? V[p + nx] : zero<S>();
+        if constexpr (ANI) cye = eye ? C[p + nx] : 0.0;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int64_t x = it * 64 + lane;
+          if (lane == 63) {
+            const bool e = rv[r] && x + 1 < nx;
+            xe[r] = e ? V[q * P + off[r] + 1] : zero<S>();
+            if constexpr (ANI) cxe[r] = e ? C[q * P + off[r] + 1] : 0.0;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const S c0 = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
+          double cc0 = 0.0;
+          if constexpr (ANI) cc0 = bcast(ccu[r + 1 < RB ? r + 1 : r], 0);
+          if (lane == 63) {
+            if (r + 1 < RB) {
+              xe[r] = c0;
+              if constexpr (ANI) cxe[r] = cc0;
+            } else {
+              const bool e = off[r] + 1 < nx;
+              xe[r] = e ? V[q * P + off[r] + 1] : zero<S>();
+              if constexpr (ANI) cxe[r] = e ? C[q * P + off[r] + 1] : 0.0;
+            }
+          }
+        }
+      }
+      // prefetch plane q+2
+      S nn[RB];
+      double cnn[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const bool ld = xin[r] && rv[r] && gq + 2 < g.npl && q + 2 < q1 + 1;
+        nn[r] = ld ? V[(q + 2) * P + off[r]] : zero<S>();
+        if constexpr (ANI) cnn[r] = ld ? C[(q + 2) * P + off[r]] : 0.0;
+      }
+      const bool bz = gq == 0 || gq == g.npl - 1;
+      const bool ez = gq + 1 < g.npl;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        if (!rv[r]) continue;
+        const int64_t x = DIM == 3 ? it * 64 + lane : off[r];
+        if (!xin[r]) continue;
+        const S c = cur[r];
+        const bool last = !(r + 1 < RB && rv[r + 1 < RB ? r + 1 : r]);
+        if constexpr (ANI) {
+          const double cc = ccu[r];
+          double acc = 0.0;
+          if (x + 1 < nx) acc += face_w(true, cc, cxe[r]) * abs2(c - xe[r]);
+          if constexpr (DIM == 3) {
+            const S yv = last ? ye : cur[r + 1 < RB ? r + 1 : r];
+            const double cy = last ? cye : ccu[r + 1 < RB ? r + 1 : r];
+            if (!last || eye) acc += face_w(true, cc, cy) * abs2(c - yv);
+          }
+          if (ez) acc += face_w(true, cc, cnx[r]) * abs2(c - nxt[r]);
+          n2 += abs2(c);
+          a -= g.s * acc;
+        } else {
+          S f = (x + 1 < nx) ? xe[r] : zero<S>();
+          if constexpr (DIM == 3) f = f + (last ? ye : cur[r + 1 < RB ? r + 1 : r]);
+          f = f + nxt[r];
+          const bool bnd = x == 0 || x == nx - 1 || bz ||
+                           (DIM == 3 && (yb + r == 0 || yb + r == g.nyp - 1));
+          const double c2 = abs2(c);
+          n2 += c2;
+          a += (bnd ? g.sd_bd : g.sd_in) * c2 + 2.0 * g.s * to_c(cj_mul(c, f)).re;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        cur[r] = nxt[r];
+        nxt[r] = nn[r];
+        if constexpr (ANI) {
+          ccu[r] = cnx[r];
+          cnx[r] = cnn[r];
+        }
+      }
+    }
+  }
+}
+
+template <class S, int DIM, bool ANI>
+__global__ __launch_bounds__(NTHREADS) void k_alpha(const S *__restrict__ V, Geo g, cplx *__restrict__ part) {
+  double a = 0.0, n2 = 0.0;
+  alpha_tiles<S, DIM, RB_ALPHA, ANI>(V, g, a, n2);
+  cplx v[2] = {{a, 0.0}, {n2, 0.0}};
+  block_store<2>(v, part);
+}
+
+// W_{J+1} = a * L W_J - sum_{k<=J} b_k W_k ;  partials g_k = W_k^H W_{J+1}, ||W_{J+1}||^2
+template <class S, int DIM, int J, bool ANI>
+__global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S *__restrict__ out,
+                                                     int64_t vs, Geo g,
+                                                     const KState *__restrict__ st,
+                                                     cplx *__restrict__ part) {
+  constexpr int NA = J + 2;
+  S acc[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) acc[k] = zero<S>();
+#if NLS_COEF_LDS
+  // Coefficients broadcast from LDS at every use (ds_read_b128, one address per
+  // wave): keeps 4(J+1) SGPRs free, which otherwise spill to VGPR lanes and cost
+  // ~90 v_readlane per cell row in the hot loop.  The empty asm with a memory
+  // clobber stops the compiler from hoisting the LDS reads back into registers.
+  __shared__ cplx cfs[MMAX + 2];
+  for (int k = threadIdx.x; k <= J + 1; k += NTHREADS) cfs[k] = st->coef[k];
+  __syncthreads();
+  const double a = cfs[J + 1].re;
+#define NLS_B(k) cfs[k]
+#define NLS_RELOAD() asm volatile("" ::: "memory")
+#else
+  cplx b[J + 1];
+#pragma unroll
+  for (int k = 0; k <= J; ++k) b[k] = st->coef[k];
+  const double a = st->coef[J + 1].re;
+#define NLS_B(k) b[k]
+#define NLS_RELOAD() ((void)0)
+#endif
+  const S *__restrict__ VJ = W + (int64_t)J * vs;
+  constexpr int RB = UpdRB<J>::v;
+  march<S, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
+    // every streamed load of every row first ...
+    S wk[RB][J > 0 ? J : 1];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const S *__restrict__ src = W + p[r];
+#pragma unroll
+      for (int k = 0; k < J; ++k) {
+        wk[r][k] = ok[r] ? ld_nt(src) : zero<S>();
+        src += vs;
+      }
+    }
+    NLS_RELOAD();
+    // ... then the CGS update, the store and the Gram / norm partial sums
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (!ok[r]) continue;
+      S X = a * lap[r] - coef_mul(NLS_B(J), cur[r]);
+#pragma unroll
+      for (int k = 0; k < J; ++k) X = X - coef_mul(NLS_B(k), wk[r][k]);
+      st_nt(out + p[r], X);
+#pragma unroll
+      for (int k = 0; k < J; ++k) acc[k] = acc[k] + cj_mul(wk[r][k], X);
+      acc[J] = acc[J] + cj_mul(cur[r], X);
+      acc[J + 1] = acc[J + 1] + from_real<S>(abs2(X));
+    }
+  });
+  cplx v[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) v[k] = to_c(acc[k]);
+  block_store<NA>(v, part);
+#undef NLS_B
+#undef NLS_RELOAD
+}
+
+#define NLS_J_LIST(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
+  X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) \
+  X(28) X(29) X(30)
+#define NLS_M_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) \
+  X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) \
+  X(29) X(30) X(31) X(32)
+
+}  // namespace nls

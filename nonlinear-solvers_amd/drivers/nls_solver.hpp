@@ -5,6 +5,9 @@
 //   nls::NLSESolverDevice   <- device/nlse_solver_dev.hpp:41-138 (+ CQ variant,
 //                              device/nlse_cq_solver.hpp:41-140)
 //   nls::SGESolverDevice    <- device/sg_solver_dev.hpp:92-294
+//   nls::g2::NLSESolverDevice <- nlsolvers/device/include/nlse_dev.hpp:66-361 (G2:
+//                              m(x) focusing field, div(c grad) operator, online
+//                              snapshots, apply_bc)
 //
 // Differences from the reference, by design: the Laplacian is described by the
 // grid (no CSR argument); snapshots are streamed to a callback/host buffer as
@@ -150,5 +153,56 @@ class SGESolverDevice {
   std::vector<double> u_, v_;
   uint32_t stored_ = 0;
 };
+
+namespace g2 {
+
+// G2 cubic NLSE stepper (nlsolvers/device/include/nlse_dev.hpp:66-361) as the
+// G2 drivers use it (nlse_cubic_driver_{2d,3d}.cpp): the caller stores
+// snapshot 0 with store_snapshot_online(), then per step i = 1 .. nt-1 calls
+// step(tau, i) -- which stores the (pre-BC) field when i % freq == 0 -- and
+// apply_bc().  The operator is div(c grad) built from c(x) (laplacians.hpp:
+// 54-103, 158-218); the C-ABI takes c itself instead of an assembled CSR.
+class NLSESolverDevice {
+ public:
+  struct Parameters {
+    uint32_t num_snapshots, snapshot_freq, krylov_dim;
+    Parameters(uint32_t ns = 100, uint32_t freq = 5, uint32_t m = 10)  // nlse_dev.hpp:66-75
+        : num_snapshots(ns), snapshot_freq(freq), krylov_dim(m) {}
+  };
+  using SnapshotFn = std::function<void(uint32_t index, const std::complex<double> *u, uint64_t n)>;
+
+  NLSESolverDevice(const Grid &g, const std::complex<double> *host_u0, const double *host_m,
+                   const double *host_c, const Parameters &p, SnapshotFn on_snapshot, int device = -1)
+      : h_(g, NLS_NLSE_G2, p.krylov_dim, device), p_(p), cb_(std::move(on_snapshot)), buf_(h_.n()) {
+    check(nls_set_field(h_.get(), reinterpret_cast<const double *>(host_u0), h_.n()), h_.get());
+    check(nls_set_coefficients(h_.get(), host_m, host_c, h_.n()), h_.get());
+  }
+
+  // nlse_dev.hpp:187-203 (the snapshot is taken before the driver's apply_bc)
+  void step(std::complex<double> tau, uint32_t step_number) {
+    check(nls_step(h_.get(), tau.imag(), 1), h_.get());
+    if (p_.snapshot_freq && step_number % p_.snapshot_freq == 0) store_snapshot_online();
+  }
+  void apply_bc() { check(nls_apply_bc(h_.get()), h_.get()); }  // nlse_dev.hpp:178-185
+
+  // nlse_dev.hpp:323-334: at most num_snapshots, silently ignored beyond
+  void store_snapshot_online() {
+    if (stored_ >= p_.num_snapshots) return;
+    check(nls_get_field(h_.get(), reinterpret_cast<double *>(buf_.data()), h_.n()), h_.get());
+    if (cb_) cb_(stored_, buf_.data(), h_.n());
+    ++stored_;
+  }
+  uint32_t snapshots_stored() const { return stored_; }
+  uint64_t n() const { return h_.n(); }
+
+ private:
+  Handle h_;
+  Parameters p_;
+  SnapshotFn cb_;
+  std::vector<std::complex<double>> buf_;
+  uint32_t stored_ = 0;
+};
+
+}  // namespace g2
 
 }  // namespace nls

@@ -14,12 +14,12 @@ import os
 import numpy as np
 
 __all__ = [
-    "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
+    "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "NLSE_G2", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
     "F_SINC2_SQRT", "F_ID_SQRT", "F_SINC2_HALF", "MAX_KRYLOV", "NlsError", "Config", "Solver",
     "lib", "lib_path", "rccl_unique_id", "EXPORTED_SYMBOLS",
 ]
 
-NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI = 0, 1, 2
+NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI, NLSE_G2 = 0, 1, 2, 3
 F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF = range(7)
 MAX_KRYLOV = 32
 
@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = (
     "nls_local_planes", "nls_set_field", "nls_set_sg_state", "nls_step", "nls_sync",
     "nls_get_field", "nls_get_sg_velocity", "nls_krylov_apply", "nls_laplacian_apply",
     "nls_rccl_unique_id", "nls_group_create", "nls_group_destroy", "nls_set_timing",
-    "nls_get_timing", "nls_reset_timing",
+    "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
 )
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -91,6 +91,8 @@ def lib():
     L.nls_set_field.argtypes = [H, dp, C.c_uint64]
     L.nls_set_sg_state.argtypes = [H, dp, dp, dp, C.c_uint64]
     L.nls_step.argtypes = [H, C.c_double, C.c_uint32]
+    L.nls_set_coefficients.argtypes = [H, dp, dp, C.c_uint64]
+    L.nls_apply_bc.argtypes = [H]
     L.nls_sync.argtypes = [H]
     L.nls_get_field.argtypes = [H, dp, C.c_uint64]
     L.nls_get_sg_velocity.argtypes = [H, C.c_double, dp, C.c_uint64]
@@ -148,7 +150,8 @@ def _dptr(a: np.ndarray):
 class Solver:
     """One device handle (nls_handle).
 
-    equation: NLSE_CUBIC / NLSE_CQ (complex128 fields) or SG_GAUTSCHI (float64).
+    equation: NLSE_CUBIC / NLSE_CQ / NLSE_G2 (complex128 fields) or SG_GAUTSCHI (float64).
+    NLSE_G2 (nlsolvers/device/include/nlse_dev.hpp) also needs set_coefficients(m, c).
     Grid: dim 2 -> (ny, nx), dim 3 -> (nz, ny, nx); dx, dy as the reference
     drivers compute them (dx = 2 Lx / (nx - 1)).
     """
@@ -224,6 +227,15 @@ class Solver:
     def set_sg_state(self, u, u_past, mfield):
         a, b, c = self._in(u, np.float64), self._in(u_past, np.float64), self._in(mfield, np.float64)
         self._call(lib().nls_set_sg_state, _dptr(a), _dptr(b), _dptr(c), self.n_local)
+
+    def set_coefficients(self, mfield, cfield):
+        """G2: focusing field m(x) and anisotropy c(x) of div(c grad u) (local slab)."""
+        a, b = self._in(mfield, np.float64), self._in(cfield, np.float64)
+        self._call(lib().nls_set_coefficients, _dptr(a), _dptr(b), self.n_local)
+
+    def apply_bc(self):
+        """Neumann copy BC of the G2 drivers (boundaries.cuh:10-81)."""
+        self._call(lib().nls_apply_bc)
 
     def step(self, dt, nsteps=1):
         self._call(lib().nls_step, float(dt), int(nsteps))

@@ -77,6 +77,59 @@ struct StencilOp {
   template <class S> void apply(const S *x, S *y) const { lap_apply(G, x, y); }
 };
 
+// Matrix-free restatement of the G2 anisotropic builders
+// build_anisotropic_laplacian_noflux (nlsolvers/common/include/laplacians.hpp:54-103)
+// and build_anisotropic_laplacian_noflux_3d (:158-218), called by the G2
+// drivers with nx-2, ny-2(, nz-2) so the operator spans the full grid
+// (nlse_cubic_driver_3d.cpp:103-106):
+//   x     (i, i+1) unless (i+1) % nx == 0, weight (c_i + c_{i+1}) / 2.0   (:183-191)
+//   "y"   (i, i+nx) for every i < N - nx (3D: the same y-wrap as the
+//         isotropic builder), weight (c_i + c_{i+nx}) / 2.0             (:193-199)
+//   z     (i, i+P) (3D)                                                   (:201-207)
+//   diag  -diagonal_sums[i], accumulated in the loop order above          (:209-211)
+//   L *= 1/(dx*dy) (2D, :101) or 1/(dx*dx) (3D, :216)
+// Row idx is evaluated in Eigen's column order like lap_apply.
+template <class S>
+void lap_aniso_apply(const Grid &G, const double *c, const S *x, S *y) {
+  const uint64_t nx = G.nx, N = G.N, P = G.nx * G.ny;
+  const double s = G.scale;
+  for (uint64_t idx = 0; idx < N; ++idx) {
+    const uint64_t i = idx % nx;
+    const bool ezm = G.dim == 3 && idx >= P, ezp = G.dim == 3 && idx + P < N;
+    const bool eym = idx >= nx, eyp = idx + nx < N;
+    const bool exm = i > 0, exp_ = i + 1 < nx;
+    const double wzm = ezm ? (c[idx - P] + c[idx]) / 2.0 : 0.0;
+    const double wzp = ezp ? (c[idx] + c[idx + P]) / 2.0 : 0.0;
+    const double wym = eym ? (c[idx - nx] + c[idx]) / 2.0 : 0.0;
+    const double wyp = eyp ? (c[idx] + c[idx + nx]) / 2.0 : 0.0;
+    const double wxm = exm ? (c[idx - 1] + c[idx]) / 2.0 : 0.0;
+    const double wxp = exp_ ? (c[idx] + c[idx + 1]) / 2.0 : 0.0;
+    double ds = 0.0;  // diagonal_sums[idx] in the builder's accumulation order
+    if (exm) ds += wxm;
+    if (exp_) ds += wxp;
+    if (eym) ds += wym;
+    if (eyp) ds += wyp;
+    if (ezm) ds += wzm;
+    if (ezp) ds += wzp;
+    S acc = S(0);
+    if (ezm) acc += (wzm * s) * x[idx - P];
+    if (eym) acc += (wym * s) * x[idx - nx];
+    if (exm) acc += (wxm * s) * x[idx - 1];
+    acc += (-ds * s) * x[idx];
+    if (exp_) acc += (wxp * s) * x[idx + 1];
+    if (eyp) acc += (wyp * s) * x[idx + nx];
+    if (ezp) acc += (wzp * s) * x[idx + P];
+    y[idx] = acc;
+  }
+}
+
+struct AnisoOp {
+  Grid G;
+  const double *c;
+  uint64_t n() const { return G.N; }
+  template <class S> void apply(const S *x, S *y) const { lap_aniso_apply(G, c, x, y); }
+};
+
 struct CsrOp {
   uint64_t N;
   const int64_t *rp, *ci;
@@ -289,6 +342,45 @@ void nonlin_half(cd *u, uint64_t n, double dt, int nonlin, const double *sg) {
   }
 }
 
+// G2 nonlinear half step (nlsolvers/device/include/nlse_dev.hpp:20-40):
+//   rho = m * (re^2 + im^2);  out = in * exp(0.5*tau * rho),  tau = 1j*dt
+void nonlin_half_g2(cd *u, const double *mf, uint64_t n, double dt) {
+  const cd ht = 0.5 * cd(0.0, dt);
+  for (uint64_t p = 0; p < n; ++p) {
+    const double rho = mf[p] * (u[p].real() * u[p].real() + u[p].imag() * u[p].imag());
+    u[p] = u[p] * std::exp(ht * cd(rho, 0.0));
+  }
+}
+
+// neumann_bc_no_velocity_blocking{,_3d} (nlsolvers/device/include/boundaries.cuh:10-19,
+// :24-81), the strided copies in the reference's order.  The reference indexes
+// u[a*n^2 + b*n + c] (a slowest) on cubic grids; here a = z, b = y, c = x of
+// the [nz][ny][nx] layout with per-axis extents (2D: a = y, b = x).
+template <class S> void neumann_bc(const Grid &G, S *u) {
+  const uint64_t nx = G.nx, ny = G.ny, nz = G.nz;
+  auto at3 = [&](uint64_t a, uint64_t b, uint64_t c) -> S & { return u[(a * ny + b) * nx + c]; };
+  if (G.dim == 2) {
+    auto at2 = [&](uint64_t a, uint64_t b) -> S & { return u[a * nx + b]; };
+    for (uint64_t b = 1; b + 1 < nx; ++b) at2(0, b) = at2(1, b);             // :12-13
+    for (uint64_t b = 1; b + 1 < nx; ++b) at2(ny - 1, b) = at2(ny - 2, b);   // :14-15
+    for (uint64_t a = 0; a < ny; ++a) at2(a, 0) = at2(a, 1);                 // :16-17
+    for (uint64_t a = 0; a < ny; ++a) at2(a, nx - 1) = at2(a, nx - 2);       // :18-19
+    return;
+  }
+  for (uint64_t b = 1; b + 1 < ny; ++b)  // x-min / x-max of the reference (:28-45)
+    for (uint64_t c = 1; c + 1 < nx; ++c) at3(0, b, c) = at3(1, b, c);
+  for (uint64_t b = 1; b + 1 < ny; ++b)
+    for (uint64_t c = 1; c + 1 < nx; ++c) at3(nz - 1, b, c) = at3(nz - 2, b, c);
+  for (uint64_t a = 0; a < nz; ++a)  // y-min / y-max (:47-63)
+    for (uint64_t c = 1; c + 1 < nx; ++c) at3(a, 0, c) = at3(a, 1, c);
+  for (uint64_t a = 0; a < nz; ++a)
+    for (uint64_t c = 1; c + 1 < nx; ++c) at3(a, ny - 1, c) = at3(a, ny - 2, c);
+  for (uint64_t a = 0; a < nz; ++a)  // z-min / z-max (:65-81)
+    for (uint64_t b = 0; b < ny; ++b) at3(a, b, 0) = at3(a, b, 1);
+  for (uint64_t a = 0; a < nz; ++a)
+    for (uint64_t b = 0; b < ny; ++b) at3(a, b, nx - 1) = at3(a, b, nx - 2);
+}
+
 }  // namespace
 
 extern "C" {
@@ -373,6 +465,59 @@ int oracle_nlse_steps(const oracle_grid *g, double *u_, double dt,
     krylov_apply(op, rho.data(), -tau, m, ORACLE_F_EXP_ABS, buf.data());
     nonlin_half(buf.data(), n, dt, nonlin, sigma);
     std::memcpy(u, buf.data(), n * sizeof(cd));
+  }
+  return 0;
+}
+
+int oracle_laplacian_aniso_apply_c(const oracle_grid *g, const double *c, const double *x,
+                                   double *y) {
+  Grid G;
+  if (!make_grid(g, G) || !c || !x || !y) return -1;
+  lap_aniso_apply(G, c, as_c(x), as_c(y));
+  return 0;
+}
+
+int oracle_krylov_aniso_c(const oracle_grid *g, const double *c, const double *u,
+                          double t_re, double t_im, uint32_t m, int func, double *out) {
+  Grid G;
+  if (!make_grid(g, G) || !c || m < 1) return -1;
+  AnisoOp op{G, c};
+  krylov_apply(op, as_c(u), cd(t_re, t_im), m, func, as_c(out));
+  return 0;
+}
+
+int oracle_neumann_bc_c(const oracle_grid *g, double *u) {
+  Grid G;
+  if (!make_grid(g, G) || !u) return -1;
+  if (G.nx < 3 || G.ny < 3 || (G.dim == 3 && G.nz < 3)) return -1;
+  neumann_bc(G, as_c(u));
+  return 0;
+}
+
+// G2 NLSESolverDevice::step (nlsolvers/device/include/nlse_dev.hpp:187-203),
+// tau = 1j*dt: u <- N(exp(tau L) N(u)) with N(v) = v exp(tau/2 m|v|^2) and
+// the G2 matrix function exp(t*lambda), t = +tau, Q f Q^H
+// (nlsolvers/device/include/matfunc_complex.hpp:254-375); the G2 Lanczos is
+// the G1 device one (rounding-level equal to this MGS restatement).  With
+// bc != 0 the driver's apply_bc() follows every step
+// (nlse_cubic_driver_3d.cpp:116-119).
+int oracle_nlse_g2_steps(const oracle_grid *g, const double *c, const double *mfield,
+                         double *u_, double dt, uint32_t nsteps, uint32_t m, int bc) {
+  Grid G;
+  if (!make_grid(g, G) || !c || !mfield || m < 1) return -1;
+  if (bc && (G.nx < 3 || G.ny < 3 || (G.dim == 3 && G.nz < 3))) return -1;
+  AnisoOp op{G, c};
+  const uint64_t n = G.N;
+  cd *u = as_c(u_);
+  std::vector<cd> buf(u, u + n), out(n);
+  const cd tau(0.0, dt);
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    std::memcpy(buf.data(), u, n * sizeof(cd));
+    nonlin_half_g2(buf.data(), mfield, n, dt);
+    krylov_apply(op, buf.data(), tau, m, ORACLE_F_EXP, out.data());
+    nonlin_half_g2(out.data(), mfield, n, dt);
+    std::memcpy(u, out.data(), n * sizeof(cd));
+    if (bc) neumann_bc(G, u);
   }
   return 0;
 }

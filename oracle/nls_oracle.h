@@ -8,6 +8,11 @@
  *   nlse_solver.hpp:53-77            (Strang SS2 cubic NLSE step)
  *   device/nlse_cq_solver.hpp:16-39  (cubic-quintic density, G1 device semantics)
  *   sg_solver.hpp:53-74              (sine-Gordon Gautschi step)
+ * and of the G2 3D/2D device stepper behind nlse_cubic_driver_{2d,3d}.cpp:
+ *   nlsolvers/common/include/laplacians.hpp:54-103,158-218 (anisotropic div(c grad))
+ *   nlsolvers/device/include/nlse_dev.hpp:20-40,187-203     (m|u|^2, +tau/2, exp(tau L))
+ *   nlsolvers/device/include/matfunc_complex.hpp:254-375     (exp(t*lambda), Q f Q^H)
+ *   nlsolvers/device/include/boundaries.cuh:10-81            (Neumann copy BC)
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
  * load this library.  The product path (libnls_amd.so) never links it.
@@ -69,6 +74,20 @@ int oracle_krylov_csr_r(uint64_t n, const int64_t *rowptr, const int64_t *col,
 int oracle_nlse_steps(const oracle_grid *g, double *u, double dt,
                       uint32_t nsteps, uint32_t m, int nonlin,
                       const double *sigma);
+
+/* G2: anisotropic operator with coefficient field c (real, N cells) */
+int oracle_laplacian_aniso_apply_c(const oracle_grid *g, const double *c,
+                                   const double *x, double *y);
+int oracle_krylov_aniso_c(const oracle_grid *g, const double *c, const double *u,
+                          double t_re, double t_im, uint32_t m, int func,
+                          double *out);
+/* G2 Neumann copy boundary condition, in place (needs >= 3 cells per axis) */
+int oracle_neumann_bc_c(const oracle_grid *g, double *u);
+/* G2 SS2 steps (tau = 1j*dt) with focusing field m and anisotropy c; bc != 0
+ * applies the Neumann copy BC after every step. */
+int oracle_nlse_g2_steps(const oracle_grid *g, const double *c,
+                         const double *mfield, double *u, double dt,
+                         uint32_t nsteps, uint32_t m, int bc);
 
 /* sine-Gordon Gautschi (sg_solver.hpp:53-74); u, u_past updated in place. */
 int oracle_sg_steps(const oracle_grid *g, double *u, double *u_past,

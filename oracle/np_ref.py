@@ -8,7 +8,8 @@ anisotropic builder used by the reference's scipy known-answer test.
 
 Reference lines followed:
   laplacians.hpp:10-52 / :55-105          build_laplacian_noflux{,_3d}
-  nlsolvers/common/include/laplacians.hpp:158-218   anisotropic 3D (c-field)
+  nlsolvers/common/include/laplacians.hpp:54-103, 158-218   anisotropic 2D/3D (c-field)
+  nlsolvers/device/include/nlse_dev.hpp:187-203, boundaries.cuh:10-81   G2 step + BC
   eigen_krylov_complex.hpp:10-84          lanczos_L + expm_multiply (|lambda|)
   eigen_krylov_real.hpp:5-201             real Lanczos + cos/sinc^2/id filters
   nlse_solver.hpp:53-77                   Strang SS2 step
@@ -91,6 +92,57 @@ def aniso_laplacian_3d(n: int, dx: float, c: np.ndarray) -> sp.csr_matrix:
     A = sp.coo_matrix((np.concatenate(v), (np.concatenate(r), np.concatenate(cc))), shape=(N, N)).tocsr()
     A.sum_duplicates()
     return A * (1.0 / (dx * dx))
+
+
+def aniso_laplacian(dim: int, nx: int, ny: int, nz: int, dx: float, dy: float,
+                    c: np.ndarray) -> sp.csr_matrix:
+    """build_anisotropic_laplacian_noflux{,_3d} on a general grid
+    (nlsolvers/common/include/laplacians.hpp:54-103 for 2D, :158-218 for 3D):
+    fast-axis couplings (i, i+1) unless (i+1) % nx == 0, flat (i, i+nx) for
+    i < N - nx, and (3D) (i, i+P); weight (c_a + c_b)/2, diagonal -sum."""
+    P = nx * ny
+    N = P * (nz if dim == 3 else 1)
+    c = np.asarray(c, dtype=np.float64).ravel()
+    assert c.size == N
+    diag = np.zeros(N)
+    r, cc, v = [], [], []
+    idx = np.arange(N - 1)
+    i0 = idx[(idx + 1) % nx != 0]
+    a = (c[i0] + c[i0 + 1]) / 2.0
+    r += [i0, i0 + 1]; cc += [i0 + 1, i0]; v += [a, a]
+    np.add.at(diag, i0, a); np.add.at(diag, i0 + 1, a)
+    for off in ((nx, P) if dim == 3 else (nx,)):
+        i0 = np.arange(N - off)
+        a = (c[i0] + c[i0 + off]) / 2.0
+        r += [i0, i0 + off]; cc += [i0 + off, i0]; v += [a, a]
+        np.add.at(diag, i0, a); np.add.at(diag, i0 + off, a)
+    r.append(np.arange(N)); cc.append(np.arange(N)); v.append(-diag)
+    A = sp.coo_matrix((np.concatenate(v), (np.concatenate(r), np.concatenate(cc))), shape=(N, N)).tocsr()
+    A.sum_duplicates()
+    return A * (1.0 / (dx * dy) if dim == 2 else 1.0 / (dx * dx))
+
+
+def neumann_bc(dim, nx, ny, nz, u):
+    """Neumann copy BC (nlsolvers/device/include/boundaries.cuh:10-81) as the
+    clamp gather it amounts to: u[k, j, i] <- u[clamp(k), clamp(j), clamp(i)]
+    with every index clamped into [1, n-2]."""
+    u = np.asarray(u).reshape(_shape(dim, nx, ny, nz)).copy()
+    idx = [np.clip(np.arange(n), 1, n - 2) for n in u.shape]
+    return u[np.ix_(*idx)].ravel()
+
+
+def nlse_g2_steps(dim, nx, ny, nz, dx, dy, c, mfield, u, dt, nsteps, m, bc=True):
+    """G2 SS2 (nlsolvers/device/include/nlse_dev.hpp:187-203) + driver BC."""
+    A = aniso_laplacian(dim, nx, ny, nz, dx, dy, c)
+    mf = np.asarray(mfield, dtype=np.float64).ravel()
+    u = np.asarray(u, dtype=np.complex128).ravel().copy()
+    N = lambda v: v * np.exp(0.5 * 1j * dt * (mf * (v.real * v.real + v.imag * v.imag)))
+    for _ in range(nsteps):
+        b = krylov(lambda v: A @ v, N(u), 1j * dt, m, F_EXP)
+        u = N(b)
+        if bc:
+            u = neumann_bc(dim, nx, ny, nz, u)
+    return u
 
 
 def laplacian_apply(dim, nx, ny, nz, dx, dy, x):

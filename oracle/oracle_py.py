@@ -41,6 +41,12 @@ def lib():
         L.oracle_nlse_steps.argtypes = [g, dp, C.c_double, C.c_uint32, C.c_uint32, C.c_int,
                                         C.POINTER(C.c_double)]
         L.oracle_sg_steps.argtypes = [g, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32]
+        L.oracle_laplacian_aniso_apply_c.argtypes = [g, dp, dp, dp]
+        L.oracle_krylov_aniso_c.argtypes = [g, dp, dp, C.c_double, C.c_double, C.c_uint32, C.c_int,
+                                            dp]
+        L.oracle_neumann_bc_c.argtypes = [g, dp]
+        L.oracle_nlse_g2_steps.argtypes = [g, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
+                                           C.c_int]
     return _LIB
 
 
@@ -116,3 +122,35 @@ def sg_steps(g, u, u_past, mfield, dt, nsteps, m):
     mf = np.ascontiguousarray(mfield, dtype=np.float64).ravel()
     _check(lib().oracle_sg_steps(C.byref(g), u, up, mf, dt, nsteps, m))
     return u, up
+
+
+def _r(a):
+    return np.ascontiguousarray(a, dtype=np.float64).ravel()
+
+
+def laplacian_aniso_c(g, c, x):
+    """G2 div(c grad) operator (nlsolvers/common/include/laplacians.hpp:54-218)."""
+    xi = _c(x)
+    out = np.zeros_like(xi)
+    _check(lib().oracle_laplacian_aniso_apply_c(C.byref(g), _r(c), xi, out))
+    return out.view(np.complex128)
+
+
+def krylov_aniso_c(g, c, u, t, m, func=1):
+    ui = _c(u)
+    out = np.zeros_like(ui)
+    t = complex(t)
+    _check(lib().oracle_krylov_aniso_c(C.byref(g), _r(c), ui, t.real, t.imag, m, func, out))
+    return out.view(np.complex128)
+
+
+def neumann_bc(g, u):
+    ui = _c(u).copy()
+    _check(lib().oracle_neumann_bc_c(C.byref(g), ui))
+    return ui.view(np.complex128)
+
+
+def nlse_g2_steps(g, c, mfield, u, dt, nsteps, m, bc=True):
+    ui = _c(u).copy()
+    _check(lib().oracle_nlse_g2_steps(C.byref(g), _r(c), _r(mfield), ui, dt, nsteps, m, 1 if bc else 0))
+    return ui.view(np.complex128)

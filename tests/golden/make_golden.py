@@ -93,6 +93,21 @@ def main():
     lap = O.laplacian_c(g, uc)
     cases["krylov3d"] = dict(dim=3, n=n, dx=dx, m=12, ur=ur, uc=uc, lap=lap,
                              **{"r_" + k: v for k, v in kr.items()}, **{"c_" + k: v for k, v in kc.items()})
+    # --- G2 cubic NLSE with m(x), c(x) and the Neumann copy BC -----------------
+    #     (nlse_cubic_driver_3d.cpp: m=25; nlse_cubic_driver_2d.cpp: m=20)
+    for name, dim, n, m, steps in (("g2_3d", 3, 12, 25, 5), ("g2_2d", 2, 24, 20, 10)):
+        L = 4.0
+        dx = 2 * L / (n - 1)
+        rng = np.random.default_rng(7 + dim)
+        u0 = field(dim, n, L, 10 + dim)
+        N = u0.size
+        cf = 1.0 + 0.5 * np.sin(np.arange(N) * 0.37) + 0.1 * rng.random(N)
+        mf = 1.0 + 0.3 * rng.standard_normal(N)
+        g = O.grid(dim, n, n, n, dx, dx)
+        out = O.nlse_g2_steps(g, cf, mf, u0, dt, steps, m, bc=True)
+        tw = np_ref.nlse_g2_steps(dim, n, n, n, dx, dx, cf, mf, u0, dt, steps, m, bc=True)
+        assert np.linalg.norm(out - tw) / np.linalg.norm(tw) < 1e-12
+        cases[name] = dict(dim=dim, n=n, dx=dx, dt=dt, steps=steps, m=m, u0=u0, c=cf, mfield=mf, u=out)
     for name, d in cases.items():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **{k: np.asarray(v) for k, v in d.items()})
     total = sum(os.path.getsize(os.path.join(HERE, f"{k}.npz")) for k in cases)

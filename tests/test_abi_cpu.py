@@ -48,14 +48,19 @@ def test_config_default_matches_reference_defaults():
 @pytest.mark.parametrize("kw,msg", [
     (dict(m=0), "krylov_m"), (dict(m=33), "krylov_m"), (dict(dim=4), "dim"),
     (dict(nx=1), "grid too small"), (dict(dx=0.0), "dx"), (dict(nranks=2), "rccl_id"),
+    (dict(equation=4), "unknown equation"), (dict(equation=3, nx=2), "G2 NLSE needs >= 3"),
+    (dict(equation=3, dim=3, nz=3, nranks=2, group=True), "2 planes per rank"),
 ])
 def test_invalid_config_rejected_before_device(kw, msg):
     base = dict(dim=2, nx=16, ny=16, nz=1, dx=0.5)
     base.update(kw)
     m = base.pop("m", 10)
     nranks = base.pop("nranks", 1)
+    eq = base.pop("equation", 0)
+    grp = nls_amd.Group(nranks) if base.pop("group", False) else None
     with pytest.raises(nls_amd.NlsError) as e:
-        nls_amd.Solver(base["dim"], base["nx"], base["ny"], base["nz"], base["dx"], m=m, nranks=nranks)
+        nls_amd.Solver(base["dim"], base["nx"], base["ny"], base["nz"], base["dx"], m=m, nranks=nranks,
+                       equation=eq, group=grp)
     assert e.value.code == -1 and msg in str(e.value)
 
 
@@ -117,3 +122,43 @@ def test_npy_codec_rejects_wrong_dtype(tmp_path):
     np.save(f, np.zeros((3, 3), np.float32))
     r = run([os.path.join(BIN, "npy_tool"), "copy-c16", str(f), str(tmp_path / "b.npy")])
     assert r.returncode == 1 and "dtype" in r.stderr
+
+
+# ---- G2 drivers (nlse_3d_dev / nlse_2d_dev): argv and input contract, no GPU needed
+
+
+@pytest.mark.parametrize("prog,npos", [("nlse_3d_dev", 13), ("nlse_2d_dev", 11)])
+def test_g2_driver_usage(prog, npos):
+    for k in (0, npos - 2, npos - 1, npos + 1):   # nlse_cubic_driver_3d.cpp:20-31 (argc != 14)
+        r = run([os.path.join(BIN, prog)] + ["8"] * k)
+        assert r.returncode == 1 and "Usage:" in r.stderr and "input_m.npy input_c.npy" in r.stderr
+
+
+def _g2_files(tmp_path, ushape, mshape, cshape):
+    paths = []
+    for name, shp, dt in (("u0", ushape, complex), ("m", mshape, float), ("c", cshape, float)):
+        f = tmp_path / f"{name}.npy"
+        np.save(f, np.ones(shp, dt))
+        paths.append(str(f))
+    return paths
+
+
+def test_g2_driver_shape_checks(tmp_path):
+    exe = os.path.join(BIN, "nlse_3d_dev")
+    out = str(tmp_path / "o.npy")
+    u, mf, cf = _g2_files(tmp_path, (6, 5, 4), (6, 5, 4), (6, 5, 4))
+    r = run([exe, "4", "5", "7", "2", "2", "2", u, out, "1", "10", "5", mf, cf])
+    assert r.returncode == 1 and "Input array dimensions mismatch" in r.stderr
+    u, mf, cf = _g2_files(tmp_path, (6, 5, 4), (6, 5, 3), (6, 5, 4))
+    r = run([exe, "4", "5", "6", "2", "2", "2", u, out, "1", "10", "5", mf, cf])
+    assert r.returncode == 1 and "Coupling array dimensions mismatch" in r.stderr and "Faulty m" in r.stderr
+    u, mf, cf = _g2_files(tmp_path, (6, 5, 4), (6, 5, 4), (5, 4))
+    r = run([exe, "4", "5", "6", "2", "2", "2", u, out, "1", "10", "5", mf, cf])
+    assert r.returncode == 1 and "Faulty c" in r.stderr
+    u, mf, cf = _g2_files(tmp_path, (6, 5, 4), (6, 5, 4), (6, 5, 4))
+    r = run([exe, "4", "5", "6", "2", "2", "2", u, out, "1", "3", "5", mf, cf])
+    assert r.returncode == 1 and "num_snapshots" in r.stderr
+    # 2D: the reference checks [nx, ny] (nlse_cubic_driver_2d.cpp:49-56)
+    u, mf, cf = _g2_files(tmp_path, (6, 6), (6, 6), (6, 5))
+    r = run([os.path.join(BIN, "nlse_2d_dev"), "6", "6", "2", "2", u, out, "1", "10", "5", mf, cf])
+    assert r.returncode == 1 and "Faulty c" in r.stderr

@@ -1,0 +1,235 @@
+"""GPU parity of the G2 stepper (nlsolvers/device/include/nlse_dev.hpp behind
+nlse_cubic_driver_{2d,3d}.cpp) against the CPU oracle, through the C-ABI.
+
+G2 differs from G1 in every part of the step: the
+operator is div(c grad) with face-averaged c (laplacians.hpp:54-218), the
+nonlinear phase is exp(+tau/2 m(x)|u|^2), the linear flow is exp(tau*lambda)
+(no |.|), and the drivers apply the Neumann copy BC after every step.
+
+Tolerances: stencil apply <= 1e-14, one Krylov action <= 1e-12, trajectories
+<= 1e-10 (north_star's bound), BC bit-exact (it is a copy).
+"""
+import os
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+nls_amd = pytest.importorskip("nls_amd")
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BIN = os.path.join(os.path.dirname(HERE), "nonlinear-solvers_amd", "bin")
+GOLD = os.path.join(HERE, "golden")
+TOL_OP, TOL_KRYLOV, TOL_TRAJ = 1e-14, 1e-12, 1e-10
+
+
+def fields(dim, nx, ny, nz, seed=0, L=4.0):
+    """u0 (a few Gaussian bumps + noise), m(x) > 0 focusing, c(x) in [0.5, 1.5]."""
+    rng = np.random.default_rng(seed)
+    shp = (ny, nx) if dim == 2 else (nz, ny, nx)
+    axes = [np.linspace(-L, L, s) for s in shp]
+    grids = np.meshgrid(*axes, indexing="ij")
+    r2 = sum(g * g for g in grids)
+    u = np.exp(-r2) * np.exp(1j * grids[-1]) + 0.4 * np.exp(-sum((g - 1.0) ** 2 for g in grids))
+    u = u.ravel() + 1e-3 * (rng.standard_normal(u.size) + 1j * rng.standard_normal(u.size))
+    c = 1.0 + 0.5 * np.sin(0.7 * grids[-1] + 0.3 * grids[0]).ravel() * rng.uniform(0.5, 1.0, u.size)
+    mf = 1.0 + 0.5 * np.cos(grids[0]).ravel()
+    return u, mf, c
+
+
+GRIDS = [  # (dim, nx, ny, nz)
+    (2, 32, 32, 1),
+    (2, 300, 20, 1),     # two partial x-tiles
+    (2, 7, 5, 1),
+    (3, 12, 12, 12),
+    (3, 70, 9, 11),      # partial x / y tiles, several z chunks, y-wrap across planes
+    (3, 5, 6, 3),
+]
+
+
+def solver(dim, nx, ny, nz, dx, m, **kw):
+    return nls_amd.Solver(dim, nx, ny, nz, dx, dx, equation=nls_amd.NLSE_G2, m=m, **kw)
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", GRIDS)
+def test_aniso_laplacian_matches_oracle(dim, nx, ny, nz):
+    dx = 0.37
+    u, mf, c = fields(dim, nx, ny, nz, seed=1)
+    g = O.grid(dim, nx, ny, nz, dx, dx)
+    ref = O.laplacian_aniso_c(g, c, u)
+    with solver(dim, nx, ny, nz, dx, 4) as s:
+        s.set_coefficients(mf, c)
+        y = s.laplacian(u)
+    assert rel_l2(y, ref) <= TOL_OP
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", GRIDS)
+@pytest.mark.parametrize("m", [1, 2, 10, 25])
+def test_g2_exp_action_matches_oracle(dim, nx, ny, nz, m):
+    """exp(t*lambda) with t = +1j*dt (nlsolvers/device/include/matfunc_complex.hpp:281-287)."""
+    dx = 8.0 / (nx - 1)
+    u, mf, c = fields(dim, nx, ny, nz, seed=2)
+    g = O.grid(dim, nx, ny, nz, dx, dx)
+    m = min(m, nx * ny * nz)
+    with solver(dim, nx, ny, nz, dx, m) as s:
+        s.set_coefficients(mf, c)
+        for t in (1e-3j, 1e-2j):
+            ref = O.krylov_aniso_c(g, c, u, t, m, nls_amd.F_EXP)
+            assert rel_l2(s.krylov_apply(u, t, nls_amd.F_EXP), ref) <= TOL_KRYLOV
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", GRIDS)
+def test_neumann_bc_bit_exact(dim, nx, ny, nz):
+    u, mf, c = fields(dim, nx, ny, nz, seed=3)
+    g = O.grid(dim, nx, ny, nz, 0.5, 0.5)
+    with solver(dim, nx, ny, nz, 0.5, 4) as s:
+        s.set_coefficients(mf, c)
+        s.set_field(u)
+        s.apply_bc()
+        assert np.array_equal(s.get_field(), O.neumann_bc(g, u))
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,m", [(2, 32, 32, 1, 20), (2, 300, 20, 1, 20), (3, 12, 12, 12, 25),
+                                            (3, 70, 9, 11, 25), (3, 16, 16, 16, 10)])
+def test_g2_trajectory_with_bc_matches_oracle(dim, nx, ny, nz, m):
+    """The driver loop (nlse_cubic_driver_3d.cpp:116-119): step, then apply_bc."""
+    L, dt, steps = 4.0, 1e-3, 12
+    dx = 2 * L / (nx - 1)
+    u, mf, c = fields(dim, nx, ny, nz, seed=4)
+    g = O.grid(dim, nx, ny, nz, dx, dx)
+    ref = O.nlse_g2_steps(g, c, mf, u, dt, steps, m, bc=True)
+    ref_nobc = O.nlse_g2_steps(g, c, mf, u, dt, steps, m, bc=False)
+    with solver(dim, nx, ny, nz, dx, m) as s:
+        s.set_coefficients(mf, c)
+        s.set_field(u)
+        for _ in range(steps):
+            s.step(dt, 1)
+            s.apply_bc()
+        out = s.get_field()
+        s.set_field(u)
+        s.step(dt, steps)
+        out_nobc = s.get_field()
+    assert rel_l2(out, ref) <= TOL_TRAJ
+    assert rel_l2(out_nobc, ref_nobc) <= TOL_TRAJ
+
+
+def test_g2_snapshot_is_pre_bc():
+    """step() stores the snapshot before the driver's apply_bc (nlse_dev.hpp:195-197)."""
+    dim, n, m, dt = 3, 10, 12, 1e-3
+    dx = 0.8
+    u, mf, c = fields(dim, n, n, n, seed=5)
+    g = O.grid(dim, n, n, n, dx, dx)
+    with solver(dim, n, n, n, dx, m) as s:
+        s.set_coefficients(mf, c)
+        s.set_field(u)
+        s.step(dt, 1)
+        pre = s.get_field()
+        s.apply_bc()
+        post = s.get_field()
+        s.step(dt, 1)
+        nxt = s.get_field()
+    ref_pre = O.nlse_g2_steps(g, c, mf, u, dt, 1, m, bc=False)
+    assert rel_l2(pre, ref_pre) <= TOL_TRAJ
+    assert np.array_equal(post, O.neumann_bc(g, pre))
+    assert rel_l2(nxt, O.nlse_g2_steps(g, c, mf, O.neumann_bc(g, ref_pre), dt, 1, m, bc=False)) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("name", ["g2_3d", "g2_2d"])
+def test_g2_golden_fixture(name):
+    d = np.load(os.path.join(GOLD, f"{name}.npz"))
+    n, dim, m, dt = int(d["n"]), int(d["dim"]), int(d["m"]), float(d["dt"])
+    with solver(dim, n, n, n, float(d["dx"]), m) as s:
+        s.set_coefficients(d["mfield"], d["c"])
+        s.set_field(d["u0"])
+        for _ in range(int(d["steps"])):
+            s.step(dt, 1)
+            s.apply_bc()
+        assert rel_l2(s.get_field(), d["u"]) <= TOL_TRAJ
+
+
+def test_g2_state_errors():
+    with solver(3, 8, 8, 8, 0.5, 4) as s:
+        s.set_field(np.ones(512, complex))
+        with pytest.raises(nls_amd.NlsError) as e:
+            s.step(1e-3)
+        assert e.value.code == -6 and "set_coefficients" in str(e.value)
+    with nls_amd.Solver(3, 8, 8, 8, 0.5, m=4) as s:
+        with pytest.raises(nls_amd.NlsError) as e:
+            s.set_coefficients(np.ones(512), np.ones(512))
+        assert e.value.code == -6
+
+
+@pytest.mark.parametrize("dim,n,nranks", [(3, 16, 2), (3, 13, 3), (2, 40, 4)])
+def test_g2_slabs_match_single_rank(dim, n, nranks):
+    """z-slab decomposition (local transport): c halo exchanged once, BC across
+    the boundary slabs, W_0 refresh + halo after the BC."""
+    m, dt, steps = 12, 1e-3, 6
+    dx = 8.0 / (n - 1)
+    u, mf, c = fields(dim, n, n, n, seed=6)
+    P = n * n if dim == 3 else n
+    ref = O.nlse_g2_steps(O.grid(dim, n, n, n, dx, dx), c, mf, u, dt, steps, m, bc=True)
+    grp = nls_amd.Group(nranks)
+    out = [None] * nranks
+    err = []
+
+    def work(r):
+        try:
+            s = solver(dim, n, n, n, dx, m, device=0, nranks=nranks, rank=r, group=grp)
+            sl = slice(s.z0 * P, (s.z0 + s.nzl) * P)
+            s.set_coefficients(mf[sl], c[sl])
+            s.set_field(u[sl])
+            for _ in range(steps):
+                s.step(dt, 1)
+                s.apply_bc()
+            out[r] = s.get_field()
+            s.close()
+        except Exception as e:  # noqa: BLE001
+            err.append((r, e))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    grp.close()
+    assert not err, err
+    assert rel_l2(np.concatenate(out), ref) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("dim", [3, 2])
+def test_g2_driver_matches_oracle(tmp_path, dim):
+    """nlse_3d_dev / nlse_2d_dev end to end: no normalisation, snapshot 0 = u0,
+    snapshots pre-BC every nt/ns steps, BC after each step, m = 25 / 20."""
+    n, L, T, nt, ns = (12, 4.0, 0.02, 10, 5) if dim == 3 else (24, 4.0, 0.02, 10, 5)
+    m = 25 if dim == 3 else 20
+    dx = 2 * L / (n - 1)
+    u, mf, c = fields(dim, n, n, n, seed=7, L=L)
+    shp = (n,) * dim
+    paths = {k: str(tmp_path / f"{k}.npy") for k in ("u0", "m", "c", "out")}
+    np.save(paths["u0"], u.reshape(shp))
+    np.save(paths["m"], mf.reshape(shp))
+    np.save(paths["c"], c.reshape(shp))
+    if dim == 3:
+        args = [os.path.join(BIN, "nlse_3d_dev"), str(n), str(n), str(n), str(L), str(L), str(L)]
+    else:
+        args = [os.path.join(BIN, "nlse_2d_dev"), str(n), str(n), str(L), str(L)]
+    args += [paths["u0"], paths["out"], str(T), str(nt), str(ns), paths["m"], paths["c"]]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    traj = np.load(paths["out"])
+    assert traj.shape == (ns,) + shp and traj.dtype == np.complex128
+    g = O.grid(dim, n, n, n, dx, dx)
+    dt, freq = T / nt, nt // ns
+    cur = u.copy()
+    expect = [u.copy()]
+    for i in range(1, nt):
+        cur = O.nlse_g2_steps(g, c, mf, cur, dt, 1, m, bc=False)
+        if i % freq == 0 and len(expect) < ns:
+            expect.append(cur.copy())
+        cur = O.neumann_bc(g, cur)
+    assert np.array_equal(traj[0].ravel(), u)
+    for k in range(1, ns):
+        assert rel_l2(traj[k].ravel(), expect[k]) <= TOL_TRAJ, k

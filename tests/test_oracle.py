@@ -169,3 +169,94 @@ def test_golden_krylov_functions():
     assert rel_l2(O.krylov_c(g, d["uc"], -1e-2j, m, 0), d["c_f0"]) < 1e-13
     assert rel_l2(O.krylov_c(g, d["uc"], 1e-2j, m, 1), d["c_f1"]) < 1e-13
     assert rel_l2(O.laplacian_c(g, d["uc"]), d["lap"]) < 1e-15
+
+
+# ---------------------------------------------------------------------------
+# G2 (nlsolvers/): anisotropic operator, exp(t*lambda) stepper, Neumann copy BC
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", [(2, 3, 3, 1), (2, 9, 7, 1), (3, 3, 3, 3), (3, 6, 5, 4)])
+def test_aniso_operator_equals_builder(dim, nx, ny, nz):
+    """Matrix-free G2 operator == the triplet builder
+    (nlsolvers/common/include/laplacians.hpp:54-103, 158-218), entry for entry."""
+    N = nx * ny * (nz if dim == 3 else 1)
+    rng = np.random.default_rng(N)
+    c = rng.uniform(0.2, 3.0, N)
+    A = np_ref.aniso_laplacian(dim, nx, ny, nz, 0.31, 0.29, c).toarray()
+    g = O.grid(dim, nx, ny, nz, 0.31, 0.29)
+    M = np.stack([O.laplacian_aniso_c(g, c, np.eye(N)[k]) for k in range(N)], axis=1)
+    assert np.allclose(M, A, rtol=1e-15, atol=1e-15)
+    assert np.array_equal(A, A.T)
+    # the diagonal is minus the row sum of the couplings: constants are in the kernel
+    assert np.allclose(A.sum(axis=1), 0.0, atol=1e-12)
+
+
+def test_aniso_quirks():
+    """c == 1 is NOT the isotropic operator (diagonal = -#couplings), and the 3D
+    builder keeps the flat-index y-wrap (i, ny-1, k) <-> (i, 0, k+1)."""
+    n = 5
+    Aa = np_ref.aniso_laplacian(3, n, n, n, 1.0, 1.0, np.ones(n ** 3)).toarray()
+    Ai = np_ref.laplacian_triplets(3, n, 1.0).toarray()
+    off = ~np.eye(n ** 3, dtype=bool)
+    assert np.array_equal(Aa[off], Ai[off])
+    assert not np.array_equal(np.diag(Aa), np.diag(Ai))
+    p = (0 * n + (n - 1)) * n + 2          # (i=2, j=n-1, k=0)
+    q = (1 * n + 0) * n + 2                # (i=2, j=0, k=1)
+    assert Aa[p, q] == 1.0
+
+
+def test_scipy_kat_stencil_operator():
+    """The published KAT again, now through the matrix-free G2 operator the
+    device kernels restate (c == 1, full 50^3 grid) -- same error levels."""
+    A, u0, t = _kat_setup()
+    n, L = 50, 2.0
+    g = O.grid(3, n, n, n, 2 * L / n, 2 * L / n)
+    ones = np.ones(n ** 3)
+    yc = spla.expm_multiply(1j * A.astype(np.complex128), u0.astype(np.complex128),
+                            start=0, stop=t, endpoint=True, num=2)[-1]
+    ec = {m: rel_l2(O.krylov_aniso_c(g, ones, u0, 1j * t, m, O_F_EXP), yc) for m in (10, 20)}
+    assert 7e-10 < ec[10] < 2e-9, ec
+    assert 5e-14 < ec[20] < 1e-12, ec
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", [(2, 3, 3, 1), (2, 8, 11, 1), (3, 3, 4, 5), (3, 7, 6, 5)])
+def test_neumann_bc(dim, nx, ny, nz):
+    """The reference's copy sequence (boundaries.cuh:10-81) == the clamp gather
+    the device kernel implements; interior untouched; idempotent."""
+    N = nx * ny * (nz if dim == 3 else 1)
+    rng = np.random.default_rng(N)
+    u = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    g = O.grid(dim, nx, ny, nz, 1.0, 1.0)
+    b = O.neumann_bc(g, u)
+    assert np.array_equal(b, np_ref.neumann_bc(dim, nx, ny, nz, u))
+    assert np.array_equal(O.neumann_bc(g, b), b)
+    shp = (ny, nx) if dim == 2 else (nz, ny, nx)
+    inner = tuple(slice(1, s - 1) for s in shp)
+    assert np.array_equal(b.reshape(shp)[inner], u.reshape(shp)[inner])
+
+
+@pytest.mark.parametrize("dim,n,m", [(2, 16, 20), (3, 8, 25)])
+def test_g2_oracle_matches_numpy_twin(dim, n, m):
+    rng = np.random.default_rng(dim)
+    N = n ** dim
+    dx = 0.5
+    c = rng.uniform(0.5, 2.0, N)
+    mf = rng.uniform(-1.0, 2.0, N)
+    u = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    g = O.grid(dim, n, n, n, dx, dx)
+    for bc in (False, True):
+        a = O.nlse_g2_steps(g, c, mf, u, 1e-3, 4, m, bc=bc)
+        b = np_ref.nlse_g2_steps(dim, n, n, n, dx, dx, c, mf, u, 1e-3, 4, m, bc=bc)
+        assert rel_l2(a, b) < 1e-12
+    # no BC, the G2 step is unitary too (Hermitian T, unit-modulus phase)
+    a = O.nlse_g2_steps(g, c, mf, u, 1e-3, 4, m, bc=False)
+    assert abs(np.linalg.norm(a) / np.linalg.norm(u) - 1) < 1e-12
+
+
+@pytest.mark.parametrize("name", ["g2_3d", "g2_2d"])
+def test_golden_g2(name):
+    d = np.load(os.path.join(GOLD, f"{name}.npz"))
+    n, dim = int(d["n"]), int(d["dim"])
+    g = O.grid(dim, n, n, n, float(d["dx"]), float(d["dx"]))
+    out = O.nlse_g2_steps(g, d["c"], d["mfield"], d["u0"], float(d["dt"]), int(d["steps"]), int(d["m"]))
+    assert rel_l2(out, d["u"]) < 1e-13
