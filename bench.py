@@ -41,7 +41,21 @@ WORKLOADS = {
                       desc="2D sine-Gordon 8192x8192, Gautschi, Krylov m=10, fp64"),
     "cq3d_1024": dict(dim=3, n=1024, L=10.0, m=16, eq=1, dt=1e-3,
                       desc="3D cubic-quintic NLSE 1024^3, Krylov m=16, fp64 complex"),
+    # G2 production driver (nlse_cubic_driver_3d.cpp: m=25, m(x), c(x), Neumann BC per step)
+    "g2_3d_256": dict(dim=3, n=256, L=10.0, m=25, eq=3, dt=1e-3,
+                      desc="G2 3D cubic NLSE 256^3 with m(x), div(c grad), Neumann BC, Krylov m=25, fp64 complex"),
 }
+
+
+def g2_coefficients(n, L, z0, nzl):
+    """Smooth synthetic focusing field m(x) in [0.5, 1.5] and anisotropy c(x) in [0.7, 1.3]."""
+    x = np.linspace(-L, L, n)
+    Z = x[z0:z0 + nzl][:, None, None]
+    Y = x[None, :, None]
+    X = x[None, None, :]
+    mf = 1.0 + 0.5 * np.cos(0.3 * X) * np.cos(0.2 * Y) * np.cos(0.25 * Z)
+    cf = 1.0 + 0.3 * np.sin(0.4 * X + 0.1 * Y) * np.cos(0.3 * Z)
+    return mf.ravel(), cf.ravel()
 
 
 def algorithmic_bytes_per_cell_step(m: int, eq: int) -> int:
@@ -103,7 +117,20 @@ def cpu_baseline(args):
     import oracle_py
 
     w = dict(WORKLOADS[args.workload])
-    if w["eq"] == 2:
+    if w["eq"] == 3:
+        ns, steps = 64, 3
+        w["n"] = ns
+        dx = 2 * w["L"] / (ns - 1)
+        u = synthetic_ic(w, 0, ns)
+        mf, cf = g2_coefficients(ns, w["L"], 0, ns)
+        g = oracle_py.grid(3, ns, ns, ns, dx, dx)
+        oracle_py.nlse_g2_steps(g, cf, mf, u, w["dt"], 1, w["m"])  # warm caches
+        t0 = time.perf_counter()
+        oracle_py.nlse_g2_steps(g, cf, mf, u, w["dt"], steps, w["m"])
+        el = time.perf_counter() - t0
+        cells = ns ** 3
+        sample = f"G2 3D NLSE {ns}^3 m={w['m']}, {steps} steps + BC (sub-grid of the workload, 1 thread)"
+    elif w["eq"] == 2:
         ns, steps = 256, 3
         w["n"] = ns
         dx = 2 * w["L"] / (ns - 1)
@@ -192,6 +219,9 @@ def main():
     u = synthetic_ic(w, s.z0, s.nzl)
     if w["eq"] == 2:
         s.set_sg_state(u, u.copy(), -np.ones(u.size))
+    elif w["eq"] == 3:  # G2 drivers do not normalise u0 (nlse_cubic_driver_3d.cpp:54-65)
+        s.set_field(u)
+        s.set_coefficients(*g2_coefficients(n, w["L"], s.z0, s.nzl))
     else:
         dv = dx ** dim
         mass = float(np.sum(np.abs(u) ** 2) * dv)
@@ -204,8 +234,17 @@ def main():
         s.set_field(u)
     del u
     dt = w["dt"]
+
+    def run(k):
+        if w["eq"] == 3:  # the G2 driver loop: step, then apply_bc (nlse_cubic_driver_3d.cpp:116-119)
+            for _ in range(k):
+                s.step(dt, 1)
+                s.apply_bc()
+        else:
+            s.step(dt, k)
+
     if args.warmup:
-        s.step(dt, args.warmup)
+        run(args.warmup)
     s.sync()
     s.reset_timing()
     s.set_timing(True)
@@ -213,7 +252,7 @@ def main():
         dist.barrier()
     s.sync()
     t0 = time.perf_counter()
-    s.step(dt, args.steps)
+    run(args.steps)
     s.sync()
     if dist is not None:
         dist.barrier()
@@ -254,7 +293,7 @@ def main():
         "dtype": "f64" if w["eq"] == 2 else "c128 (fp64 complex)",
         "data": "synthetic (8 random Gaussian solitons + 1e-3 complex white noise, seeded)",
         "config": {"workload": w["desc"], "grid": [n] * dim, "krylov_m": m, "dt": dt,
-                   "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi"][w["eq"]],
+                   "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi", "nlse_g2"][w["eq"]],
                    "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
         "roofline": {
             "bound": "hbm",

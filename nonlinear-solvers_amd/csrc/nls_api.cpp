@@ -45,6 +45,17 @@ struct Fail {
   int code;
 };
 
+// Launches of one update pass: a single full-slab launch, or (collective
+// handles) the two boundary planes first and the interior after, so the halo
+// exchange of the new vector overlaps the interior launch.  All launches write
+// one column-major partial array (stride = total blocks).
+struct UpdPlan {
+  int n = 0;
+  int qa[3] = {}, qb[3] = {}, grid[3] = {}, off[3] = {};
+  int total = 0;
+  int nbnd = 0;  // the first nbnd launches cover the boundary planes
+};
+
 constexpr int NSUM = 2 * MMAX + 8;  // cplx words of KState::sums
 constexpr int EVRING = 8;            // events per handle for the local transport
 
@@ -84,7 +95,7 @@ struct nls_handle {
   void *scratch = nullptr;  // nloc elements
   cplx *partA = nullptr, *partU = nullptr;
   int grid_alpha = 1, grid_lap = 1, grid_pw = 1;
-  int grid_update[MMAX] = {};
+  UpdPlan plan[MMAX];
   bool field_set = false, w0_ready = false;
   double w0_dt = 0.0;  // dt the live start vector W_0 = N(u) was built with
   int nonlin = 0;
@@ -102,6 +113,10 @@ struct nls_handle {
   bool collective = false;     // split reductions + exchanges (nranks > 1, or NLS_FORCE_RCCL=1)
   hipEvent_t evring[EVRING] = {};
   uint64_t evnext = 0, ar_count = 0;
+  // halo/compute overlap (collective handles): exchange on cstream
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_bnd = nullptr, ev_halo = nullptr;
+  bool halo_pending = false;
 };
 
 namespace {
@@ -219,30 +234,32 @@ std::vector<std::vector<uint64_t>> rendezvous(nls_handle *h, std::vector<uint64_
 
 hipEvent_t next_event(nls_handle *h) { return h->evring[h->evnext++ % EVRING]; }
 
-void halo_local(nls_handle *h, char *first, char *last, char *gbelow, char *gabove, size_t bytes) {
+void halo_local(nls_handle *h, hipStream_t st, char *first, char *last, char *gbelow, char *gabove,
+                size_t bytes) {
   hipEvent_t ev = next_event(h);
-  hip_check(h, hipEventRecord(ev, h->stream), "hipEventRecord");
+  hip_check(h, hipEventRecord(ev, st), "hipEventRecord");
   auto all = rendezvous(h, {(uint64_t)(uintptr_t)first, (uint64_t)(uintptr_t)last,
                             (uint64_t)(uintptr_t)ev});
   if (h->rank > 0) {
     const auto &nb = all[h->rank - 1];
-    hip_check(h, hipStreamWaitEvent(h->stream, (hipEvent_t)(uintptr_t)nb[2], 0), "hipStreamWaitEvent");
+    hip_check(h, hipStreamWaitEvent(st, (hipEvent_t)(uintptr_t)nb[2], 0), "hipStreamWaitEvent");
     hip_check(h, hipMemcpyAsync(gbelow, (const void *)(uintptr_t)nb[1], bytes, hipMemcpyDeviceToDevice,
-                                h->stream), "hipMemcpyAsync(halo)");
+                                st), "hipMemcpyAsync(halo)");
   }
   if (h->rank < h->nranks - 1) {
     const auto &nb = all[h->rank + 1];
-    hip_check(h, hipStreamWaitEvent(h->stream, (hipEvent_t)(uintptr_t)nb[2], 0), "hipStreamWaitEvent");
+    hip_check(h, hipStreamWaitEvent(st, (hipEvent_t)(uintptr_t)nb[2], 0), "hipStreamWaitEvent");
     hip_check(h, hipMemcpyAsync(gabove, (const void *)(uintptr_t)nb[0], bytes, hipMemcpyDeviceToDevice,
-                                h->stream), "hipMemcpyAsync(halo)");
+                                st), "hipMemcpyAsync(halo)");
   }
 }
 
 // Exchange the boundary planes of a slab-stored array (local plane 0 at v,
 // ghost planes at -P and nzl*P) into the neighbours' ghost planes (z-slab
 // decomposition; one plane covers the 3D y-wrap too).
-void halo_planes(nls_handle *h, char *v, int64_t es) {
+void halo_planes(nls_handle *h, char *v, int64_t es, hipStream_t st = nullptr) {
   if (!h->collective) return;
+  if (!st) st = h->stream;
   const int64_t P = h->geo.P;
   const size_t cnt = (size_t)P * (size_t)(es / 8);
   char *first = v, *last = v + (h->geo.nzl - 1) * P * es;
@@ -251,34 +268,50 @@ void halo_planes(nls_handle *h, char *v, int64_t es) {
   if (h->timing) {
     rec.a = get_event(h);
     rec.b = get_event(h);
-    hip_check(h, hipEventRecord(rec.a, h->stream), "hipEventRecord");
+    hip_check(h, hipEventRecord(rec.a, st), "hipEventRecord");
   }
   if (h->group) {
-    halo_local(h, first, last, gbelow, gabove, (size_t)P * es);
+    halo_local(h, st, first, last, gbelow, gabove, (size_t)P * es);
     if (h->timing) {
-      hip_check(h, hipEventRecord(rec.b, h->stream), "hipEventRecord");
+      hip_check(h, hipEventRecord(rec.b, st), "hipEventRecord");
       h->recs.push_back(rec);
     }
     return;
   }
   rccl_check(h, ncclGroupStart(), "ncclGroupStart");
   if (h->rank > 0) {
-    rccl_check(h, ncclSend(first, cnt, ncclDouble, h->rank - 1, h->comm, h->stream), "ncclSend");
-    rccl_check(h, ncclRecv(gbelow, cnt, ncclDouble, h->rank - 1, h->comm, h->stream), "ncclRecv");
+    rccl_check(h, ncclSend(first, cnt, ncclDouble, h->rank - 1, h->comm, st), "ncclSend");
+    rccl_check(h, ncclRecv(gbelow, cnt, ncclDouble, h->rank - 1, h->comm, st), "ncclRecv");
   }
   if (h->rank < h->nranks - 1) {
-    rccl_check(h, ncclSend(last, cnt, ncclDouble, h->rank + 1, h->comm, h->stream), "ncclSend");
-    rccl_check(h, ncclRecv(gabove, cnt, ncclDouble, h->rank + 1, h->comm, h->stream), "ncclRecv");
+    rccl_check(h, ncclSend(last, cnt, ncclDouble, h->rank + 1, h->comm, st), "ncclSend");
+    rccl_check(h, ncclRecv(gabove, cnt, ncclDouble, h->rank + 1, h->comm, st), "ncclRecv");
   }
   rccl_check(h, ncclGroupEnd(), "ncclGroupEnd");
   if (h->timing) {
-    hip_check(h, hipEventRecord(rec.b, h->stream), "hipEventRecord");
+    hip_check(h, hipEventRecord(rec.b, st), "hipEventRecord");
     h->recs.push_back(rec);
   }
 }
 
 // vector k of basis b
 void halo(nls_handle *h, int b, int k) { halo_planes(h, vec_ptr(h, b, k), (int64_t)h->esize); }
+
+// Overlapped form: called once the boundary planes of vector k are enqueued on
+// the compute stream; the exchange runs on cstream while the interior planes
+// are computed.  halo_wait() orders the compute stream after it.
+void halo_begin(nls_handle *h, int b, int k) {
+  hip_check(h, hipEventRecord(h->ev_bnd, h->stream), "hipEventRecord");
+  hip_check(h, hipStreamWaitEvent(h->cstream, h->ev_bnd, 0), "hipStreamWaitEvent");
+  halo_planes(h, vec_ptr(h, b, k), (int64_t)h->esize, h->cstream);
+  hip_check(h, hipEventRecord(h->ev_halo, h->cstream), "hipEventRecord");
+  h->halo_pending = true;
+}
+void halo_wait(nls_handle *h) {
+  if (!h->halo_pending) return;
+  hip_check(h, hipStreamWaitEvent(h->stream, h->ev_halo, 0), "hipStreamWaitEvent");
+  h->halo_pending = false;
+}
 
 void allreduce_sums(nls_handle *h, int b, int ncplx) {
   void *p = &h->B[b].st->sums[0];
@@ -320,7 +353,7 @@ void allreduce_sums(nls_handle *h, int b, int ncplx) {
 
 void reduce_iter(nls_handle *h, int b, int j) {
   KState *st = h->B[b].st;
-  int nbA = h->grid_alpha, nbU = j >= 1 ? h->grid_update[j - 1] : 0;
+  int nbA = h->grid_alpha, nbU = j >= 1 ? h->plan[j - 1].total : 0;
   const void *fn = kernel_reduce_iter();
   if (!h->collective) {
     int ds = 1, dc = 1;
@@ -340,7 +373,7 @@ void reduce_iter(nls_handle *h, int b, int j) {
 
 void reduce_final(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
   KState *st = h->B[b].st;
-  int m = h->m, nbU = m >= 2 ? h->grid_update[m - 2] : 0;
+  int m = h->m, nbU = m >= 2 ? h->plan[m - 2].total : 0;
   const void *fn = kernel_reduce_final();
   if (!h->collective) {
     int ds = 1, dc = 1;
@@ -375,15 +408,27 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   for (int j = 0; j + 1 < m; ++j) {
     void *out = vec_ptr(h, b, j + 1);
     if (j >= 1) {
+      halo_wait(h);
       void *vj = vec_ptr(h, b, j);
       void *args[] = {&vj, &g, &h->partA};
       launch(h, 0, j, fa, h->grid_alpha, args);
       reduce_iter(h, b, j);
     }
-    void *args[] = {&W, &out, &vs, &g, &st, &h->partU};
-    launch(h, 1, j, kernel_update(h->cplx_, (int)h->cfg.dim, j, h->ani), h->grid_update[j], args);
-    if (j + 1 <= m - 2) halo(h, b, j + 1);
+    const void *fu = kernel_update(h->cplx_, (int)h->cfg.dim, j, h->ani);
+    const UpdPlan &pl = h->plan[j];
+    const bool need_halo = j + 1 <= m - 2 && h->collective;
+    for (int i = 0; i < pl.n; ++i) {
+      Geo gi = g;
+      gi.qa = pl.qa[i];
+      gi.qb = pl.qb[i];
+      int ps = pl.total, po = pl.off[i];
+      void *args[] = {&W, &out, &vs, &gi, &st, &h->partU, &ps, &po};
+      launch(h, 1, j, fu, pl.grid[i], args);
+      if (need_halo && i + 1 == pl.nbnd) halo_begin(h, b, j + 1);
+    }
+    if (need_halo && pl.nbnd == 0) halo(h, b, j + 1);
   }
+  halo_wait(h);
   reduce_final(h, b, nf, f0, f1, tr, ti);
 }
 
@@ -417,6 +462,8 @@ void setup_geometry(nls_handle *h) {
   g.Ng = g.P * g.npl;
   const int64_t base = g.npl / h->nranks, rem = g.npl % h->nranks;
   g.nzl = base + (h->rank < rem ? 1 : 0);
+  g.qa = 0;
+  g.qb = (int32_t)g.nzl;
   g.z0 = (int64_t)h->rank * base + std::min<int64_t>(h->rank, rem);
   g.nloc = g.nzl * g.P;
   // laplacians.hpp:49 (2D 1/(dx*dy)) and :102 (3D 1/(dx*dx)); values -4/-3, -6/-5 times scale
@@ -468,9 +515,30 @@ void alloc_all(nls_handle *h) {
   h->grid_lap = occupancy_grid(h, kernel_lap(c, dim, ani), ta);
   int64_t cap = 2 * (int64_t)h->grid_alpha;
   for (int j = 0; j + 1 < h->m; ++j) {
-    h->grid_update[j] = occupancy_grid(h, kernel_update(c, dim, j, ani),
-                                       stencil_tiles(g, dim, update_rows_per_thread(j)));
-    cap = std::max<int64_t>(cap, (int64_t)h->grid_update[j] * (j + 2));
+    const void *fu = kernel_update(c, dim, j, ani);
+    UpdPlan &pl = h->plan[j];
+    pl = UpdPlan{};
+    auto add = [&](int qa, int qb, bool bnd) {
+      Geo gi = g;
+      gi.qa = qa;
+      gi.qb = qb;
+      const int i = pl.n++;
+      pl.qa[i] = qa;
+      pl.qb[i] = qb;
+      pl.grid[i] = occupancy_grid(h, fu, stencil_tiles(gi, dim, update_rows_per_thread(j)));
+      pl.off[i] = pl.total;
+      pl.total += pl.grid[i];
+      if (bnd) pl.nbnd = pl.n;
+    };
+    const int nzl = (int)g.nzl;
+    if (h->collective && nzl >= 3) {
+      add(0, 1, true);
+      add(nzl - 1, nzl, true);
+      add(1, nzl - 1, false);
+    } else {
+      add(0, nzl, false);
+    }
+    cap = std::max<int64_t>(cap, (int64_t)pl.total * (j + 2));
   }
   hip_check(h, hipMalloc(&h->partA, 2 * (size_t)h->grid_alpha * sizeof(cplx)), "hipMalloc(partA)");
   hip_check(h, hipMalloc(&h->partU, (size_t)cap * sizeof(cplx)), "hipMalloc(partU)");
@@ -584,7 +652,6 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   int rc = guarded(h, [&] {
     hip_check(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
     setup_geometry(h);
-    alloc_all(h);
     if (h->nranks > 1 && c.local_group) {
       h->group = static_cast<nls_group *>(c.local_group);
       for (auto &e : h->evring)
@@ -608,12 +675,23 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
       rccl_check(h, ncclCommInitRank(&h->comm, 1, id, 0), "ncclCommInitRank");
     }
     h->collective = h->nranks > 1 || h->comm != nullptr;
+    if (h->collective) {
+      hip_check(h, hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking), "hipStreamCreate");
+      hip_check(h, hipEventCreateWithFlags(&h->ev_bnd, hipEventDisableTiming), "hipEventCreate");
+      hip_check(h, hipEventCreateWithFlags(&h->ev_halo, hipEventDisableTiming), "hipEventCreate");
+    }
+    alloc_all(h);  // the update launch plan depends on h->collective
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
   });
   if (rc != NLS_OK) {
     g_create_error = h->err;
     free_all(h);
     if (h->comm) ncclCommDestroy(h->comm);
+    for (hipEvent_t e : {h->ev_bnd, h->ev_halo})
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : h->evring)
+      if (e) (void)hipEventDestroy(e);
+    if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return rc;
@@ -626,6 +704,10 @@ int nls_destroy(nls_handle *h) {
   if (!h) return NLS_ERR_ARG;
   (void)hipSetDevice(h->dev);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->cstream) (void)hipStreamSynchronize(h->cstream);
+  for (hipEvent_t e : {h->ev_bnd, h->ev_halo})
+    if (e) (void)hipEventDestroy(e);
+  if (h->cstream) (void)hipStreamDestroy(h->cstream);
   for (auto &r : h->recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);

@@ -58,6 +58,7 @@ struct Geo {
   double sd_bd;   // boundary diagonal  -3*s / -5*s
   int32_t kz;     // planes (3D) / rows per wave (2D) per tile of the stencil kernels
   int32_t remap;  // 1: XCD-banded tile order (speed only)
+  int32_t qa, qb; // local planes [qa, qb) covered by a stencil launch (default 0, nzl)
   const double *cf;  // G2 anisotropic operator: c field at local plane 0 (ghost planes at
                      // -P and nzl*P, like a basis vector); unused by the isotropic operator
 };

@@ -6,7 +6,8 @@
 namespace nls {
 
 // stencil kernels (tiled march), argument lists:
-//   update : (const S* W, S* out, int64_t vs, Geo g, const KState* st, cplx* part)
+//   update : (const S* W, S* out, int64_t vs, Geo g, const KState* st, cplx* part,
+//             int part_stride, int part_off)   -- partials at part[k*stride + off + block]
 //   alpha  : (const S* V, Geo g, cplx* part)
 //   lap    : (const S* V, Geo g, S* out)
 // ani = true: the G2 anisotropic operator (complex only; Geo::cf = c field)

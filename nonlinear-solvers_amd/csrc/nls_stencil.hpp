@@ -30,10 +30,11 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// partials are stored column-major: out[k * gridDim.x + blockIdx.x], so the
+// partials are stored column-major: out[k * stride + off + blockIdx.x] (stride =
+// gridDim.x, off = 0 unless several launches share one partial array), so the
 // single-workgroup reduction reads each column with coalesced 1 KiB wave loads.
 template <int NA>
-__device__ __forceinline__ void block_store(cplx (&v)[NA], cplx *__restrict__ out) {
+__device__ __forceinline__ void block_store(cplx (&v)[NA], cplx *__restrict__ out, int stride, int off) {
   __shared__ cplx red[NTHREADS / 64][NA];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -50,7 +51,7 @@ __device__ __forceinline__ void block_store(cplx (&v)[NA], cplx *__restrict__ ou
     cplx s = red[0][k];
 #pragma unroll
     for (int q = 1; q < NTHREADS / 64; ++q) s += red[q][k];
-    out[(int64_t)k * gridDim.x + blockIdx.x] = s;
+    out[(int64_t)k * stride + off + blockIdx.x] = s;
   }
 }
 
@@ -96,14 +97,15 @@ __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 
 
 template <int DIM, int RB> __host__ __device__ inline void tile_counts(const Geo &g, int64_t &ntx,
                                                                         int64_t &nty, int64_t &ntz) {
+  const int64_t nq = g.qb - g.qa;  // local planes [qa, qb) covered by this launch
   if (DIM == 3) {
     ntx = cdiv(g.nx, 64);
     nty = cdiv(g.nyp, 4 * RB);
-    ntz = cdiv(g.nzl, g.kz);
+    ntz = cdiv(nq, g.kz);
   } else {
     ntx = cdiv(g.nx, 64 * RB);
     nty = 1;
-    ntz = cdiv(g.nzl, 4 * (int64_t)g.kz);
+    ntz = cdiv(nq, 4 * (int64_t)g.kz);
   }
 }
 
@@ -131,7 +133,7 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
   const int ntx = (int)ntx64, nty = (int)nty64;
   const int tiles = (int)(ntx64 * nty64 * ntz64);
   const int T8 = tiles / 8;
-  const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, nzl = (int)g.nzl, kz = g.kz;
+  const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, qa = g.qa, qb = g.qb, kz = g.kz;
   const int z0 = (int)g.z0, npl = (int)g.npl;
   for (int t0 = blockIdx.x; t0 < tiles; t0 += gridDim.x) {
     // optional XCD-banded order (workgroups b, b+8 share an XCD): speed only
@@ -145,8 +147,8 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
       const bool xin = x < nx;
       const int yb = jt * (4 * RB) + w * RB;
       if (yb >= nyp) continue;  // wave-uniform
-      const int q0 = kt * kz;
-      const int q1 = q0 + kz < nzl ? q0 + kz : nzl;
+      const int q0 = qa + kt * kz;
+      const int q1 = q0 + kz < qb ? q0 + kz : qb;
       bool rv[RB];
       int off[RB];
       S prev[RB], cur[RB];
@@ -243,9 +245,9 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
         }
       }
     } else {
-      const int q0 = (kt * 4 + w) * kz;
-      if (q0 >= nzl) continue;  // wave-uniform
-      const int q1 = q0 + kz < nzl ? q0 + kz : nzl;
+      const int q0 = qa + (kt * 4 + w) * kz;
+      if (q0 >= qb) continue;  // wave-uniform
+      const int q1 = q0 + kz < qb ? q0 + kz : qb;
       int xr[RB];
       S prev[RB], cur[RB];
       double cprv[RB], ccur[RB];
@@ -376,7 +378,7 @@ __device__ __forceinline__ void alpha_tiles(const S *__restrict__ V, const Geo &
     if constexpr (DIM == 3) {
       yb = jt * (4 * RB) + (int64_t)w * RB;
       if (yb >= g.nyp) continue;
-      q0 = kt * g.kz;
+      q0 = g.qa + kt * g.kz;
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         rv[r] = yb + r < g.nyp;
@@ -384,8 +386,8 @@ __device__ __forceinline__ void alpha_tiles(const S *__restrict__ V, const Geo &
         xin[r] = it * 64 + lane < nx;
       }
     } else {
-      q0 = (kt * 4 + w) * (int64_t)g.kz;
-      if (q0 >= g.nzl) continue;
+      q0 = g.qa + (kt * 4 + w) * (int64_t)g.kz;
+      if (q0 >= g.qb) continue;
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         rv[r] = true;
@@ -393,7 +395,7 @@ __device__ __forceinline__ void alpha_tiles(const S *__restrict__ V, const Geo &
         xin[r] = off[r] < nx;
       }
     }
-    q1 = q0 + g.kz < g.nzl ? q0 + g.kz : g.nzl;
+    q1 = q0 + g.kz < g.qb ? q0 + g.kz : g.qb;
     S cur[RB], nxt[RB];
     double ccu[RB], cnx[RB];
 #pragma unroll
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(NTHREADS) void k_alpha(const S *__restrict__ V, Geo
   double a = 0.0, n2 = 0.0;
   alpha_tiles<S, DIM, RB_ALPHA, ANI>(V, g, a, n2);
   cplx v[2] = {{a, 0.0}, {n2, 0.0}};
-  block_store<2>(v, part);
+  block_store<2>(v, part, gridDim.x, 0);
 }
 
 // W_{J+1} = a * L W_J - sum_{k<=J} b_k W_k ;  partials g_k = W_k^H W_{J+1}, ||W_{J+1}||^2
@@ -522,7 +524,7 @@ template <class S, int DIM, int J, bool ANI>
 __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S *__restrict__ out,
                                                      int64_t vs, Geo g,
                                                      const KState *__restrict__ st,
-                                                     cplx *__restrict__ part) {
+                                                     cplx *__restrict__ part, int pstride, int poff) {
   constexpr int NA = J + 2;
   S acc[NA];
 #pragma unroll
@@ -578,7 +580,7 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
   cplx v[NA];
 #pragma unroll
   for (int k = 0; k < NA; ++k) v[k] = to_c(acc[k]);
-  block_store<NA>(v, part);
+  block_store<NA>(v, part, pstride, poff);
 #undef NLS_B
 #undef NLS_RELOAD
 }
