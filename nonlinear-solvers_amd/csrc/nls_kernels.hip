@@ -70,6 +70,36 @@ __device__ void sum_partials(const cplx *__restrict__ part, int nb, int nc, cplx
   }
 }
 
+// The same column sums for large partial arrays (one tile per workgroup
+// grids): one workgroup per column, fixed order -> st->sums layout
+// [partA columns 0..ncA) then [partU columns 0..ncU).
+__global__ __launch_bounds__(NTHREADS) void k_colsum(const cplx *__restrict__ partA, int nbA, int ncA,
+                                                     const cplx *__restrict__ partU, int nbU,
+                                                     cplx *__restrict__ dst) {
+  const int v = blockIdx.x;
+  const cplx *__restrict__ col = v < ncA ? partA + (int64_t)v * nbA : partU + (int64_t)(v - ncA) * nbU;
+  const int nb = v < ncA ? nbA : nbU;
+  double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
+  int q = threadIdx.x;
+  for (; q + NTHREADS < nb; q += 2 * NTHREADS) {
+    const cplx x0 = col[q], x1 = col[q + NTHREADS];
+    a0 += x0.re; b0 += x0.im;
+    a1 += x1.re; b1 += x1.im;
+  }
+  if (q < nb) { const cplx x0 = col[q]; a0 += x0.re; b0 += x0.im; }
+  const double a = wave_sum(a0 + a1), b = wave_sum(b0 + b1);
+  __shared__ double ra[NTHREADS / 64], rb[NTHREADS / 64];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { ra[w] = a; rb[w] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sa = ra[0], sb = rb[0];
+    for (int i = 1; i < NTHREADS / 64; ++i) { sa += ra[i]; sb += rb[i]; }
+    dst[v] = {sa, sb};
+  }
+}
+const void *kernel_colsum() { return reinterpret_cast<const void *>(&k_colsum); }
+
 __device__ __forceinline__ double inv_or_zero(double s) { return s > 0.0 ? 1.0 / s : 0.0; }
 
 // After k_alpha<j> (and k_update<j-1>): sums layout

@@ -34,6 +34,9 @@ const void *kernel_reduce_iter();
 //   sum_ranks    : (cplx* dst, const cplx* pub, int nranks, int parity, int n, int stride)
 const void *kernel_sum_ranks();
 const void *kernel_reduce_final();
+//   colsum       : (const cplx* partA, int nbA, int ncA, const cplx* partU, int nbU, cplx* dst)
+//                  grid = ncA + ncU columns; dst = KState::sums (the do_sum phase, parallel)
+const void *kernel_colsum();
 
 // pointwise (grid-stride):
 //   nl_init   : (const cplx* u, cplx* w0, const double* mf, int64_t n, double dt, int nonlin,
