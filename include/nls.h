@@ -24,6 +24,8 @@
  *                       SGESolverDevice::step(tau=dt, i)                   device/sg_solver_dev.hpp:168-193
  *                       G2 NLSESolverDevice::step(tau=1j*dt, i)            nlsolvers/device/include/nlse_dev.hpp:187-203
  *   nls_get_field    <- transfer_snapshots(dst) / store_snapshot D2D+D2H   device/nlse_solver_dev.hpp:113-124
+ *   nls_get_field_async / nls_wait_field
+ *                    <- store_snapshot_online(host_dst) (G2)               nlsolvers/device/include/nlse_dev.hpp:323-334
  *   nls_get_sg_velocity <- transfer_snapshots(dst, 'v')                    device/sg_solver_dev.hpp:195-222
  *   nls_krylov_apply <- MatrixFunctionApplicator{Complex,Real}::apply(out, in, t[, type])
  *                                                                          device/matfunc_complex.hpp:155-177
@@ -142,6 +144,22 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps);
 int nls_sync(nls_handle *h);
 
 int nls_get_field(nls_handle *h, double *u, uint64_t n_local);
+
+/* Asynchronous snapshot (the online snapshot of
+ * nlsolvers/device/include/nlse_dev.hpp:323-334 without stalling the time
+ * loop): enqueue, after all work enqueued so far, a device-side copy of the
+ * field into a staging buffer and its D2H transfer into dst on a copy stream,
+ * then return.  dst must stay valid and must not be read until
+ * nls_wait_field(h) returns; pinned memory from nls_host_alloc makes the
+ * transfer fully asynchronous.  At most one snapshot is in flight per handle
+ * (a new call orders its staging copy after the previous transfer on the
+ * device, without blocking the host).  nls_wait_field may be called from
+ * another host thread than the one driving the handle. */
+int nls_get_field_async(nls_handle *h, double *dst, uint64_t n_local);
+int nls_wait_field(nls_handle *h);
+/* Page-locked host memory for nls_get_field_async (hipHostMalloc). */
+int nls_host_alloc(uint64_t bytes, void **out);
+int nls_host_free(void *p);
 int nls_get_sg_velocity(nls_handle *h, double dt, double *v, uint64_t n_local);
 
 /* One Krylov matrix-function action out = f(L) in (no time stepping), t complex

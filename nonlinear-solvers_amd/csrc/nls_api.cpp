@@ -119,6 +119,16 @@ struct nls_handle {
   hipStream_t cstream = nullptr;
   hipEvent_t ev_bnd = nullptr, ev_halo = nullptr;
   bool halo_pending = false;
+  // asynchronous snapshots: staging copy on the compute stream, D2H on xstream
+  hipStream_t xstream = nullptr;
+  hipEvent_t ev_snap = nullptr, ev_snap_done = nullptr;
+  void *snap = nullptr;
+  bool snap_issued = false;
+  // bounded host run-ahead: at most `runahead` steps enqueued beyond the GPU
+  static constexpr int RA_MAX = 16;
+  hipEvent_t stepev[RA_MAX] = {};
+  int runahead = 0;  // NLS_RUNAHEAD=k: off by default (no measured effect, tools/exp_runahead.sh)
+  uint64_t steps_issued = 0;
 };
 
 namespace {
@@ -594,10 +604,10 @@ void free_all(nls_handle *h) {
     h->B[b] = Basis{};
   }
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
-  for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch,
+  for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap,
                   (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
-  h->u = h->scratch = nullptr;
+  h->u = h->scratch = h->snap = nullptr;
   h->up = h->mf = h->cfb = nullptr;
   h->partA = h->partU = nullptr;
 }
@@ -685,6 +695,8 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   h->s2 = {c.sigma2[0], c.sigma2[1]};
   h->rank = c.rank;
   h->nranks = c.nranks;
+  if (const char *e = std::getenv("NLS_RUNAHEAD"))
+    h->runahead = std::min(nls_handle::RA_MAX, std::max(0, std::atoi(e)));
   if (c.device >= 0) {
     h->dev = c.device;
   } else if (hipGetDevice(&h->dev) != hipSuccess) {
@@ -748,9 +760,13 @@ int nls_destroy(nls_handle *h) {
   (void)hipSetDevice(h->dev);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->cstream) (void)hipStreamSynchronize(h->cstream);
-  for (hipEvent_t e : {h->ev_bnd, h->ev_halo})
+  if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+  for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_snap, h->ev_snap_done})
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->stepev)
     if (e) (void)hipEventDestroy(e);
   if (h->cstream) (void)hipStreamDestroy(h->cstream);
+  if (h->xstream) (void)hipStreamDestroy(h->xstream);
   for (auto &r : h->recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -860,6 +876,11 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
     const int64_t n = h->geo.nloc;
     int64_t vs = h->vs;
     for (uint32_t s = 0; s < nsteps; ++s) {
+      // Optionally keep the host at most `runahead` steps ahead of the device
+      // (bounded queue depth for callers that enqueue thousands of steps).
+      const int ra = h->runahead;
+      if (ra > 0 && h->steps_issued >= (uint64_t)ra)
+        hip_check(h, hipEventSynchronize(h->stepev[h->steps_issued % ra]), "hipEventSynchronize");
       if (h->cplx_) {
         // NLSESolverDevice::step (device/nlse_solver_dev.hpp:94-111), tau = 1j*dt:
         //   N(1/2) -> exp(L*dt) via exp(t|lambda|), t = -tau -> N(1/2)
@@ -905,6 +926,12 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
         }
       }
       h->tacc.steps += 1;
+      if (ra > 0) {
+        hipEvent_t &e = h->stepev[h->steps_issued % ra];
+        if (!e) hip_check(h, hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        hip_check(h, hipEventRecord(e, h->stream), "hipEventRecord");
+      }
+      ++h->steps_issued;
     }
     hip_check(h, hipGetLastError(), "kernel launch");
   });
@@ -923,6 +950,57 @@ int nls_get_field(nls_handle *h, double *u, uint64_t n) {
               "hipMemcpy D2H");
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
   });
+}
+
+int nls_get_field_async(nls_handle *h, double *dst, uint64_t n) {
+  return guarded(h, [&] {
+    if (!dst) fail(h, NLS_ERR_ARG, "dst is NULL");
+    check_len(h, n);
+    const size_t bytes = (size_t)n * h->esize;
+    if (!h->xstream) {
+      hip_check(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking), "hipStreamCreate");
+      hip_check(h, hipEventCreateWithFlags(&h->ev_snap, hipEventDisableTiming), "hipEventCreate");
+      hip_check(h, hipEventCreateWithFlags(&h->ev_snap_done, hipEventDisableTiming), "hipEventCreate");
+      hip_check(h, hipMalloc(&h->snap, bytes), "hipMalloc(snapshot staging)");
+    }
+    // the staging buffer is free once the previous transfer has finished
+    if (h->snap_issued)
+      hip_check(h, hipStreamWaitEvent(h->stream, h->ev_snap_done, 0), "hipStreamWaitEvent");
+    const void *src = h->cplx_ ? h->u : (const void *)vec_ptr(h, 0, 0);
+    hip_check(h, hipMemcpyAsync(h->snap, src, bytes, hipMemcpyDeviceToDevice, h->stream),
+              "hipMemcpyAsync(snapshot D2D)");
+    hip_check(h, hipEventRecord(h->ev_snap, h->stream), "hipEventRecord");
+    hip_check(h, hipStreamWaitEvent(h->xstream, h->ev_snap, 0), "hipStreamWaitEvent");
+    hip_check(h, hipMemcpyAsync(dst, h->snap, bytes, hipMemcpyDeviceToHost, h->xstream),
+              "hipMemcpyAsync(snapshot D2H)");
+    hip_check(h, hipEventRecord(h->ev_snap_done, h->xstream), "hipEventRecord");
+    h->snap_issued = true;
+  });
+}
+
+int nls_wait_field(nls_handle *h) {
+  if (!h) return NLS_ERR_ARG;
+  if (!h->snap_issued) return NLS_OK;
+  // no handle state is touched: safe from a second host thread
+  (void)hipSetDevice(h->dev);
+  const hipError_t e = hipEventSynchronize(h->ev_snap_done);
+  if (e != hipSuccess) return e == hipErrorOutOfMemory ? NLS_ERR_OOM : NLS_ERR_HIP;
+  return NLS_OK;
+}
+
+int nls_host_alloc(uint64_t bytes, void **out) {
+  if (!out) return NLS_ERR_ARG;
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes == 0 ? 1 : (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
+    g_create_error = "hipHostMalloc failed";
+    return NLS_ERR_OOM;
+  }
+  return NLS_OK;
+}
+
+int nls_host_free(void *p) {
+  if (p && hipHostFree(p) != hipSuccess) return NLS_ERR_HIP;
+  return NLS_OK;
 }
 
 int nls_get_sg_velocity(nls_handle *h, double dt, double *v, uint64_t n) {

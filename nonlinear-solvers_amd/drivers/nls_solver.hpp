@@ -15,11 +15,17 @@
 // would need 215 GB at 512^3); errors are reported as
 // std::runtime_error carrying nls_last_error().
 #pragma once
+#include <chrono>
 #include <complex>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
+#include <exception>
 #include <functional>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nls.h"
@@ -35,6 +41,128 @@ struct Grid {
   uint32_t nx = 0, ny = 0, nz = 1;
   double dx = 1.0, dy = 1.0;
   uint64_t cells() const { return (uint64_t)nx * ny * (dim == 3 ? nz : 1); }
+};
+
+// Double-buffered snapshot pipeline: snapshot k is copied on the device and
+// transferred into pinned buffer k % 2 (nls_get_field_async) while the time
+// loop continues; a writer thread hands completed buffers to the callback in
+// order.  The host blocks only when the writer still holds the buffer it
+// needs (blocked_seconds() reports that time).
+template <class T> class SnapshotPipe {
+ public:
+  using Fn = std::function<void(uint32_t index, const T *u, uint64_t n)>;
+  SnapshotPipe(nls_handle *h, uint64_t n, Fn cb) : h_(h), n_(n), cb_(std::move(cb)) {
+    for (auto &b : buf_) {
+      void *p = nullptr;
+      check(nls_host_alloc(n * sizeof(T), &p), nullptr);
+      b = static_cast<T *>(p);
+    }
+    writer_ = std::thread([this] { run(); });
+  }
+  ~SnapshotPipe() {
+    try {
+      finish();
+    } catch (...) {
+    }
+    for (auto b : buf_) nls_host_free(b);
+  }
+  SnapshotPipe(const SnapshotPipe &) = delete;
+  SnapshotPipe &operator=(const SnapshotPipe &) = delete;
+
+  // enqueue snapshot `index` of the field as of all work enqueued so far
+  void push(uint32_t index) {
+    rethrow();
+    const int b = next_;
+    next_ ^= 1;
+    {  // the writer must be done with this buffer (from two snapshots ago)
+      auto t0 = std::chrono::steady_clock::now();
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return !busy_[b] || err_; });
+      blocked_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      busy_[b] = true;
+    }
+    hand_over_pending();  // the previous transfer is complete by now or soon
+    check(nls_get_field_async(h_, reinterpret_cast<double *>(buf_[b]), n_), h_);
+    pending_ = true;
+    pend_index_ = index;
+    pend_buf_ = b;
+  }
+  // all snapshots written; rethrows a callback error
+  void finish() {
+    if (done_) return;
+    hand_over_pending();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (writer_.joinable()) writer_.join();
+    done_ = true;
+    rethrow();
+  }
+  double blocked_seconds() const { return blocked_; }
+
+ private:
+  void hand_over_pending() {
+    if (!pending_) return;
+    check(nls_wait_field(h_), h_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      jobs_.push_back({pend_index_, pend_buf_});
+    }
+    cv_.notify_all();
+    pending_ = false;
+  }
+  void run() {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
+        if (jobs_.empty()) return;
+        j = jobs_.front();
+        jobs_.pop_front();
+      }
+      try {
+        if (!err_ && cb_) cb_(j.index, buf_[j.buf], n_);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!err_) err_ = std::current_exception();
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        busy_[j.buf] = false;
+      }
+      cv_.notify_all();
+    }
+  }
+  void rethrow() {
+    std::exception_ptr e;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      e = err_;
+    }
+    if (e) std::rethrow_exception(e);
+  }
+  struct Job {
+    uint32_t index = 0;
+    int buf = 0;
+  };
+  nls_handle *h_;
+  uint64_t n_;
+  Fn cb_;
+  T *buf_[2] = {nullptr, nullptr};
+  bool busy_[2] = {false, false};
+  int next_ = 0;
+  bool pending_ = false, done_ = false, stop_ = false;
+  uint32_t pend_index_ = 0;
+  int pend_buf_ = 0;
+  double blocked_ = 0.0;
+  std::deque<Job> jobs_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::exception_ptr err_;
+  std::thread writer_;
 };
 
 class Handle {
@@ -84,25 +212,34 @@ class NLSESolverDevice {
   };
   using SnapshotFn = std::function<void(uint32_t index, const std::complex<double> *u, uint64_t n)>;
 
-  // ctor stores snapshot 0 (the initial field), like device/nlse_solver_dev.hpp:83
+  // ctor stores snapshot 0 (the initial field), like device/nlse_solver_dev.hpp:83.
+  // Later snapshots go through a SnapshotPipe: the callback runs on its writer
+  // thread, in snapshot order; call finish() before using its results.
   NLSESolverDevice(const Grid &g, const std::complex<double> *host_u0, const Parameters &p,
                    SnapshotFn on_snapshot, int equation = NLS_NLSE_CUBIC, int device = -1,
                    std::complex<double> s1 = {0.0, 0.5}, std::complex<double> s2 = {-0.5, 0.0})
       : h_(g, equation, p.krylov_dim, device, s1, s2), p_(p), cb_(std::move(on_snapshot)),
-        buf_(h_.n()) {
+        pipe_(h_.get(), h_.n(), cb_) {
     check(nls_set_field(h_.get(), reinterpret_cast<const double *>(host_u0), h_.n()), h_.get());
-    emit(host_u0);
+    // snapshot 0 = u0, taken from the device copy (bit-identical) so that its
+    // file write also runs on the writer thread
+    pipe_.push(stored_++);
   }
 
   // tau = 1j*dt as in the reference (device/nlse_solver_dev.hpp:94); snapshot
   // when step_number % freq == 0, at most num_snapshots in total.
   void step(std::complex<double> tau, uint32_t step_number) {
     check(nls_step(h_.get(), tau.imag(), 1), h_.get());
-    if (p_.snapshot_freq && step_number % p_.snapshot_freq == 0 && stored_ < p_.num_snapshots) {
-      check(nls_get_field(h_.get(), reinterpret_cast<double *>(buf_.data()), h_.n()), h_.get());
-      emit(buf_.data());
-    }
+    if (p_.snapshot_freq && step_number % p_.snapshot_freq == 0 && stored_ < p_.num_snapshots)
+      pipe_.push(stored_++);
   }
+  void finish() { pipe_.finish(); }
+  // all enqueued steps and snapshot transfers complete (file writes may still run)
+  void sync() {
+    check(nls_sync(h_.get()), h_.get());
+    check(nls_wait_field(h_.get()), h_.get());
+  }
+  double blocked_seconds() const { return pipe_.blocked_seconds(); }
   void get_field(std::complex<double> *dst) {
     check(nls_get_field(h_.get(), reinterpret_cast<double *>(dst), h_.n()), h_.get());
   }
@@ -110,14 +247,10 @@ class NLSESolverDevice {
   uint64_t n() const { return h_.n(); }
 
  private:
-  void emit(const std::complex<double> *u) {
-    if (cb_) cb_(stored_, u, h_.n());
-    ++stored_;
-  }
   Handle h_;
   Parameters p_;
   SnapshotFn cb_;
-  std::vector<std::complex<double>> buf_;
+  SnapshotPipe<std::complex<double>> pipe_;
   uint32_t stored_ = 0;
 };
 
@@ -173,7 +306,8 @@ class NLSESolverDevice {
 
   NLSESolverDevice(const Grid &g, const std::complex<double> *host_u0, const double *host_m,
                    const double *host_c, const Parameters &p, SnapshotFn on_snapshot, int device = -1)
-      : h_(g, NLS_NLSE_G2, p.krylov_dim, device), p_(p), cb_(std::move(on_snapshot)), buf_(h_.n()) {
+      : h_(g, NLS_NLSE_G2, p.krylov_dim, device), p_(p), cb_(std::move(on_snapshot)),
+        pipe_(h_.get(), h_.n(), cb_) {
     check(nls_set_field(h_.get(), reinterpret_cast<const double *>(host_u0), h_.n()), h_.get());
     check(nls_set_coefficients(h_.get(), host_m, host_c, h_.n()), h_.get());
   }
@@ -185,13 +319,19 @@ class NLSESolverDevice {
   }
   void apply_bc() { check(nls_apply_bc(h_.get()), h_.get()); }  // nlse_dev.hpp:178-185
 
-  // nlse_dev.hpp:323-334: at most num_snapshots, silently ignored beyond
+  // nlse_dev.hpp:323-334: at most num_snapshots, silently ignored beyond.
+  // Asynchronous (SnapshotPipe): the callback runs on the writer thread.
   void store_snapshot_online() {
     if (stored_ >= p_.num_snapshots) return;
-    check(nls_get_field(h_.get(), reinterpret_cast<double *>(buf_.data()), h_.n()), h_.get());
-    if (cb_) cb_(stored_, buf_.data(), h_.n());
-    ++stored_;
+    pipe_.push(stored_++);
   }
+  void finish() { pipe_.finish(); }
+  // all enqueued steps and snapshot transfers complete (file writes may still run)
+  void sync() {
+    check(nls_sync(h_.get()), h_.get());
+    check(nls_wait_field(h_.get()), h_.get());
+  }
+  double blocked_seconds() const { return pipe_.blocked_seconds(); }
   uint32_t snapshots_stored() const { return stored_; }
   uint64_t n() const { return h_.n(); }
 
@@ -199,7 +339,7 @@ class NLSESolverDevice {
   Handle h_;
   Parameters p_;
   SnapshotFn cb_;
-  std::vector<std::complex<double>> buf_;
+  SnapshotPipe<std::complex<double>> pipe_;
   uint32_t stored_ = 0;
 };
 

@@ -14,8 +14,9 @@
 // it); m and c are float64 of the same shape; snapshot 0 = u0, then for
 // i = 1 .. nt-1: step (snapshot when i % freq == 0, before the BC), apply_bc;
 // output complex128 [ns, nz, ny, nx] (3D) or [ns, ny, nx] (2D); nothing on stdout.
-// Differences: snapshots are streamed to the output file as they are produced
-// (the reference holds ns*n complex values on the host); num_snapshots > nt is
+// Differences: snapshots are streamed to the output file as they are produced,
+// by a writer thread overlapping the time loop (the reference holds ns*n
+// complex values on the host and copies each snapshot synchronously); num_snapshots > nt is
 // rejected with exit 1 (the reference takes i % 0); a failed m/c load exits 1
 // after the reference's messages (the reference rethrows into std::terminate).
 #include <complex>
@@ -183,6 +184,7 @@ int main(int argc, char **argv) {
       solver.step(dti, i);
       solver.apply_bc();
     }
+    solver.finish();
     out.close();
   } catch (const std::exception &e) {
     std::cerr << "Error: " << e.what() << "\n";

@@ -29,6 +29,7 @@ EXPORTED_SYMBOLS = (
     "nls_get_field", "nls_get_sg_velocity", "nls_krylov_apply", "nls_laplacian_apply",
     "nls_rccl_unique_id", "nls_group_create", "nls_group_destroy", "nls_set_timing",
     "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
+    "nls_get_field_async", "nls_wait_field", "nls_host_alloc", "nls_host_free",
 )
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -96,6 +97,10 @@ def lib():
     L.nls_sync.argtypes = [H]
     L.nls_get_field.argtypes = [H, dp, C.c_uint64]
     L.nls_get_sg_velocity.argtypes = [H, C.c_double, dp, C.c_uint64]
+    L.nls_get_field_async.argtypes = [H, dp, C.c_uint64]
+    L.nls_wait_field.argtypes = [H]
+    L.nls_host_alloc.argtypes = [C.c_uint64, C.POINTER(C.c_void_p)]
+    L.nls_host_free.argtypes = [C.c_void_p]
     L.nls_krylov_apply.argtypes = [H, dp, C.c_double, C.c_double, C.c_int32, dp, C.c_uint64]
     L.nls_laplacian_apply.argtypes = [H, dp, dp, C.c_uint64]
     L.nls_rccl_unique_id.argtypes = [C.c_void_p]
@@ -247,6 +252,18 @@ class Solver:
         out = self._out()
         self._call(lib().nls_get_field, _dptr(out.view(np.float64)), self.n_local)
         return out
+
+    def get_field_async(self, out: np.ndarray):
+        """Enqueue a snapshot of the field into `out` (keep it alive and unread
+        until wait_field())."""
+        if out.dtype != self.dtype or out.size != self.n_local or not out.flags.c_contiguous:
+            raise NlsError(-2, "out must be a C-contiguous array of the field dtype and size")
+        self._async_out = out
+        self._call(lib().nls_get_field_async, _dptr(out.view(np.float64)), self.n_local)
+
+    def wait_field(self):
+        self._call(lib().nls_wait_field)
+        self._async_out = None
 
     def get_sg_velocity(self, dt):
         out = self._out(np.float64)

@@ -195,3 +195,27 @@ def test_shape_and_state_errors():
             s.set_field(np.zeros(10, complex))
     with pytest.raises(nls_amd.NlsError):
         nls_amd.Solver(2, 16, 16, 1, 0.5, 0.5, m=33)
+
+
+def test_async_snapshots_match_sync_field():
+    """nls_get_field_async (the G2 online snapshot, nlse_dev.hpp:323-334) captures the
+    field as of the enqueue point while later steps run; two back-to-back requests
+    are ordered on the device."""
+    n, L, m, dt = 48, 10.0, 12, 1e-3
+    dx = spacing(n, L)
+    u = soliton_field(2, n, n, 1, L, seed=9)
+    g = O.grid(2, n, n, 1, dx, dx)
+    with nls_amd.Solver(2, n, n, 1, dx, m=m) as s:
+        s.set_field(u)
+        s.step(dt, 3)
+        a = np.empty(n * n, complex)
+        b = np.empty(n * n, complex)
+        s.get_field_async(a)
+        s.step(dt, 1)
+        s.get_field_async(b)
+        s.step(dt, 2)
+        s.wait_field()
+        last = s.get_field()
+    assert rel_l2(a, O.nlse_steps(g, u, dt, 3, m)) <= TOL_TRAJ
+    assert rel_l2(b, O.nlse_steps(g, u, dt, 4, m)) <= TOL_TRAJ
+    assert rel_l2(last, O.nlse_steps(g, u, dt, 6, m)) <= TOL_TRAJ
