@@ -117,6 +117,12 @@ const char *nls_last_error(const nls_handle *h); /* h == NULL: last nls_create e
  * (3D: z, 2D: y); n_local = nzl * plane size. */
 int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t *n_local);
 
+/* The slab decomposition itself (pure function, no device needed): planes
+ * [*z0, *z0 + *nzl) of npl planes owned by `rank` of `nranks` -- contiguous,
+ * the first npl % nranks ranks one plane larger.  nls_local_planes() of a
+ * handle returns the same. */
+int nls_slab_planes(uint32_t npl, int32_t nranks, int32_t rank, uint32_t *z0, uint32_t *nzl);
+
 /* NLSE: u (complex interleaved, 2*n_local doubles).  SG: u (n_local doubles).
  * (The G2 drivers do not normalise u0, nlse_cubic_driver_3d.cpp:54-65; the G1
  * drivers do, nlse_call.cpp:41-49 -- the caller decides.) */

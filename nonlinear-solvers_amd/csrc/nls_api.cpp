@@ -503,11 +503,12 @@ void setup_geometry(nls_handle *h) {
   }
   g.P = g.nx * g.nyp;
   g.Ng = g.P * g.npl;
-  const int64_t base = g.npl / h->nranks, rem = g.npl % h->nranks;
-  g.nzl = base + (h->rank < rem ? 1 : 0);
+  uint32_t z0 = 0, nzl = 0;
+  nls_slab_planes((uint32_t)g.npl, h->nranks, h->rank, &z0, &nzl);
+  g.nzl = nzl;
+  g.z0 = z0;
   g.qa = 0;
   g.qb = (int32_t)g.nzl;
-  g.z0 = (int64_t)h->rank * base + std::min<int64_t>(h->rank, rem);
   g.nloc = g.nzl * g.P;
   // laplacians.hpp:49 (2D 1/(dx*dy)) and :102 (3D 1/(dx*dx)); values -4/-3, -6/-5 times scale
   g.s = c.dim == 2 ? 1.0 / (c.dx * c.dy) : 1.0 / (c.dx * c.dx);
@@ -783,6 +784,14 @@ int nls_destroy(nls_handle *h) {
 
 const char *nls_last_error(const nls_handle *h) {
   return h ? h->err.c_str() : g_create_error.c_str();
+}
+
+int nls_slab_planes(uint32_t npl, int32_t nranks, int32_t rank, uint32_t *z0, uint32_t *nzl) {
+  if (nranks < 1 || rank < 0 || rank >= nranks || (uint32_t)nranks > npl) return NLS_ERR_ARG;
+  const uint32_t base = npl / (uint32_t)nranks, rem = npl % (uint32_t)nranks;
+  if (nzl) *nzl = base + ((uint32_t)rank < rem ? 1u : 0u);
+  if (z0) *z0 = (uint32_t)rank * base + std::min<uint32_t>((uint32_t)rank, rem);
+  return NLS_OK;
 }
 
 int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t *n_local) {

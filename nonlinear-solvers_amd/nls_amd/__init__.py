@@ -16,7 +16,7 @@ import numpy as np
 __all__ = [
     "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "NLSE_G2", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
     "F_SINC2_SQRT", "F_ID_SQRT", "F_SINC2_HALF", "MAX_KRYLOV", "NlsError", "Config", "Solver",
-    "lib", "lib_path", "rccl_unique_id", "EXPORTED_SYMBOLS",
+    "lib", "lib_path", "rccl_unique_id", "slab_planes", "EXPORTED_SYMBOLS",
 ]
 
 NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI, NLSE_G2 = 0, 1, 2, 3
@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "nls_get_field", "nls_get_sg_velocity", "nls_krylov_apply", "nls_laplacian_apply",
     "nls_rccl_unique_id", "nls_group_create", "nls_group_destroy", "nls_set_timing",
     "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
-    "nls_get_field_async", "nls_wait_field", "nls_host_alloc", "nls_host_free",
+    "nls_get_field_async", "nls_wait_field", "nls_host_alloc", "nls_host_free", "nls_slab_planes",
 )
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -89,6 +89,8 @@ def lib():
     L.nls_last_error.restype = C.c_char_p
     L.nls_local_planes.argtypes = [H, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint64)]
+    L.nls_slab_planes.argtypes = [C.c_uint32, C.c_int32, C.c_int32, C.POINTER(C.c_uint32),
+                                  C.POINTER(C.c_uint32)]
     L.nls_set_field.argtypes = [H, dp, C.c_uint64]
     L.nls_set_sg_state.argtypes = [H, dp, dp, dp, C.c_uint64]
     L.nls_step.argtypes = [H, C.c_double, C.c_uint32]
@@ -113,6 +115,15 @@ def lib():
         raise RuntimeError("libnls_amd ABI mismatch")
     _LIB = L
     return L
+
+
+def slab_planes(npl: int, nranks: int, rank: int) -> tuple[int, int]:
+    """(z0, nzl) of `rank`'s slab -- the library's own decomposition (no device needed)."""
+    z0, nzl = C.c_uint32(), C.c_uint32()
+    rc = lib().nls_slab_planes(npl, nranks, rank, C.byref(z0), C.byref(nzl))
+    if rc != 0:
+        raise NlsError(rc, "bad slab arguments")
+    return z0.value, nzl.value
 
 
 def rccl_unique_id() -> bytes:

@@ -1,0 +1,106 @@
+"""world_size 2 / 3 gloo tests of the N > 1 path, on CPU.
+
+What runs on N GPUs is (a) bench.py's host orchestration -- RCCL id broadcast,
+per-rank slab of the synthetic input, global mass normalisation, barrier and
+max-over-ranks timing -- and (b) the library's slab decomposition with halo
+exchange and all-reduced dots.  (a) is exercised here with the real bench.py
+helpers over gloo; (b) with tests/dist_model.py, a numpy restatement of the same
+data movement (ghost planes, one-plane halos incl. the 3D y-wrap, split
+reductions) whose gathered result must equal the single-process oracle.  The
+GPU implementation of (b) is tested against the oracle in
+tests/test_gpu_multirank.py (in-process ranks, RCCL collective path).
+"""
+import json
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, case, outdir):
+    import dist_model as DM  # noqa: F401  (sets sys.path)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = {}
+        if case["kind"] == "nlse":
+            import oracle_py as O
+            dim, n, m, dt, steps = case["dim"], case["n"], case["m"], case["dt"], case["steps"]
+            L = 10.0
+            dx = 2 * L / (n - 1)
+            sl = DM.Slab(dim, n, n, n, dx, dx, rank, world)
+            N = n ** dim
+            rng = np.random.default_rng(5)
+            u = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+            u_loc = u[sl.z0 * sl.P:(sl.z0 + sl.nzl) * sl.P]
+            # one stencil application with halos == the oracle operator
+            lap = DM.gather(sl, sl.lap(sl.ext(u_loc)))
+            out = DM.gather(sl, DM.nlse_steps_dist(sl, u_loc, dt, steps, m))
+            if rank == 0:
+                g = O.grid(dim, n, n, n, dx, dx)
+                res["lap"] = float(np.linalg.norm(lap - O.laplacian_c(g, u)) / np.linalg.norm(O.laplacian_c(g, u)))
+                ref = O.nlse_steps(g, u, dt, steps, m)
+                res["traj"] = float(np.linalg.norm(out - ref) / np.linalg.norm(ref))
+        else:  # bench.py orchestration helpers
+            import bench
+            w = dict(bench.WORKLOADS[case["workload"]])
+            w["n"] = case["n"]
+            import nls_amd
+            npl = w["n"]
+            z0, nzl = nls_amd.slab_planes(npl, world, rank)
+            u = bench.synthetic_ic(w, z0, nzl)
+            dx = 2 * w["L"] / (w["n"] - 1)
+            mass = bench.global_mass(u, dx ** w["dim"], dist)
+            full = DM.gather(DM.Slab(w["dim"], w["n"], w["n"], w["n"], dx, dx, rank, world), u)
+            el = bench.max_over_ranks(0.1 * (rank + 1), dist)
+            if rank == 0:
+                ref = bench.synthetic_ic(w, 0, npl)
+                res["ic_equal"] = bool(np.array_equal(full, ref))
+                res["mass"] = float(abs(mass - np.sum(np.abs(ref) ** 2) * dx ** w["dim"]) / mass)
+                res["max"] = el
+        if rank == 0:
+            with open(os.path.join(outdir, "res.json"), "w") as f:
+                json.dump(res, f)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, case):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), case, d), nprocs=world, join=True,
+                           start_method="spawn")
+        with open(os.path.join(d, "res.json")) as f:
+            return json.load(f)
+
+
+@pytest.mark.parametrize("world,dim,n", [(2, 3, 10), (3, 3, 11), (2, 2, 24), (3, 2, 17)])
+def test_slab_decomposition_matches_single_process_oracle(world, dim, n):
+    """Halo planes (incl. the 3D y-wrap across slab boundaries) and all-reduced
+    dots reproduce the single-process operator and a 3-step SS2 trajectory."""
+    r = _run(world, dict(kind="nlse", dim=dim, n=n, m=10, dt=1e-3, steps=3))
+    assert r["lap"] <= 1e-15
+    assert r["traj"] <= 1e-12
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_orchestration_over_gloo(world):
+    """bench.py N>1 host logic: slab ICs concatenate to the single-rank IC, the
+    mass normalisation is global, the timing is the max over ranks."""
+    r = _run(world, dict(kind="bench", workload="nlse3d_512", n=20))
+    assert r["ic_equal"]
+    assert r["mass"] < 1e-14
+    assert abs(r["max"] - 0.1 * world) < 1e-12
