@@ -45,7 +45,7 @@ def main():
             h, mi = c["TCC_HIT_sum"], c["TCC_MISS_sum"]
             e["l2_hit_rate"] = h / max(h + mi, 1)
         kernels[name] = e
-    dom = next((k for k in kernels if re.fullmatch(rf"k_update<.*, {J}>", k)), None)
+    dom = next((k for k in kernels if re.fullmatch(rf"k_update<[^,]*, [23], {J}(, (true|false))?>", k)), None)
     res = {
         "workload": workload, "m": m, "cells": cells,
         "dominant_kernel": dom,
