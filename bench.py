@@ -44,6 +44,10 @@ WORKLOADS = {
     # G2 production driver (nlse_cubic_driver_3d.cpp: m=25, m(x), c(x), Neumann BC per step)
     "g2_3d_256": dict(dim=3, n=256, L=10.0, m=25, eq=3, dt=1e-3,
                       desc="G2 3D cubic NLSE 256^3 with m(x), div(c grad), Neumann BC, Krylov m=25, fp64 complex"),
+    # G2 sEWI driver (nlse_cubic_sewi_driver_3d.cpp: m=15, three Krylov actions per step)
+    "sewi_3d_256": dict(dim=3, n=256, L=10.0, m=15, eq=3, dt=1e-3, sewi=True,
+                        desc="G2 3D cubic NLSE 256^3, sEWI integrator, m(x), div(c grad), Neumann BC, "
+                             "Krylov m=15, fp64 complex"),
 }
 
 
@@ -58,11 +62,16 @@ def g2_coefficients(n, L, z0, nzl):
     return mf.ravel(), cf.ravel()
 
 
-def algorithmic_bytes_per_cell_step(m: int, eq: int) -> int:
+def algorithmic_bytes_per_cell_step(m: int, eq: int, sewi: bool = False) -> int:
     """SURVEY.md 8(d): E(m) = ((m-1)(m+2)/2 + m + 3) * 16 B (NLSE c128);
-    E_SG(m) = ((m-1)(m+2) + 2m + 10) * 8 B (sine-Gordon f64)."""
+    E_SG(m) = ((m-1)(m+2) + 2m + 10) * 8 B (sine-Gordon f64).  sEWI: three
+    Krylov actions per step, each (m-1)(m+2)/2 + m + 1 elements (start vector
+    written, basis streamed, result combined), plus B(u), u_prev copy and the
+    final update (read u, e, write u, u_prev)."""
     if eq == 2:
         return ((m - 1) * (m + 2) + 2 * m + 10) * 8
+    if sewi:
+        return (3 * ((m - 1) * (m + 2) // 2 + m + 1) + 8) * 16
     return ((m - 1) * (m + 2) // 2 + m + 3) * 16
 
 
@@ -139,7 +148,20 @@ def cpu_baseline(args):
     import oracle_py
 
     w = dict(WORKLOADS[args.workload])
-    if w["eq"] == 3:
+    if w.get("sewi"):
+        ns, steps = 48, 3
+        w["n"] = ns
+        dx = 2 * w["L"] / (ns - 1)
+        u = synthetic_ic(w, 0, ns)
+        mf, cf = g2_coefficients(ns, w["L"], 0, ns)
+        g = oracle_py.grid(3, ns, ns, ns, dx, dx)
+        u1, up1 = oracle_py.nlse_sewi_steps(g, cf, mf, u, None, w["dt"], 1, 1, w["m"])  # step 1 (SS2)
+        t0 = time.perf_counter()
+        oracle_py.nlse_sewi_steps(g, cf, mf, u1, up1, w["dt"], 2, steps, w["m"])
+        el = time.perf_counter() - t0
+        cells = ns ** 3
+        sample = f"G2 3D sEWI {ns}^3 m={w['m']}, {steps} sEWI steps + BC (sub-grid of the workload, 1 thread)"
+    elif w["eq"] == 3:
         ns, steps = 64, 3
         w["n"] = ns
         dx = 2 * w["L"] / (ns - 1)
@@ -250,8 +272,15 @@ def main():
     del u
     dt = w["dt"]
 
+    step_no = [0]
+
     def run(k):
-        if w["eq"] == 3:  # the G2 driver loop: step, then apply_bc (nlse_cubic_driver_3d.cpp:116-119)
+        if w.get("sewi"):  # nlse_cubic_sewi_driver_3d.cpp: step_sewi(i), apply_bc
+            for _ in range(k):
+                step_no[0] += 1
+                s.step_sewi(dt, step_no[0])
+                s.apply_bc()
+        elif w["eq"] == 3:  # the G2 driver loop: step, then apply_bc (nlse_cubic_driver_3d.cpp:116-119)
             for _ in range(k):
                 s.step(dt, 1)
                 s.apply_bc()
@@ -287,7 +316,7 @@ def main():
     bytes_launch = (J + 2) * esz * n_local
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if cnt else None
     traffic = load_traffic(args.workload, m) if world == 1 else None
-    step_bytes = algorithmic_bytes_per_cell_step(m, w["eq"]) * n_local
+    step_bytes = algorithmic_bytes_per_cell_step(m, w["eq"], w.get("sewi", False)) * n_local
     step_ms = el * 1e3 / args.steps
     result = {
         "metric": "Mcells*steps/s and achieved HBM GB/s, 3D NLSE 512^3 at 1/2/4/8 MI355X"
@@ -304,7 +333,8 @@ def main():
         "dtype": "f64" if w["eq"] == 2 else "c128 (fp64 complex)",
         "data": "synthetic (8 random Gaussian solitons + 1e-3 complex white noise, seeded)",
         "config": {"workload": w["desc"], "grid": [n] * dim, "krylov_m": m, "dt": dt,
-                   "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi", "nlse_g2"][w["eq"]],
+                   "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi", "nlse_g2"][w["eq"]]
+                   + ("_sewi" if w.get("sewi") else ""),
                    "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
         "roofline": {
             "bound": "hbm",
@@ -318,7 +348,7 @@ def main():
             "avg_launch_ms": avg_ms,
         },
         "step_roofline": {
-            "algorithmic_bytes_per_cell_step": algorithmic_bytes_per_cell_step(m, w["eq"]),
+            "algorithmic_bytes_per_cell_step": algorithmic_bytes_per_cell_step(m, w["eq"], w.get("sewi", False)),
             "achieved_GBs": step_bytes / (step_ms * 1e-3) / 1e9,
             "frac": step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "gpu_kernel_ms_per_step": {k: v / max(tm["steps"], 1) for k, v in tm["class_ms"].items()},

@@ -23,6 +23,7 @@
  *   nls_step         <- NLSESolverDevice::step(tau=1j*dt, i)               device/nlse_solver_dev.hpp:94-111
  *                       SGESolverDevice::step(tau=dt, i)                   device/sg_solver_dev.hpp:168-193
  *                       G2 NLSESolverDevice::step(tau=1j*dt, i)            nlsolvers/device/include/nlse_dev.hpp:187-203
+ *   nls_step_sewi    <- G2 NLSESolverDevice::step_sewi(tau=1j*dt, i)       nlsolvers/device/include/nlse_dev.hpp:205-238
  *   nls_get_field    <- transfer_snapshots(dst) / store_snapshot D2D+D2H   device/nlse_solver_dev.hpp:113-124
  *   nls_get_field_async / nls_wait_field
  *                    <- store_snapshot_online(host_dst) (G2)               nlsolvers/device/include/nlse_dev.hpp:323-334
@@ -85,7 +86,8 @@ enum nls_func {
   NLS_F_SINC_SQRT = 3,  /* sinc(t*sqrt|lambda|)     eigen_krylov_real.hpp:87-105 */
   NLS_F_SINC2_SQRT = 4, /* sinc^2(t*sqrt|lambda|)   eigen_krylov_real.hpp:107-141 */
   NLS_F_ID_SQRT = 5,    /* t*sqrt|lambda|           eigen_krylov_real.hpp:143-170 */
-  NLS_F_SINC2_HALF = 6  /* sinc^2(t/2*sqrt|lambda|) eigen_krylov_real.hpp:172-201 */
+  NLS_F_SINC2_HALF = 6, /* sinc^2(t/2*sqrt|lambda|) eigen_krylov_real.hpp:172-201 */
+  NLS_F_SINC = 7        /* sinc(t*lambda), G2 "sinc" nlsolvers/device/include/matfunc_complex.hpp:290-300 */
 };
 
 typedef struct nls_config {
@@ -142,6 +144,14 @@ int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfie
  * all coordinates clamped into [1, n-2].  Complex (NLSE) handles; needs >= 3
  * cells per dimension.  Like nls_step it is enqueued asynchronously. */
 int nls_apply_bc(nls_handle *h);
+
+/* G2 only: one step of the symmetric exponential wave integrator,
+ * NLSESolverDevice::step_sewi(tau = 1j*dt, step_number)
+ * (nlsolvers/device/include/nlse_dev.hpp:205-238): step_number 1 saves
+ * u_prev = u and takes an SS2 step; later steps compute
+ *   u <- exp(2 tau L) u_prev - 2 tau exp(tau L) sinc(dt L) B(u),  B(u) = -m|u|^2 u,
+ * and u_prev <- the old u (three Krylov actions per step). */
+int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number);
 
 /* Enqueue nsteps time steps (NLSE: tau = 1j*dt; SG: tau = dt) on the handle's
  * stream and return.  Errors of asynchronous execution surface at nls_sync /

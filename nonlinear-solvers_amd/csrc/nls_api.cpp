@@ -92,6 +92,8 @@ struct nls_handle {
   double *cfb = nullptr;    // G2 anisotropy c(x): (nzl + 2) planes, local plane 0 at +P
   bool ani = false;         // G2 operator div(c grad) (laplacians.hpp:54-218)
   bool u_slot = false;      // u stored as slot m of basis 0
+  void *uprev = nullptr;    // G2 sEWI: u of the previous step (nlse_dev.hpp:206-229)
+  bool uprev_set = false;
   int64_t u_off = 0;        // extra element offset of that slot
   bool coef_set = false;
   void *scratch = nullptr;  // nloc elements
@@ -605,10 +607,10 @@ void free_all(nls_handle *h) {
     h->B[b] = Basis{};
   }
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
-  for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap,
+  for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
                   (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
-  h->u = h->scratch = h->snap = nullptr;
+  h->u = h->scratch = h->snap = h->uprev = nullptr;
   h->up = h->mf = h->cfb = nullptr;
   h->partA = h->partU = nullptr;
 }
@@ -876,6 +878,86 @@ int nls_apply_bc(nls_handle *h) {
   });
 }
 
+// One Strang SS2 step of an NLSE handle.
+// NLSESolverDevice::step (device/nlse_solver_dev.hpp:94-111), tau = 1j*dt:
+//   N(1/2) -> exp(L*dt) via exp(t|lambda|), t = -tau -> N(1/2)
+// G2 (nlsolvers/device/include/nlse_dev.hpp:187-203): N uses +tau/2 m|u|^2
+// and the linear flow is exp(t*lambda) with t = +tau
+// (nlsolvers/device/include/matfunc_complex.hpp:281-287).
+void ss2_step(nls_handle *h, double dt) {
+  const int m = h->m;
+  const int64_t n = h->geo.nloc;
+  int64_t vs = h->vs;
+  if (!h->w0_ready || h->w0_dt != dt) {
+    void *w0 = vec_ptr(h, 0, 0);
+    int nl = h->nonlin;
+    void *args[] = {&h->u, &w0, &h->mf, (void *)&n, &dt, &nl, &h->s1, &h->s2};
+    pw_launch(h, 3, kernel_nl_init(), args);
+    halo(h, 0, 0);
+  }
+  if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt);
+  else run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt);
+  void *W = vec_ptr(h, 0, 0);
+  KState *st = h->B[0].st;
+  int nl = h->nonlin;
+  void *args[] = {&W, &vs, (void *)&n, &st, &h->u, &h->mf, &dt, &nl, &h->s1, &h->s2};
+  pw_launch(h, 3, kernel_final_nlse(m), args);
+  halo(h, 0, 0);
+  h->w0_ready = true;
+  h->w0_dt = dt;
+}
+
+int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number) {
+  return guarded(h, [&] {
+    if (!h->ani) fail(h, NLS_ERR_STATE, "nls_step_sewi needs a G2 (NLS_NLSE_G2) handle");
+    if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
+    if (!h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
+    if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");
+    if (step_number == 0) fail(h, NLS_ERR_ARG, "step numbers start at 1 (nlse_dev.hpp:206)");
+    const int m = h->m;
+    int64_t n = h->geo.nloc, vs = h->vs;
+    const size_t bytes = (size_t)n * sizeof(cplx);
+    if (!h->uprev) hip_check(h, hipMalloc(&h->uprev, bytes), "hipMalloc(u_prev)");
+    if (step_number == 1) {  // nlse_dev.hpp:206-210: u_prev = u, then an SS2 step
+      hip_check(h, hipMemcpyAsync(h->uprev, h->u, bytes, hipMemcpyDeviceToDevice, h->stream), "D2D");
+      h->uprev_set = true;
+      ss2_step(h, dt);
+    } else {
+      if (!h->uprev_set) fail(h, NLS_ERR_STATE, "sEWI step > 1 before step 1 (no u_prev)");
+      void *W = vec_ptr(h, 0, 0);
+      KState *st = h->B[0].st;
+      // B(u) -> sinc(dt L) B -> exp(tau L) (.) -> e (scratch)
+      {
+        void *args[] = {&h->u, &h->mf, &W, &n};
+        pw_launch(h, 3, kernel_sewi_b(), args);
+        halo(h, 0, 0);
+      }
+      run_lanczos(h, 0, 1, NLS_F_SINC, 0, dt, 0.0);
+      {
+        void *args[] = {&W, &vs, &n, &st};
+        pw_launch(h, 3, kernel_combine_w0(m), args);
+        halo(h, 0, 0);
+      }
+      run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt);
+      {
+        void *args[] = {&W, &vs, &n, &st, &h->scratch};
+        pw_launch(h, 3, kernel_combine(true, m), args);
+      }
+      // exp(2 tau L) u_prev, then u = that - 2 tau e, u_prev <- old u
+      hip_check(h, hipMemcpyAsync(W, h->uprev, bytes, hipMemcpyDeviceToDevice, h->stream), "D2D");
+      halo(h, 0, 0);
+      run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, 2.0 * dt);
+      {
+        void *args[] = {&W, &vs, &n, &st, &h->u, &h->uprev, &h->scratch, &dt};
+        pw_launch(h, 3, kernel_sewi_end(m), args);
+      }
+      h->w0_ready = false;
+    }
+    h->tacc.steps += 1;
+    hip_check(h, hipGetLastError(), "kernel launch");
+  });
+}
+
 int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
   return guarded(h, [&] {
     if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
@@ -891,28 +973,7 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
       if (ra > 0 && h->steps_issued >= (uint64_t)ra)
         hip_check(h, hipEventSynchronize(h->stepev[h->steps_issued % ra]), "hipEventSynchronize");
       if (h->cplx_) {
-        // NLSESolverDevice::step (device/nlse_solver_dev.hpp:94-111), tau = 1j*dt:
-        //   N(1/2) -> exp(L*dt) via exp(t|lambda|), t = -tau -> N(1/2)
-        // G2 (nlsolvers/device/include/nlse_dev.hpp:187-203): N uses +tau/2 m|u|^2
-        // and the linear flow is exp(t*lambda) with t = +tau
-        // (nlsolvers/device/include/matfunc_complex.hpp:281-287).
-        if (!h->w0_ready || h->w0_dt != dt) {
-          void *w0 = vec_ptr(h, 0, 0);
-          int nl = h->nonlin;
-          void *args[] = {&h->u, &w0, &h->mf, (void *)&n, &dt, &nl, &h->s1, &h->s2};
-          pw_launch(h, 3, kernel_nl_init(), args);
-          halo(h, 0, 0);
-        }
-        if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt);
-        else run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt);
-        void *W = vec_ptr(h, 0, 0);
-        KState *st = h->B[0].st;
-        int nl = h->nonlin;
-        void *args[] = {&W, &vs, (void *)&n, &st, &h->u, &h->mf, &dt, &nl, &h->s1, &h->s2};
-        pw_launch(h, 3, kernel_final_nlse(m), args);
-        halo(h, 0, 0);
-        h->w0_ready = true;
-        h->w0_dt = dt;
+        ss2_step(h, dt);
       } else {
         // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u
         run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0);
@@ -1031,7 +1092,7 @@ int nls_krylov_apply(nls_handle *h, const double *in, double t_re, double t_im, 
                      double *out, uint64_t n) {
   return guarded(h, [&] {
     if (!in || !out) fail(h, NLS_ERR_ARG, "NULL buffer");
-    if (func < 0 || func > 6) fail(h, NLS_ERR_ARG, "unknown func");
+    if (func < 0 || func > 7) fail(h, NLS_ERR_ARG, "unknown func");
     if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     check_len(h, n);
     const int b = h->cplx_ ? 0 : 1;  // SG: the scratch basis keeps u intact

@@ -205,6 +205,13 @@ __device__ cplx eval_f(int func, double lam, double t_re, double t_im) {
       const double s = sin(x) / x;
       return {s * s, 0.0};
     }
+    case 7: {  // G2 "sinc": sinc(t*lambda), nlsolvers/device/include/matfunc_complex.hpp:293-300
+      const double a = t_re * lam, b = t_im * lam;
+      if (hypot(a, b) < 1e-8) return {1.0, 0.0};
+      const cplx sv = {sin(a) * cosh(b), cos(a) * sinh(b)};
+      const double d = a * a + b * b;
+      return {(sv.re * a + sv.im * b) / d, (sv.im * a - sv.re * b) / d};
+    }
     default: return {__builtin_nan(""), __builtin_nan("")};
   }
 }
@@ -478,6 +485,60 @@ __global__ __launch_bounds__(NTHREADS) void k_neumann_bc(cplx *__restrict__ u, c
   }
 }
 
+// ---- G2 sEWI (nlsolvers/device/include/nlse_dev.hpp:205-238) ----------------
+// start vector B(u) = -m |u|^2 u  (compute_B, nlse_dev.hpp:42-50)
+__global__ __launch_bounds__(NTHREADS) void k_sewi_b(const cplx *__restrict__ u, const double *__restrict__ mf,
+                                                     cplx *__restrict__ w0, int64_t n) {
+  for (int64_t p = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * NTHREADS) {
+    const cplx v = u[p];
+    const double s = -mf[p] * (v.re * v.re + v.im * v.im);
+    w0[p] = s * v;
+  }
+}
+
+// W_0 <- sum_k fin_k W_k in place: the result of one action becomes the start
+// vector of the next (each thread reads all M values of its cell first)
+template <int M>
+__global__ __launch_bounds__(NTHREADS) void k_combine_w0(cplx *W, int64_t vs, int64_t n,
+                                                         const KState *__restrict__ st) {
+  __shared__ cplx cf[MMAX];
+  for (int k = threadIdx.x; k < M; k += NTHREADS) cf[k] = st->fin[0][k];
+  __syncthreads();
+  for (int64_t p = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * NTHREADS) {
+    cplx w[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) w[k] = ld_nt(W + (int64_t)k * vs + p);
+    cplx y = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < M; ++k) y += cmul(cf[k], w[k]);
+    W[p] = y;
+  }
+}
+
+// apply_sewi (nlse_dev.hpp:52-63):  u_new = exp(2 tau L) u_prev - 2 tau e,
+// e = exp(tau L) sinc(dt L) B(u) (in `e`); u_prev <- old u.  tau = 1j*dt.
+template <int M>
+__global__ __launch_bounds__(NTHREADS) void k_sewi_end(const cplx *__restrict__ W, int64_t vs, int64_t n,
+                                                       const KState *__restrict__ st,
+                                                       cplx *__restrict__ u, cplx *__restrict__ up,
+                                                       const cplx *__restrict__ e, double dt) {
+  __shared__ cplx cf[MMAX];
+  for (int k = threadIdx.x; k < M; k += NTHREADS) cf[k] = st->fin[0][k];
+  __syncthreads();
+  const cplx two_tau = {0.0, 2.0 * dt};
+  for (int64_t p = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * NTHREADS) {
+    cplx y = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < M; ++k) y += cmul(cf[k], ld_nt(W + (int64_t)k * vs + p));
+    const cplx uo = u[p];
+    u[p] = y - cmul(two_tau, e[p]);
+    up[p] = uo;
+  }
+}
+
 // out = sum_k fin[fi][k] W_k  (one matrix-function action)
 template <class S, int M>
 __global__ __launch_bounds__(NTHREADS) void k_combine(const S *__restrict__ W, int64_t vs, int64_t n,
@@ -584,6 +645,25 @@ const void *kernel_reduce_final() { return reinterpret_cast<const void *>(&k_red
 const void *kernel_nl_init() { return reinterpret_cast<const void *>(&k_nl_init); }
 const void *kernel_sg_velocity() { return reinterpret_cast<const void *>(&k_sg_velocity); }
 const void *kernel_neumann_bc() { return reinterpret_cast<const void *>(&k_neumann_bc); }
+const void *kernel_sewi_b() { return reinterpret_cast<const void *>(&k_sewi_b); }
+
+const void *kernel_combine_w0(int M) {
+  switch (M) {
+#define X(M) case M: return reinterpret_cast<const void *>(&k_combine_w0<M>);
+    NLS_M_LIST(X)
+#undef X
+    default: return nullptr;
+  }
+}
+
+const void *kernel_sewi_end(int M) {
+  switch (M) {
+#define X(M) case M: return reinterpret_cast<const void *>(&k_sewi_end<M>);
+    NLS_M_LIST(X)
+#undef X
+    default: return nullptr;
+  }
+}
 
 const void *kernel_final_nlse(int M) {
   switch (M) {

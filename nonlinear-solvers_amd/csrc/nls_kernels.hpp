@@ -58,6 +58,13 @@ const void *kernel_sg_mid(int M);
 const void *kernel_sg_end(int M);
 const void *kernel_sg_velocity();
 const void *kernel_neumann_bc();
+//   sewi_b    : (const cplx* u, const double* mf, cplx* w0, int64_t n)
+//   combine_w0: (cplx* W, int64_t vs, int64_t n, const KState*)          -- W_0 <- sum fin_k W_k
+//   sewi_end  : (const cplx* W, int64_t vs, int64_t n, const KState*, cplx* u, cplx* up,
+//                const cplx* e, double dt)
+const void *kernel_sewi_b();
+const void *kernel_combine_w0(int M);
+const void *kernel_sewi_end(int M);
 int64_t neumann_bc_cells(const Geo &g);
 
 }  // namespace nls

@@ -319,6 +319,12 @@ class NLSESolverDevice {
   }
   void apply_bc() { check(nls_apply_bc(h_.get()), h_.get()); }  // nlse_dev.hpp:178-185
 
+  // nlse_dev.hpp:205-238 (step 1: SS2 + u_prev; snapshots as step())
+  void step_sewi(std::complex<double> tau, uint32_t step_number) {
+    check(nls_step_sewi(h_.get(), tau.imag(), step_number), h_.get());
+    if (p_.snapshot_freq && step_number % p_.snapshot_freq == 0) store_snapshot_online();
+  }
+
   // nlse_dev.hpp:323-334: at most num_snapshots, silently ignored beyond.
   // Asynchronous (SnapshotPipe): the callback runs on the writer thread.
   void store_snapshot_online() {

@@ -2,7 +2,10 @@
 // nlsolvers/device/drivers/nlse_cubic_driver_3d.cpp (13 positional args,
 // Krylov m = 25) and nlse_cubic_driver_2d.cpp (11 positional args, m = 20),
 // CMake targets nlse_3d_dev / nlse_2d_dev (nlsolvers/device/drivers/
-// CMakeLists.txt:63-65), on the MI355X library:
+// CMakeLists.txt:63-65), on the MI355X library.  Built with -DG2_SEWI=1 the
+// same source gives nlse_sewi_3d_dev / nlse_sewi_2d_dev
+// (nlse_cubic_sewi_driver_{3d,2d}.cpp, CMakeLists.txt:64,66): step_sewi
+// instead of step, Krylov m = 15 (3D) / 25 (2D), otherwise identical.
 //
 //   3D: prog nx ny nz Lx Ly Lz input_u0.npy output_traj.npy T nt num_snapshots input_m.npy input_c.npy
 //   2D: prog nx ny Lx Ly input_u0.npy output_traj.npy T nt num_snapshots input_m.npy input_c.npy
@@ -30,6 +33,15 @@
 
 #ifndef G2_DIM
 #define G2_DIM 3
+#endif
+#ifndef G2_SEWI
+#define G2_SEWI 0
+#endif
+// Krylov dimension of each reference driver
+#if G2_SEWI
+constexpr int G2_M = G2_DIM == 3 ? 15 : 25;  // nlse_cubic_sewi_driver_3d.cpp:113, _2d.cpp:105
+#else
+constexpr int G2_M = G2_DIM == 3 ? 25 : 20;  // nlse_cubic_driver_3d.cpp:113, _2d.cpp:105
 #endif
 
 namespace {
@@ -98,7 +110,7 @@ int main(int argc, char **argv) {
     T = std::stod(a.pos[6 + 2 * o]);
     nt = std::stoul(a.pos[7 + 2 * o]);
     ns = std::stoul(a.pos[8 + 2 * o]);
-    m = cli::flag_int(a, "m", G2_DIM == 3 ? 25 : 20);
+    m = cli::flag_int(a, "m", G2_M);
     device = cli::flag_int(a, "device", -1);
   } catch (const std::exception &e) {
     std::cerr << "Error: bad argument (" << e.what() << ")\n";
@@ -181,7 +193,11 @@ int main(int argc, char **argv) {
     solver.store_snapshot_online();
     const std::complex<double> dti(0.0, dt);
     for (uint32_t i = 1; i < nt; ++i) {
+#if G2_SEWI
+      solver.step_sewi(dti, i);
+#else
       solver.step(dti, i);
+#endif
       solver.apply_bc();
     }
     solver.finish();

@@ -15,12 +15,12 @@ import numpy as np
 
 __all__ = [
     "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "NLSE_G2", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
-    "F_SINC2_SQRT", "F_ID_SQRT", "F_SINC2_HALF", "MAX_KRYLOV", "NlsError", "Config", "Solver",
+    "F_SINC2_SQRT", "F_ID_SQRT", "F_SINC2_HALF", "F_SINC", "MAX_KRYLOV", "NlsError", "Config", "Solver",
     "lib", "lib_path", "rccl_unique_id", "slab_planes", "EXPORTED_SYMBOLS",
 ]
 
 NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI, NLSE_G2 = 0, 1, 2, 3
-F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF = range(7)
+F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF, F_SINC = range(8)
 MAX_KRYLOV = 32
 
 EXPORTED_SYMBOLS = (
@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "nls_rccl_unique_id", "nls_group_create", "nls_group_destroy", "nls_set_timing",
     "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
     "nls_get_field_async", "nls_wait_field", "nls_host_alloc", "nls_host_free", "nls_slab_planes",
+    "nls_step_sewi",
 )
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -94,6 +95,7 @@ def lib():
     L.nls_set_field.argtypes = [H, dp, C.c_uint64]
     L.nls_set_sg_state.argtypes = [H, dp, dp, dp, C.c_uint64]
     L.nls_step.argtypes = [H, C.c_double, C.c_uint32]
+    L.nls_step_sewi.argtypes = [H, C.c_double, C.c_uint32]
     L.nls_set_coefficients.argtypes = [H, dp, dp, C.c_uint64]
     L.nls_apply_bc.argtypes = [H]
     L.nls_sync.argtypes = [H]
@@ -252,6 +254,10 @@ class Solver:
     def apply_bc(self):
         """Neumann copy BC of the G2 drivers (boundaries.cuh:10-81)."""
         self._call(lib().nls_apply_bc)
+
+    def step_sewi(self, dt, step_number):
+        """G2 sEWI step (nlse_dev.hpp:205-238); step_number 1 is an SS2 step."""
+        self._call(lib().nls_step_sewi, float(dt), int(step_number))
 
     def step(self, dt, nsteps=1):
         self._call(lib().nls_step, float(dt), int(nsteps))

@@ -263,6 +263,10 @@ cd eval_f(int func, double lam, cd t) {
   switch (func) {
     case ORACLE_F_EXP_ABS: return std::exp(t * std::fabs(lam));
     case ORACLE_F_EXP: return std::exp(t * lam);
+    case ORACLE_F_SINC: {  // nlsolvers/device/include/matfunc_complex.hpp:293-300
+      const cd val = t * lam;
+      return std::abs(val) < 1e-8 ? cd(1.0, 0.0) : std::sin(val) / val;
+    }
     default: break;
   }
   const double x = t.real() * std::sqrt(std::fabs(lam));
@@ -517,6 +521,42 @@ int oracle_nlse_g2_steps(const oracle_grid *g, const double *c, const double *mf
     krylov_apply(op, buf.data(), tau, m, ORACLE_F_EXP, out.data());
     nonlin_half_g2(out.data(), mfield, n, dt);
     std::memcpy(u, out.data(), n * sizeof(cd));
+    if (bc) neumann_bc(G, u);
+  }
+  return 0;
+}
+
+int oracle_nlse_sewi_steps(const oracle_grid *g, const double *c, const double *mfield,
+                           double *u_, double *up_, double dt, uint32_t first_step,
+                           uint32_t nsteps, uint32_t m, int bc) {
+  Grid G;
+  if (!make_grid(g, G) || !c || !mfield || !u_ || !up_ || m < 1 || first_step < 1) return -1;
+  if (bc && (G.nx < 3 || G.ny < 3 || (G.dim == 3 && G.nz < 3))) return -1;
+  AnisoOp op{G, c};
+  const uint64_t n = G.N;
+  cd *u = as_c(u_), *up = as_c(up_);
+  std::vector<cd> buf(n), b2(n), b3(n);
+  const cd tau(0.0, dt);
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    const uint32_t step_number = first_step + s;
+    if (step_number == 1) {  // nlse_dev.hpp:206-210: u_prev = u; SS2 step
+      std::memcpy(up, u, n * sizeof(cd));
+      std::memcpy(buf.data(), u, n * sizeof(cd));
+      nonlin_half_g2(buf.data(), mfield, n, dt);
+      krylov_apply(op, buf.data(), tau, m, ORACLE_F_EXP, b2.data());
+      nonlin_half_g2(b2.data(), mfield, n, dt);
+      std::memcpy(u, b2.data(), n * sizeof(cd));
+    } else {  // nlse_dev.hpp:211-229
+      std::memcpy(buf.data(), u, n * sizeof(cd));
+      for (uint64_t p = 0; p < n; ++p)  // compute_B, nlse_dev.hpp:42-50
+        b2[p] = -mfield[p] * (u[p].real() * u[p].real() + u[p].imag() * u[p].imag()) * u[p];
+      krylov_apply(op, b2.data(), cd(dt, 0.0), m, ORACLE_F_SINC, b3.data());
+      krylov_apply(op, b3.data(), tau, m, ORACLE_F_EXP, b2.data());
+      krylov_apply(op, up, 2.0 * tau, m, ORACLE_F_EXP, b3.data());
+      const cd two_tau = 2.0 * tau;
+      for (uint64_t p = 0; p < n; ++p) u[p] = b3[p] - two_tau * b2[p];  // apply_sewi :52-63
+      std::memcpy(up, buf.data(), n * sizeof(cd));
+    }
     if (bc) neumann_bc(G, u);
   }
   return 0;

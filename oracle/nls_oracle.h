@@ -43,7 +43,8 @@ enum {
   ORACLE_F_SINC_SQRT = 3, /* sinc(t*sqrt|lambda|)      eigen_krylov_real.hpp:87-105 */
   ORACLE_F_SINC2_SQRT = 4,/* sinc^2(t*sqrt|lambda|)    eigen_krylov_real.hpp:107-141 */
   ORACLE_F_ID_SQRT = 5,   /* t*sqrt|lambda|            eigen_krylov_real.hpp:143-170 */
-  ORACLE_F_SINC2_HALF = 6 /* sinc^2(t/2*sqrt|lambda|)  eigen_krylov_real.hpp:172-201 */
+  ORACLE_F_SINC2_HALF = 6,/* sinc^2(t/2*sqrt|lambda|)  eigen_krylov_real.hpp:172-201 */
+  ORACLE_F_SINC = 7       /* sinc(t*lambda) (G2 "sinc") nlsolvers/device/include/matfunc_complex.hpp:290-300 */
 };
 
 int oracle_laplacian_apply_c(const oracle_grid *g, const double *x, double *y);
@@ -88,6 +89,16 @@ int oracle_neumann_bc_c(const oracle_grid *g, double *u);
 int oracle_nlse_g2_steps(const oracle_grid *g, const double *c,
                          const double *mfield, double *u, double dt,
                          uint32_t nsteps, uint32_t m, int bc);
+
+/* G2 sEWI stepper (NLSESolverDevice::step_sewi, nlsolvers/device/include/nlse_dev.hpp:205-238)
+ * for step numbers first_step .. first_step+nsteps-1: step 1 is an SS2 step that
+ * saves u_prev = u; later steps u <- exp(2 tau L) u_prev - 2 tau exp(tau L)
+ * sinc(dt L) B(u), B(u) = -m|u|^2 u, u_prev <- old u.  bc != 0: Neumann copy BC
+ * after every step (nlse_cubic_sewi_driver_3d.cpp).  u, u_prev in/out. */
+int oracle_nlse_sewi_steps(const oracle_grid *g, const double *c,
+                           const double *mfield, double *u, double *u_prev,
+                           double dt, uint32_t first_step, uint32_t nsteps,
+                           uint32_t m, int bc);
 
 /* sine-Gordon Gautschi (sg_solver.hpp:53-74); u, u_past updated in place. */
 int oracle_sg_steps(const oracle_grid *g, double *u, double *u_past,

@@ -21,7 +21,7 @@ from __future__ import annotations
 import numpy as np
 import scipy.sparse as sp
 
-F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF = range(7)
+F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF, F_SINC = range(8)
 
 
 def _shape(dim, nx, ny, nz):
@@ -145,6 +145,30 @@ def nlse_g2_steps(dim, nx, ny, nz, dx, dy, c, mfield, u, dt, nsteps, m, bc=True)
     return u
 
 
+def nlse_sewi_steps(dim, nx, ny, nz, dx, dy, c, mfield, u, u_prev, dt, first_step, nsteps, m, bc=True):
+    """G2 sEWI (nlsolvers/device/include/nlse_dev.hpp:205-238) + driver BC."""
+    A = aniso_laplacian(dim, nx, ny, nz, dx, dy, c)
+    ap = lambda v: A @ v
+    mf = np.asarray(mfield, dtype=np.float64).ravel()
+    u = np.asarray(u, dtype=np.complex128).ravel().copy()
+    up = u.copy() if u_prev is None else np.asarray(u_prev, dtype=np.complex128).ravel().copy()
+    N = lambda v: v * np.exp(0.5 * 1j * dt * (mf * (v.real * v.real + v.imag * v.imag)))
+    for s in range(nsteps):
+        i = first_step + s
+        if i == 1:
+            up = u.copy()
+            u = N(krylov(ap, N(u), 1j * dt, m, F_EXP))
+        else:
+            B = -mf * (u.real * u.real + u.imag * u.imag) * u
+            e = krylov(ap, krylov(ap, B, dt, m, F_SINC), 1j * dt, m, F_EXP)
+            new = krylov(ap, up, 2j * dt, m, F_EXP) - 2j * dt * e
+            up = u
+            u = new
+        if bc:
+            u = neumann_bc(dim, nx, ny, nz, u)
+    return u, up
+
+
 def laplacian_apply(dim, nx, ny, nz, dx, dy, x):
     """Vectorised matrix-free application (same operator, flat-index form)."""
     x = np.asarray(x).ravel()
@@ -203,6 +227,10 @@ def _f(func, lam, t):
         return np.exp(t * np.abs(lam))
     if func == F_EXP:
         return np.exp(t * lam)
+    if func == F_SINC:  # sinc(t*lambda), complex t (matfunc_complex.hpp:293-300)
+        val = t * lam + 0j
+        safe = np.where(np.abs(val) < 1e-8, 1.0, val)
+        return np.where(np.abs(val) < 1e-8, 1.0, np.sin(safe) / safe)
     x = np.real(t) * np.sqrt(np.abs(lam))
     sinc = lambda z: np.where(np.abs(z) < 1e-8, 1.0, np.sin(z) / np.where(z == 0, 1, z))
     if func == F_COS_SQRT:

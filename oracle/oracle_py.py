@@ -47,6 +47,8 @@ def lib():
         L.oracle_neumann_bc_c.argtypes = [g, dp]
         L.oracle_nlse_g2_steps.argtypes = [g, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
                                            C.c_int]
+        L.oracle_nlse_sewi_steps.argtypes = [g, dp, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
+                                             C.c_uint32, C.c_int]
     return _LIB
 
 
@@ -154,3 +156,12 @@ def nlse_g2_steps(g, c, mfield, u, dt, nsteps, m, bc=True):
     ui = _c(u).copy()
     _check(lib().oracle_nlse_g2_steps(C.byref(g), _r(c), _r(mfield), ui, dt, nsteps, m, 1 if bc else 0))
     return ui.view(np.complex128)
+
+
+def nlse_sewi_steps(g, c, mfield, u, u_prev, dt, first_step, nsteps, m, bc=True):
+    """G2 sEWI steps first_step .. first_step+nsteps-1; returns (u, u_prev)."""
+    ui = _c(u).copy()
+    pi = _c(u if u_prev is None else u_prev).copy()
+    _check(lib().oracle_nlse_sewi_steps(C.byref(g), _r(c), _r(mfield), ui, pi, dt, first_step, nsteps, m,
+                                        1 if bc else 0))
+    return ui.view(np.complex128), pi.view(np.complex128)

@@ -108,6 +108,19 @@ def main():
         tw = np_ref.nlse_g2_steps(dim, n, n, n, dx, dx, cf, mf, u0, dt, steps, m, bc=True)
         assert np.linalg.norm(out - tw) / np.linalg.norm(tw) < 1e-12
         cases[name] = dict(dim=dim, n=n, dx=dx, dt=dt, steps=steps, m=m, u0=u0, c=cf, mfield=mf, u=out)
+    # --- G2 sEWI (nlse_cubic_sewi_driver_3d.cpp: m=15), steps 1..6 with BC ----
+    n, m, steps, L = 10, 15, 6, 4.0
+    dx = 2 * L / (n - 1)
+    rng = np.random.default_rng(21)
+    u0 = field(3, n, L, 22)
+    N = u0.size
+    cf = 1.0 + 0.3 * np.cos(np.arange(N) * 0.21) + 0.1 * rng.random(N)
+    mf = 1.0 + 0.2 * rng.standard_normal(N)
+    g = O.grid(3, n, n, n, dx, dx)
+    out, outp = O.nlse_sewi_steps(g, cf, mf, u0, None, dt, 1, steps, m, bc=True)
+    tw, twp = np_ref.nlse_sewi_steps(3, n, n, n, dx, dx, cf, mf, u0, None, dt, 1, steps, m, bc=True)
+    assert np.linalg.norm(out - tw) / np.linalg.norm(tw) < 1e-12
+    cases["sewi_3d"] = dict(dim=3, n=n, dx=dx, dt=dt, steps=steps, m=m, u0=u0, c=cf, mfield=mf, u=out, u_prev=outp)
     for name, d in cases.items():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **{k: np.asarray(v) for k, v in d.items()})
     total = sum(os.path.getsize(os.path.join(HERE, f"{k}.npz")) for k in cases)

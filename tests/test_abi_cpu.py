@@ -127,7 +127,8 @@ def test_npy_codec_rejects_wrong_dtype(tmp_path):
 # ---- G2 drivers (nlse_3d_dev / nlse_2d_dev): argv and input contract, no GPU needed
 
 
-@pytest.mark.parametrize("prog,npos", [("nlse_3d_dev", 13), ("nlse_2d_dev", 11)])
+@pytest.mark.parametrize("prog,npos", [("nlse_3d_dev", 13), ("nlse_2d_dev", 11), ("nlse_sewi_3d_dev", 13),
+                                      ("nlse_sewi_2d_dev", 11)])
 def test_g2_driver_usage(prog, npos):
     for k in (0, npos - 2, npos - 1, npos + 1):   # nlse_cubic_driver_3d.cpp:20-31 (argc != 14)
         r = run([os.path.join(BIN, prog)] + ["8"] * k)

@@ -233,3 +233,93 @@ def test_g2_driver_matches_oracle(tmp_path, dim):
     assert np.array_equal(traj[0].ravel(), u)
     for k in range(1, ns):
         assert rel_l2(traj[k].ravel(), expect[k]) <= TOL_TRAJ, k
+
+
+# ---- sEWI (NLSESolverDevice::step_sewi, nlse_dev.hpp:205-238) ----------------
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", GRIDS[:5])
+def test_sinc_action_matches_oracle(dim, nx, ny, nz):
+    """G2 "sinc": sinc(t*lambda) with real t = dt (matfunc_complex.hpp:290-300)."""
+    dx = 8.0 / (nx - 1)
+    u, mf, c = fields(dim, nx, ny, nz, seed=8)
+    g = O.grid(dim, nx, ny, nz, dx, dx)
+    m = min(15, nx * ny * nz)
+    with solver(dim, nx, ny, nz, dx, m) as s:
+        s.set_coefficients(mf, c)
+        for t in (1e-3, 2e-2):
+            ref = O.krylov_aniso_c(g, c, u, t, m, nls_amd.F_SINC)
+            assert rel_l2(s.krylov_apply(u, t, nls_amd.F_SINC), ref) <= TOL_KRYLOV
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,m", [(3, 12, 12, 12, 15), (3, 70, 9, 11, 15), (2, 32, 32, 1, 25),
+                                            (2, 300, 20, 1, 25)])
+def test_sewi_trajectory_matches_oracle(dim, nx, ny, nz, m):
+    """The sEWI driver loop (nlse_cubic_sewi_driver_3d.cpp:116-119): step_sewi(i), apply_bc."""
+    L, dt, steps = 4.0, 1e-3, 8
+    dx = 2 * L / (nx - 1)
+    u, mf, c = fields(dim, nx, ny, nz, seed=9)
+    g = O.grid(dim, nx, ny, nz, dx, dx)
+    ref, _ = O.nlse_sewi_steps(g, c, mf, u, None, dt, 1, steps, m, bc=True)
+    with solver(dim, nx, ny, nz, dx, m) as s:
+        s.set_coefficients(mf, c)
+        s.set_field(u)
+        for i in range(1, steps + 1):
+            s.step_sewi(dt, i)
+            s.apply_bc()
+        out = s.get_field()
+    assert rel_l2(out, ref) <= TOL_TRAJ
+
+
+def test_sewi_golden_and_errors():
+    d = np.load(os.path.join(GOLD, "sewi_3d.npz"))
+    n, m, dt = int(d["n"]), int(d["m"]), float(d["dt"])
+    with solver(3, n, n, n, float(d["dx"]), m) as s:
+        s.set_coefficients(d["mfield"], d["c"])
+        s.set_field(d["u0"])
+        with pytest.raises(nls_amd.NlsError) as e:
+            s.step_sewi(dt, 2)       # no u_prev yet
+        assert e.value.code == -6
+        for i in range(1, int(d["steps"]) + 1):
+            s.step_sewi(dt, i)
+            s.apply_bc()
+        assert rel_l2(s.get_field(), d["u"]) <= TOL_TRAJ
+    with nls_amd.Solver(3, 8, 8, 8, 0.5, m=4) as s:
+        s.set_field(np.ones(512, complex))
+        with pytest.raises(nls_amd.NlsError) as e:
+            s.step_sewi(1e-3, 1)
+        assert e.value.code == -6
+
+
+@pytest.mark.parametrize("dim", [3, 2])
+def test_sewi_driver_matches_oracle(tmp_path, dim):
+    n, L, T, nt, ns = (10, 4.0, 0.02, 10, 5) if dim == 3 else (20, 4.0, 0.02, 10, 5)
+    m = 15 if dim == 3 else 25
+    dx = 2 * L / (n - 1)
+    u, mf, c = fields(dim, n, n, n, seed=10, L=L)
+    shp = (n,) * dim
+    paths = {k: str(tmp_path / f"{k}.npy") for k in ("u0", "m", "c", "out")}
+    np.save(paths["u0"], u.reshape(shp))
+    np.save(paths["m"], mf.reshape(shp))
+    np.save(paths["c"], c.reshape(shp))
+    if dim == 3:
+        args = [os.path.join(BIN, "nlse_sewi_3d_dev"), str(n), str(n), str(n), str(L), str(L), str(L)]
+    else:
+        args = [os.path.join(BIN, "nlse_sewi_2d_dev"), str(n), str(n), str(L), str(L)]
+    args += [paths["u0"], paths["out"], str(T), str(nt), str(ns), paths["m"], paths["c"]]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    traj = np.load(paths["out"])
+    assert traj.shape == (ns,) + shp
+    g = O.grid(dim, n, n, n, dx, dx)
+    dt, freq = T / nt, nt // ns
+    cur, prev = u.copy(), None
+    expect = [u.copy()]
+    for i in range(1, nt):
+        cur, prev = O.nlse_sewi_steps(g, c, mf, cur, prev, dt, i, 1, m, bc=False)
+        if i % freq == 0 and len(expect) < ns:
+            expect.append(cur.copy())
+        cur = O.neumann_bc(g, cur)
+    assert np.array_equal(traj[0].ravel(), u)
+    for k in range(1, ns):
+        assert rel_l2(traj[k].ravel(), expect[k]) <= TOL_TRAJ, k

@@ -260,3 +260,47 @@ def test_golden_g2(name):
     g = O.grid(dim, n, n, n, float(d["dx"]), float(d["dx"]))
     out = O.nlse_g2_steps(g, d["c"], d["mfield"], d["u0"], float(d["dt"]), int(d["steps"]), int(d["m"]))
     assert rel_l2(out, d["u"]) < 1e-13
+
+
+@pytest.mark.parametrize("dim,n,m", [(2, 14, 25), (3, 7, 15)])
+def test_sewi_oracle_matches_numpy_twin(dim, n, m):
+    """G2 sEWI (nlsolvers/device/include/nlse_dev.hpp:205-238), two restatements."""
+    rng = np.random.default_rng(11 + dim)
+    N = n ** dim
+    c = rng.uniform(0.5, 2.0, N)
+    mf = rng.uniform(0.5, 1.5, N)
+    u = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    g = O.grid(dim, n, n, n, 0.6, 0.6)
+    a, ap = O.nlse_sewi_steps(g, c, mf, u, None, 1e-3, 1, 4, m, bc=True)
+    b, bp = np_ref.nlse_sewi_steps(dim, n, n, n, 0.6, 0.6, c, mf, u, None, 1e-3, 1, 4, m, bc=True)
+    assert rel_l2(a, b) < 1e-12 and rel_l2(ap, bp) < 1e-12
+    # resuming at step 3 with the state after step 2 is the same trajectory
+    s2, s2p = O.nlse_sewi_steps(g, c, mf, u, None, 1e-3, 1, 2, m, bc=True)
+    r, rp = O.nlse_sewi_steps(g, c, mf, s2, s2p, 1e-3, 3, 2, m, bc=True)
+    assert np.array_equal(r, a) and np.array_equal(rp, ap)
+
+
+def test_sinc_function_convention():
+    """G2 "sinc" is sinc(t*lambda) with no |.| or sqrt (matfunc_complex.hpp:293-300):
+    on a 1-D invariant subspace (an eigenvector of L) the action is the scalar map."""
+    n = 6
+    g = O.grid(2, n, n, 1, 1.0, 1.0)
+    ones = np.ones(n * n)
+    # constants are in the kernel of div(c grad): lambda = 0 -> sinc = 1
+    v = np.ones(n * n, complex)
+    assert rel_l2(O.krylov_aniso_c(g, ones, v, 0.3, 4, 7), v) < 1e-14
+    A = np_ref.aniso_laplacian(2, n, n, 1, 1.0, 1.0, ones).toarray()
+    lam, Q = np.linalg.eigh(A)
+    q = Q[:, 3].astype(complex)
+    t = 0.37
+    want = np.sin(t * lam[3]) / (t * lam[3]) * q
+    assert rel_l2(O.krylov_aniso_c(g, ones, q, t, 3, 7), want) < 1e-12
+
+
+def test_golden_sewi():
+    d = np.load(os.path.join(GOLD, "sewi_3d.npz"))
+    n = int(d["n"])
+    g = O.grid(3, n, n, n, float(d["dx"]), float(d["dx"]))
+    u, up = O.nlse_sewi_steps(g, d["c"], d["mfield"], d["u0"], None, float(d["dt"]), 1, int(d["steps"]),
+                              int(d["m"]))
+    assert rel_l2(u, d["u"]) < 1e-13 and rel_l2(up, d["u_prev"]) < 1e-13
