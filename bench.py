@@ -44,6 +44,10 @@ WORKLOADS = {
     # G2 production driver (nlse_cubic_driver_3d.cpp: m=25, m(x), c(x), Neumann BC per step)
     "g2_3d_256": dict(dim=3, n=256, L=10.0, m=25, eq=3, dt=1e-3,
                       desc="G2 3D cubic NLSE 256^3 with m(x), div(c grad), Neumann BC, Krylov m=25, fp64 complex"),
+    # G2 Klein-Gordon Gautschi driver (kg_driver_dev_3d.cpp: m=10, m(x), c(x), BC per step)
+    "kg_3d_256": dict(dim=3, n=256, L=10.0, m=10, eq=4, dt=1e-3,
+                      desc="G2 3D Klein-Gordon 256^3 (u_tt = div(c grad u) - m u^3), Gautschi, Neumann BC, "
+                           "Krylov m=10, fp64"),
     # G2 sEWI driver (nlse_cubic_sewi_driver_3d.cpp: m=15, three Krylov actions per step)
     "sewi_3d_256": dict(dim=3, n=256, L=10.0, m=15, eq=3, dt=1e-3, sewi=True,
                         desc="G2 3D cubic NLSE 256^3, sEWI integrator, m(x), div(c grad), Neumann BC, "
@@ -68,7 +72,7 @@ def algorithmic_bytes_per_cell_step(m: int, eq: int, sewi: bool = False) -> int:
     Krylov actions per step, each (m-1)(m+2)/2 + m + 1 elements (start vector
     written, basis streamed, result combined), plus B(u), u_prev copy and the
     final update (read u, e, write u, u_prev)."""
-    if eq == 2:
+    if eq in (2, 4):  # two real Krylov bases per step (SG: id+cos / sinc^2; KG: cos / sinc^2)
         return ((m - 1) * (m + 2) + 2 * m + 10) * 8
     if sewi:
         return (3 * ((m - 1) * (m + 2) // 2 + m + 1) + 8) * 16
@@ -85,7 +89,7 @@ def synthetic_ic(w, z0, nzl, seed=1234):
     wid = rng.uniform(0.5, 1.5, 8)
     x = np.linspace(-L, L, n)
     plane = n * n if dim == 3 else n
-    if w["eq"] == 2:
+    if w["eq"] in (2, 4):
         out = np.empty(nzl * plane, dtype=np.float64)
     else:
         out = np.empty(nzl * plane, dtype=np.complex128)
@@ -99,7 +103,7 @@ def synthetic_ic(w, z0, nzl, seed=1234):
             f = fy @ (fz[k][:, None] * fx.T)     # sum_s fz_s(k) fy_s(y) fx_s(x)
             nr = np.random.default_rng((seed, k))
             f += 1e-3 * (nr.standard_normal((n, n)) + 1j * nr.standard_normal((n, n)))
-            out[q * plane:(q + 1) * plane] = f.ravel()
+            out[q * plane:(q + 1) * plane] = (f.real if w["eq"] == 4 else f).ravel()
     else:
         for q in range(nzl):
             k = z0 + q
@@ -161,6 +165,18 @@ def cpu_baseline(args):
         el = time.perf_counter() - t0
         cells = ns ** 3
         sample = f"G2 3D sEWI {ns}^3 m={w['m']}, {steps} sEWI steps + BC (sub-grid of the workload, 1 thread)"
+    elif w["eq"] == 4:
+        ns, steps = 64, 3
+        w["n"] = ns
+        dx = 2 * w["L"] / (ns - 1)
+        u = synthetic_ic(w, 0, ns)
+        mf, cf = g2_coefficients(ns, w["L"], 0, ns)
+        g = oracle_py.grid(3, ns, ns, ns, dx, dx)
+        t0 = time.perf_counter()
+        oracle_py.kg_steps(g, cf, mf, u, u.copy(), w["dt"], steps, w["m"])
+        el = time.perf_counter() - t0
+        cells = ns ** 3
+        sample = f"G2 3D Klein-Gordon {ns}^3 m={w['m']}, {steps} Gautschi steps + BC (sub-grid, 1 thread)"
     elif w["eq"] == 3:
         ns, steps = 64, 3
         w["n"] = ns
@@ -263,6 +279,10 @@ def main():
     u = synthetic_ic(w, s.z0, s.nzl)
     if w["eq"] == 2:
         s.set_sg_state(u, u.copy(), -np.ones(u.size))
+    elif w["eq"] == 4:  # KG: u0 real part of the synthetic field, v0 = 0
+        mf, cf = g2_coefficients(n, w["L"], s.z0, s.nzl)
+        s.set_coefficients(mf, cf)
+        s.set_sg_state(u, u.copy())
     elif w["eq"] == 3:  # G2 drivers do not normalise u0 (nlse_cubic_driver_3d.cpp:54-65)
         s.set_field(u)
         s.set_coefficients(*g2_coefficients(n, w["L"], s.z0, s.nzl))
@@ -280,7 +300,7 @@ def main():
                 step_no[0] += 1
                 s.step_sewi(dt, step_no[0])
                 s.apply_bc()
-        elif w["eq"] == 3:  # the G2 driver loop: step, then apply_bc (nlse_cubic_driver_3d.cpp:116-119)
+        elif w["eq"] in (3, 4):  # the G2 driver loop: step, then apply_bc (nlse_cubic_driver_3d.cpp:116-119)
             for _ in range(k):
                 s.step(dt, 1)
                 s.apply_bc()
@@ -312,7 +332,7 @@ def main():
     J = max(m - 2, 0)
     cnt = tm["update_count"][J]
     avg_ms = tm["update_ms"][J] / cnt if cnt else float("nan")
-    esz = 8 if w["eq"] == 2 else 16
+    esz = 8 if w["eq"] in (2, 4) else 16
     bytes_launch = (J + 2) * esz * n_local
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if cnt else None
     traffic = load_traffic(args.workload, m) if world == 1 else None
@@ -330,10 +350,10 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f64" if w["eq"] == 2 else "c128 (fp64 complex)",
+        "dtype": "f64" if w["eq"] in (2, 4) else "c128 (fp64 complex)",
         "data": "synthetic (8 random Gaussian solitons + 1e-3 complex white noise, seeded)",
         "config": {"workload": w["desc"], "grid": [n] * dim, "krylov_m": m, "dt": dt,
-                   "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi", "nlse_g2"][w["eq"]]
+                   "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi", "nlse_g2", "kg_gautschi"][w["eq"]]
                    + ("_sewi" if w.get("sewi") else ""),
                    "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
         "roofline": {

@@ -16,6 +16,7 @@
  *                       (the operator is described by grid parameters, not by a CSR matrix)
  *   nls_set_field    <- cudaMemcpy H2D of host_u0 in the ctors above       device/nlse_solver_dev.hpp:63-64
  *   nls_set_sg_state <- SGESolverDevice ctor u0/u_past/m uploads           device/sg_solver_dev.hpp:118-135
+ *                       KGESolverDevice ctor (G2)                          nlsolvers/device/include/kg_dev.hpp
  *   nls_set_coefficients <- NLSESolverDevice(L, u0, m, ...) (G2) m upload  nlsolvers/device/include/nlse_dev.hpp:66-130
  *                       build_anisotropic_laplacian_noflux{,_3d}(.., c)   nlsolvers/common/include/laplacians.hpp:54-103,158-218
  *   nls_apply_bc     <- NLSESolverDevice::apply_bc() (G2)                  nlsolvers/device/include/nlse_dev.hpp:178-185,
@@ -72,10 +73,14 @@ enum nls_equation {
   NLS_NLSE_CUBIC = 0,   /* i u_t + Lap u + |u|^2 u = 0, SS2 (nlse_solver.hpp:53-77) */
   NLS_NLSE_CQ = 1,      /* rho = s1|u|^2 + s2|u|^4 (device/nlse_cq_solver.hpp:16-39) */
   NLS_SG_GAUTSCHI = 2,  /* u_tt = Lap u + m sin u, Gautschi (sg_solver.hpp:53-74) */
-  NLS_NLSE_G2 = 3       /* G2 cubic NLSE with focusing field m(x) and anisotropic operator
+  NLS_NLSE_G2 = 3,      /* G2 cubic NLSE with focusing field m(x) and anisotropic operator
                            div(c grad): SS2 with exp(+tau/2 m|u|^2) and exp(tau*lambda)
                            (nlsolvers/device/include/nlse_dev.hpp:187-203,
                            nlsolvers/device/drivers/nlse_cubic_driver_{2d,3d}.cpp) */
+  NLS_KG_GAUTSCHI = 4   /* G2 Klein-Gordon u_tt = div(c grad u) - m u^3, Gautschi with
+                           cos / sinc^2 of t sqrt|lambda| (nlsolvers/device/include/kg_single.cuh:49-86,
+                           kg_driver_dev_{2d,3d}.cpp); real field; m, c via
+                           nls_set_coefficients, u / u_past via nls_set_sg_state */
 };
 
 /* Krylov matrix functions f, applied as f(L) u (nls_krylov_apply) */
@@ -129,7 +134,8 @@ int nls_slab_planes(uint32_t npl, int32_t nranks, int32_t rank, uint32_t *z0, ui
  * (The G2 drivers do not normalise u0, nlse_cubic_driver_3d.cpp:54-65; the G1
  * drivers do, nlse_call.cpp:41-49 -- the caller decides.) */
 int nls_set_field(nls_handle *h, const double *u, uint64_t n_local);
-/* SG only: u, u_past = u0 - dt*v0 (sg_driver_dev.cpp:64,106) and the m(x) field. */
+/* SG / KG: u, u_past = u0 - dt*v0 (sg_driver_dev.cpp:64,106) and the m(x) field
+ * (KG: mfield may be NULL when nls_set_coefficients supplies it). */
 int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past,
                      const double *mfield, uint64_t n_local);
 

@@ -91,6 +91,9 @@ struct nls_handle {
   double *mf = nullptr;     // SG m(x), G2 NLSE focusing field m(x)
   double *cfb = nullptr;    // G2 anisotropy c(x): (nzl + 2) planes, local plane 0 at +P
   bool ani = false;         // G2 operator div(c grad) (laplacians.hpp:54-218)
+  bool kg = false;          // G2 Klein-Gordon Gautschi (real, ani)
+  double *vel = nullptr;    // KG velocity v = (u - u_past)/dt of the last step
+  bool vel_valid = false;   //   (set by every KG step, before the driver's BC)
   bool u_slot = false;      // u stored as slot m of basis 0
   void *uprev = nullptr;    // G2 sEWI: u of the previous step (nlse_dev.hpp:206-229)
   bool uprev_set = false;
@@ -549,16 +552,17 @@ void alloc_all(nls_handle *h) {
   if (h->cplx_) {
     if (h->u_slot) h->u = vec_ptr(h, 0, h->m) + h->u_off * (int64_t)h->esize;
     else hip_check(h, hipMalloc(&h->u, nbytes), "hipMalloc(u)");
-    if (h->ani) {
-      const size_t cbytes = (size_t)(g.nzl + 2) * g.P * sizeof(double);
-      hip_check(h, hipMalloc(&h->mf, (size_t)g.nloc * sizeof(double)), "hipMalloc(m)");
-      hip_check(h, hipMalloc(&h->cfb, cbytes), "hipMalloc(c)");
-      hip_check(h, hipMemsetAsync(h->cfb, 0, cbytes, h->stream), "hipMemset");
-      h->geo.cf = h->cfb + g.P;
-    }
+    if (h->ani) hip_check(h, hipMalloc(&h->mf, (size_t)g.nloc * sizeof(double)), "hipMalloc(m)");
   } else {
     hip_check(h, hipMalloc(&h->up, nbytes), "hipMalloc(u_past)");
     hip_check(h, hipMalloc(&h->mf, nbytes), "hipMalloc(m)");
+    if (h->kg) hip_check(h, hipMalloc(&h->vel, nbytes), "hipMalloc(v)");
+  }
+  if (h->ani) {
+    const size_t cbytes = (size_t)(g.nzl + 2) * g.P * sizeof(double);
+    hip_check(h, hipMalloc(&h->cfb, cbytes), "hipMalloc(c)");
+    hip_check(h, hipMemsetAsync(h->cfb, 0, cbytes, h->stream), "hipMemset");
+    h->geo.cf = h->cfb + g.P;
   }
   hip_check(h, hipMalloc(&h->scratch, nbytes), "hipMalloc(scratch)");
   // grid sizes from measured occupancy; partial buffers sized for the largest
@@ -608,10 +612,11 @@ void free_all(nls_handle *h) {
   }
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
+                  (void *)h->vel,
                   (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
   h->u = h->scratch = h->snap = h->uprev = nullptr;
-  h->up = h->mf = h->cfb = nullptr;
+  h->up = h->mf = h->cfb = h->vel = nullptr;
   h->partA = h->partU = nullptr;
 }
 
@@ -664,7 +669,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   const nls_config &c = *cfg;
   std::string why;
   if (c.dim != 2 && c.dim != 3) why = "dim must be 2 or 3";
-  else if (c.equation < 0 || c.equation > 3) why = "unknown equation";
+  else if (c.equation < 0 || c.equation > 4) why = "unknown equation";
   else if (c.equation == NLS_SG_GAUTSCHI && c.dim != 2 && c.dim != 3) why = "bad dim";
   else if (c.nx < 2 || c.ny < 2 || (c.dim == 3 && c.nz < 2)) why = "grid too small (need >= 2 per dimension)";
   else if (!(c.dx > 0.0) || !(c.dy > 0.0)) why = "dx, dy must be > 0";
@@ -674,10 +679,12 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   else if (c.local_group && static_cast<nls_group *>(c.local_group)->n != c.nranks)
     why = "local_group size != nranks";
   else if ((uint32_t)c.nranks > (c.dim == 3 ? c.nz : c.ny)) why = "more ranks than planes";
-  else if (c.equation == NLS_NLSE_G2 && (c.nx < 3 || c.ny < 3 || (c.dim == 3 && c.nz < 3)))
-    why = "G2 NLSE needs >= 3 cells per dimension (Neumann copy boundary)";
-  else if (c.equation == NLS_NLSE_G2 && (uint32_t)(2 * c.nranks) > (c.dim == 3 ? c.nz : c.ny))
-    why = "G2 NLSE needs >= 2 planes per rank";
+  else if ((c.equation == NLS_NLSE_G2 || c.equation == NLS_KG_GAUTSCHI) &&
+           (c.nx < 3 || c.ny < 3 || (c.dim == 3 && c.nz < 3)))
+    why = "G2 NLSE / KG need >= 3 cells per dimension (Neumann copy boundary)";
+  else if ((c.equation == NLS_NLSE_G2 || c.equation == NLS_KG_GAUTSCHI) &&
+           (uint32_t)(2 * c.nranks) > (c.dim == 3 ? c.nz : c.ny))
+    why = "G2 NLSE / KG need >= 2 planes per rank";
   if (!why.empty()) {
     g_create_error = why;
     return NLS_ERR_ARG;
@@ -688,12 +695,13 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
     return NLS_ERR_OOM;
   }
   h->cfg = c;
-  h->cplx_ = c.equation != NLS_SG_GAUTSCHI;
+  h->cplx_ = c.equation != NLS_SG_GAUTSCHI && c.equation != NLS_KG_GAUTSCHI;
   h->esize = h->cplx_ ? 16 : 8;
   h->m = (int)c.krylov_m;
   h->nbasis = h->cplx_ ? 1 : 2;
   h->nonlin = c.equation == NLS_NLSE_CQ ? 1 : (c.equation == NLS_NLSE_G2 ? 2 : 0);
-  h->ani = c.equation == NLS_NLSE_G2;
+  h->kg = c.equation == NLS_KG_GAUTSCHI;
+  h->ani = c.equation == NLS_NLSE_G2 || h->kg;
   h->s1 = {c.sigma1[0], c.sigma1[1]};
   h->s2 = {c.sigma2[0], c.sigma2[1]};
   h->rank = c.rank;
@@ -825,14 +833,17 @@ int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past, const
                      uint64_t n) {
   return guarded(h, [&] {
     if (h->cplx_) fail(h, NLS_ERR_STATE, "nls_set_sg_state on an NLSE handle");
-    if (!u || !u_past || !mfield) fail(h, NLS_ERR_ARG, "NULL input");
+    // KG: m(x) may instead come with nls_set_coefficients (NULL keeps it)
+    if (!u || !u_past || (!mfield && !h->kg)) fail(h, NLS_ERR_ARG, "NULL input");
     check_len(h, n);
     copy_in_vector(h, 0, 0, u);
     const size_t bytes = (size_t)n * sizeof(double);
     hip_check(h, hipMemcpyAsync(h->up, u_past, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
-    hip_check(h, hipMemcpyAsync(h->mf, mfield, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    if (mfield)
+      hip_check(h, hipMemcpyAsync(h->mf, mfield, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
     halo(h, 0, 0);
     h->field_set = true;
+    h->vel_valid = false;
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
   });
 }
@@ -855,13 +866,24 @@ int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfie
 
 int nls_apply_bc(nls_handle *h) {
   return guarded(h, [&] {
-    if (!h->cplx_) fail(h, NLS_ERR_STATE, "nls_apply_bc on a sine-Gordon handle");
+    if (!h->cplx_ && !h->kg) fail(h, NLS_ERR_STATE, "nls_apply_bc on a G1 sine-Gordon handle");
     if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
     const Geo &g = h->geo;
     if (g.nx < 3 || g.npl < 3 || (h->cfg.dim == 3 && g.nyp < 3))
       fail(h, NLS_ERR_ARG, "Neumann copy boundary needs >= 3 cells per dimension");
     if ((g.z0 == 0 || g.z0 + g.nzl == g.npl) && g.nzl < 2)
       fail(h, NLS_ERR_ARG, "Neumann copy boundary needs >= 2 planes on the boundary slabs");
+    if (h->kg) {  // KGESolverDevice::apply_bc: u only (nlsolvers/device/include/kg_dev.hpp)
+      void *u = vec_ptr(h, 0, 0);
+      Geo gg = g;
+      const int64_t cells = neumann_bc_cells(g);
+      const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((cells + NTHREADS - 1) / NTHREADS, 4096));
+      void *args[] = {&u, &gg};
+      launch(h, 3, -1, kernel_neumann_bc_r(), grid, args);
+      halo(h, 0, 0);
+      hip_check(h, hipGetLastError(), "kernel launch");
+      return;
+    }
     // the start vector of the next step (N(u) with the last step's dt, kept
     // from the final pass) is refreshed on the same boundary cells
     const bool refresh = h->w0_ready;
@@ -963,6 +985,7 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
     if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
     if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");
+    if (h->kg && !(dt > 0.0)) fail(h, NLS_ERR_ARG, "KG: dt must be > 0 (v = (u - u_past)/dt)");
     const int m = h->m;
     const int64_t n = h->geo.nloc;
     int64_t vs = h->vs;
@@ -974,6 +997,28 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
         hip_check(h, hipEventSynchronize(h->stepev[h->steps_issued % ra]), "hipEventSynchronize");
       if (h->cplx_) {
         ss2_step(h, dt);
+      } else if (h->kg) {
+        // KGESolver::step (nlsolvers/device/include/kg_single.cuh:49-86): sinc^2 basis
+        // of g = -m u^3, cos basis of u (the operator sign is immaterial: both
+        // functions depend on sqrt|lambda| only)
+        {
+          void *u = vec_ptr(h, 0, 0);
+          void *g0 = vec_ptr(h, 1, 0);
+          void *args[] = {&u, &h->mf, &g0, (void *)&n};
+          pw_launch(h, 3, kernel_kg_g(), args);
+          halo(h, 1, 0);
+        }
+        run_lanczos(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
+        run_lanczos(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0);
+        {
+          void *W = vec_ptr(h, 0, 0);
+          void *W2 = vec_ptr(h, 1, 0);
+          KState *st = h->B[0].st, *st2 = h->B[1].st;
+          void *args[] = {&W, &W2, &vs, (void *)&n, &st, &st2, &h->up, &h->vel, &dt};
+          pw_launch(h, 3, kernel_kg_end(m), args);
+          halo(h, 0, 0);
+        }
+        h->vel_valid = true;
       } else {
         // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u
         run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0);
@@ -1078,6 +1123,12 @@ int nls_get_sg_velocity(nls_handle *h, double dt, double *v, uint64_t n) {
     if (h->cplx_) fail(h, NLS_ERR_STATE, "velocity of an NLSE handle");
     if (!v) fail(h, NLS_ERR_ARG, "v is NULL");
     check_len(h, n);
+    if (h->kg && h->vel_valid) {  // stored by the last step (kg_single.cuh:80-85)
+      hip_check(h, hipMemcpyAsync(v, h->vel, (size_t)n * 8, hipMemcpyDeviceToHost, h->stream),
+                "hipMemcpy D2H");
+      hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+      return;
+    }
     void *u = vec_ptr(h, 0, 0);
     int64_t nn = (int64_t)n;
     void *args[] = {&u, &h->up, &h->scratch, &nn, &dt};

@@ -539,6 +539,90 @@ __global__ __launch_bounds__(NTHREADS) void k_sewi_end(const cplx *__restrict__ 
   }
 }
 
+// ---- G2 Klein-Gordon Gautschi (nlsolvers/device/include/kg_single.cuh:49-86) ----
+// start vector of the sinc^2 basis: g = -m u^3  (u = slot 0 of the cos basis)
+__global__ __launch_bounds__(NTHREADS) void k_kg_g(const double *__restrict__ u, const double *__restrict__ mf,
+                                                   double *__restrict__ g0, int64_t n) {
+  for (int64_t p = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * NTHREADS) {
+    const double x = u[p];
+    g0[p] = -mf[p] * x * x * x;
+  }
+}
+
+// u_new = (2 cos(t sqrt|L|) u - u_past) + (dt*dt) sinc^2(t sqrt|L|) g ;
+// u_past <- u ; v = (u_new - u_past) / dt.  u is slot 0 of W (read, then overwritten
+// by the same thread).
+template <int M>
+__global__ __launch_bounds__(NTHREADS) void k_kg_end(double *W, const double *__restrict__ W2, int64_t vs,
+                                                     int64_t n, const KState *__restrict__ st,
+                                                     const KState *__restrict__ st2,
+                                                     double *__restrict__ up, double *__restrict__ v,
+                                                     double dt) {
+  __shared__ double cc[MMAX], cs[MMAX];
+  for (int k = threadIdx.x; k < M; k += NTHREADS) {
+    cc[k] = st->fin[0][k].re;
+    cs[k] = st2->fin[0][k].re;
+  }
+  __syncthreads();
+  const double tt = dt * dt;
+  for (int64_t p = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * NTHREADS) {
+    double yc = 0.0, ys = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      yc += cc[k] * ld_nt(W + (int64_t)k * vs + p);
+      ys += cs[k] * ld_nt(W2 + (int64_t)k * vs + p);
+    }
+    const double uo = W[p];
+    const double un = (yc * 2.0 - up[p]) + ys * tt;
+    W[p] = un;
+    up[p] = uo;
+    v[p] = (un - uo) / dt;
+  }
+}
+
+// Neumann copy BC on a real field (u of a Klein-Gordon handle), same clamp gather
+__global__ __launch_bounds__(NTHREADS) void k_neumann_bc_r(double *__restrict__ u, Geo g) {
+  const int64_t per = bc_perimeter(g);
+  const int64_t nper = g.nzl * per;
+  const int64_t total = bc_cells(g);
+  const int64_t nx = g.nx, nyp = g.nyp;
+  for (int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * NTHREADS) {
+    int64_t q, x, y;
+    if (t < nper) {
+      q = t / per;
+      const int64_t k = t % per;
+      if (nyp == 1) {
+        x = k == 0 ? 0 : nx - 1;
+        y = 0;
+      } else if (k < nx) {
+        x = k; y = 0;
+      } else if (k < 2 * nx) {
+        x = k - nx; y = nyp - 1;
+      } else if (k < 2 * nx + nyp - 2) {
+        x = 0; y = 1 + (k - 2 * nx);
+      } else {
+        x = nx - 1; y = 1 + (k - 2 * nx - (nyp - 2));
+      }
+    } else {
+      const int64_t k = t - nper;
+      const int64_t which = k / g.P, c = k % g.P;
+      q = (which == 0 && g.z0 == 0) ? 0 : g.nzl - 1;
+      x = c % nx;
+      y = c / nx;
+    }
+    const int64_t gq = g.z0 + q;
+    const int64_t xs = x < 1 ? 1 : (x > nx - 2 ? nx - 2 : x);
+    const int64_t ys = nyp == 1 ? 0 : (y < 1 ? 1 : (y > nyp - 2 ? nyp - 2 : y));
+    const int64_t gs = gq < 1 ? 1 : (gq > g.npl - 2 ? g.npl - 2 : gq);
+    const int64_t src = (gs - g.z0) * g.P + ys * nx + xs;
+    const int64_t dst = q * g.P + y * nx + x;
+    if (src != dst) u[dst] = u[src];
+  }
+}
+
 // out = sum_k fin[fi][k] W_k  (one matrix-function action)
 template <class S, int M>
 __global__ __launch_bounds__(NTHREADS) void k_combine(const S *__restrict__ W, int64_t vs, int64_t n,
@@ -646,6 +730,17 @@ const void *kernel_nl_init() { return reinterpret_cast<const void *>(&k_nl_init)
 const void *kernel_sg_velocity() { return reinterpret_cast<const void *>(&k_sg_velocity); }
 const void *kernel_neumann_bc() { return reinterpret_cast<const void *>(&k_neumann_bc); }
 const void *kernel_sewi_b() { return reinterpret_cast<const void *>(&k_sewi_b); }
+const void *kernel_kg_g() { return reinterpret_cast<const void *>(&k_kg_g); }
+const void *kernel_neumann_bc_r() { return reinterpret_cast<const void *>(&k_neumann_bc_r); }
+
+const void *kernel_kg_end(int M) {
+  switch (M) {
+#define X(M) case M: return reinterpret_cast<const void *>(&k_kg_end<M>);
+    NLS_M_LIST(X)
+#undef X
+    default: return nullptr;
+  }
+}
 
 const void *kernel_combine_w0(int M) {
   switch (M) {

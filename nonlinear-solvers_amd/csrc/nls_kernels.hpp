@@ -63,6 +63,13 @@ const void *kernel_neumann_bc();
 //   sewi_end  : (const cplx* W, int64_t vs, int64_t n, const KState*, cplx* u, cplx* up,
 //                const cplx* e, double dt)
 const void *kernel_sewi_b();
+//   kg_g      : (const double* u, const double* mf, double* g0, int64_t n)
+//   kg_end    : (double* W, const double* W2, int64_t vs, int64_t n, const KState* st,
+//                const KState* st2, double* up, double* v, double dt)
+//   neumann_bc_r: (double* u, Geo g)
+const void *kernel_kg_g();
+const void *kernel_kg_end(int M);
+const void *kernel_neumann_bc_r();
 const void *kernel_combine_w0(int M);
 const void *kernel_sewi_end(int M);
 int64_t neumann_bc_cells(const Geo &g);

@@ -3,7 +3,7 @@
 // file four times (NLS_ANI = 0/1 x NLS_DIM = 2/3) so the ~250 instantiations
 // build in parallel; nls_kernels.hip dispatches between the four tables.
 //   NLS_ANI 0: G1 isotropic operator, f64 (sine-Gordon) and c128 (NLSE)
-//   NLS_ANI 1: G2 anisotropic div(c grad) operator, c128 only
+//   NLS_ANI 1: G2 anisotropic div(c grad) operator, c128 (NLSE) and f64 (Klein-Gordon)
 #include "nls_stencil.hpp"
 #include "nls_kernels.hpp"
 
@@ -33,11 +33,7 @@ template <class S> const void *pick(int kind, int J) {
 }  // namespace
 
 const void *NLS_TABLE(int kind, bool complex_, int J) {
-#if NLS_ANI
-  return complex_ ? pick<cplx>(kind, J) : nullptr;
-#else
   return complex_ ? pick<cplx>(kind, J) : pick<double>(kind, J);
-#endif
 }
 
 }  // namespace nls

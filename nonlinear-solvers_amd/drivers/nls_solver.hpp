@@ -287,6 +287,42 @@ class SGESolverDevice {
   uint32_t stored_ = 0;
 };
 
+// G2 Klein-Gordon Gautschi stepper (u_tt = div(c grad u) - m u^3), the
+// KGESolverDevice of nlsolvers/device/include/kg_dev.hpp as
+// kg_driver_dev_{2d,3d}.cpp drive it: ctor stores snapshot 0 = (u0, v0); per
+// step i: step(), apply_bc(), store_snapshot(i / freq) when i % freq == 0.
+class KGESolverDevice {
+ public:
+  using SnapshotFn = std::function<void(uint32_t index, const double *u, const double *v, uint64_t n)>;
+  KGESolverDevice(const Grid &g, const double *u0, const double *v0, const double *mfield,
+                  const double *cfield, double dt, uint32_t num_snapshots, uint32_t krylov_m,
+                  SnapshotFn cb, int device = -1)
+      : h_(g, NLS_KG_GAUTSCHI, krylov_m, device), ns_(num_snapshots), dt_(dt), cb_(std::move(cb)),
+        u_(h_.n()), v_(h_.n()) {
+    std::vector<double> up(h_.n());
+    for (uint64_t i = 0; i < h_.n(); ++i) up[i] = u0[i] - dt * v0[i];  // kg_dev.hpp ctor
+    check(nls_set_coefficients(h_.get(), mfield, cfield, h_.n()), h_.get());
+    check(nls_set_sg_state(h_.get(), u0, up.data(), nullptr, h_.n()), h_.get());
+    if (cb_ && ns_ > 0) cb_(0, u0, v0, h_.n());
+  }
+  void step() { check(nls_step(h_.get(), dt_, 1), h_.get()); }
+  void apply_bc() { check(nls_apply_bc(h_.get()), h_.get()); }
+  void store_snapshot(uint32_t idx) {
+    if (idx >= ns_) return;
+    check(nls_get_field(h_.get(), u_.data(), h_.n()), h_.get());
+    check(nls_get_sg_velocity(h_.get(), dt_, v_.data(), h_.n()), h_.get());
+    if (cb_) cb_(idx, u_.data(), v_.data(), h_.n());
+  }
+  uint64_t n() const { return h_.n(); }
+
+ private:
+  Handle h_;
+  uint32_t ns_;
+  double dt_;
+  SnapshotFn cb_;
+  std::vector<double> u_, v_;
+};
+
 namespace g2 {
 
 // G2 cubic NLSE stepper (nlsolvers/device/include/nlse_dev.hpp:66-361) as the

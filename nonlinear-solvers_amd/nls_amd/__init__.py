@@ -14,12 +14,12 @@ import os
 import numpy as np
 
 __all__ = [
-    "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "NLSE_G2", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
+    "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "NLSE_G2", "KG_GAUTSCHI", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
     "F_SINC2_SQRT", "F_ID_SQRT", "F_SINC2_HALF", "F_SINC", "MAX_KRYLOV", "NlsError", "Config", "Solver",
     "lib", "lib_path", "rccl_unique_id", "slab_planes", "EXPORTED_SYMBOLS",
 ]
 
-NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI, NLSE_G2 = 0, 1, 2, 3
+NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI, NLSE_G2, KG_GAUTSCHI = 0, 1, 2, 3, 4
 F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF, F_SINC = range(8)
 MAX_KRYLOV = 32
 
@@ -193,7 +193,7 @@ class Solver:
         self._group = group
         cfg.local_group = group._g if group is not None else None
         self.cfg = cfg
-        self.complex = equation != SG_GAUTSCHI
+        self.complex = equation not in (SG_GAUTSCHI, KG_GAUTSCHI)
         self.dtype = np.complex128 if self.complex else np.float64
         h = C.c_void_p()
         rc = L.nls_create(C.byref(cfg), C.byref(h))
@@ -242,9 +242,11 @@ class Solver:
         a = self._in(u)
         self._call(lib().nls_set_field, _dptr(a), self.n_local)
 
-    def set_sg_state(self, u, u_past, mfield):
-        a, b, c = self._in(u, np.float64), self._in(u_past, np.float64), self._in(mfield, np.float64)
-        self._call(lib().nls_set_sg_state, _dptr(a), _dptr(b), _dptr(c), self.n_local)
+    def set_sg_state(self, u, u_past, mfield=None):
+        a, b = self._in(u, np.float64), self._in(u_past, np.float64)
+        c = self._in(mfield, np.float64) if mfield is not None else None
+        self._call(lib().nls_set_sg_state, _dptr(a), _dptr(b), _dptr(c) if c is not None else None,
+                   self.n_local)
 
     def set_coefficients(self, mfield, cfield):
         """G2: focusing field m(x) and anisotropy c(x) of div(c grad u) (local slab)."""

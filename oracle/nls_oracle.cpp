@@ -126,8 +126,13 @@ void lap_aniso_apply(const Grid &G, const double *c, const S *x, S *y) {
 struct AnisoOp {
   Grid G;
   const double *c;
+  bool negate = false;  // -L as the KG drivers pass it (kg_driver_dev_3d.cpp:110-114)
   uint64_t n() const { return G.N; }
-  template <class S> void apply(const S *x, S *y) const { lap_aniso_apply(G, c, x, y); }
+  template <class S> void apply(const S *x, S *y) const {
+    lap_aniso_apply(G, c, x, y);
+    if (negate)  // negating the assembled values is exact: same bits as -(L x)
+      for (uint64_t p = 0; p < G.N; ++p) y[p] = -y[p];
+  }
 };
 
 struct CsrOp {
@@ -559,6 +564,44 @@ int oracle_nlse_sewi_steps(const oracle_grid *g, const double *c, const double *
     }
     if (bc) neumann_bc(G, u);
   }
+  return 0;
+}
+
+// G2 Klein-Gordon Gautschi step, KGESolver::step
+// (nlsolvers/device/include/kg_single.cuh:49-86) on the operator -div(c grad)
+// that kg_driver_dev_{2d,3d}.cpp assemble:
+//   c2 = 2 cos(t sqrt|L|) u ; g = -m u^3 ; s = sinc^2(t sqrt|L|) g  (t = dt)
+//   u_new = (c2 - u_past) + (dt*dt) s ; u_past = u ; v = (u_new - u_past)/dt
+// then (bc != 0) the driver's apply_bc() on u only (kg_driver_dev_3d.cpp:150-153).
+int oracle_kg_steps(const oracle_grid *g, const double *c, const double *mfield, double *u,
+                    double *u_past, double *v, double dt, uint32_t nsteps, uint32_t m, int bc) {
+  Grid G;
+  if (!make_grid(g, G) || !c || !mfield || !u || !u_past || !v || m < 1) return -1;
+  if (bc && (G.nx < 3 || G.ny < 3 || (G.dim == 3 && G.nz < 3))) return -1;
+  AnisoOp op{G, c, true};
+  const uint64_t n = G.N;
+  std::vector<double> c2(n), gb(n), s2(n), old(n);
+  const cd t(dt, 0.0);
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    std::memcpy(old.data(), u, n * sizeof(double));
+    krylov_apply(op, u, t, m, ORACLE_F_COS_SQRT, c2.data());
+    for (uint64_t p = 0; p < n; ++p) c2[p] = c2[p] * 2.0;
+    for (uint64_t p = 0; p < n; ++p) gb[p] = -mfield[p] * u[p] * u[p] * u[p];
+    krylov_apply(op, gb.data(), t, m, ORACLE_F_SINC2_SQRT, s2.data());
+    const double tt = dt * dt;
+    for (uint64_t p = 0; p < n; ++p) u[p] = (c2[p] - u_past[p]) + s2[p] * tt;
+    std::memcpy(u_past, old.data(), n * sizeof(double));
+    for (uint64_t p = 0; p < n; ++p) v[p] = (u[p] - u_past[p]) / dt;
+    if (bc) neumann_bc(G, u);
+  }
+  return 0;
+}
+
+int oracle_neumann_bc_r(const oracle_grid *g, double *u) {
+  Grid G;
+  if (!make_grid(g, G) || !u) return -1;
+  if (G.nx < 3 || G.ny < 3 || (G.dim == 3 && G.nz < 3)) return -1;
+  neumann_bc(G, u);
   return 0;
 }
 

@@ -13,6 +13,8 @@
  *   nlsolvers/device/include/nlse_dev.hpp:20-40,187-203     (m|u|^2, +tau/2, exp(tau L))
  *   nlsolvers/device/include/matfunc_complex.hpp:254-375     (exp(t*lambda), Q f Q^H)
  *   nlsolvers/device/include/boundaries.cuh:10-81            (Neumann copy BC)
+ *   nlsolvers/device/include/nlse_dev.hpp:205-238            (sEWI)
+ *   nlsolvers/device/include/kg_single.cuh:49-86             (Klein-Gordon Gautschi)
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
  * load this library.  The product path (libnls_amd.so) never links it.
@@ -99,6 +101,14 @@ int oracle_nlse_sewi_steps(const oracle_grid *g, const double *c,
                            const double *mfield, double *u, double *u_prev,
                            double dt, uint32_t first_step, uint32_t nsteps,
                            uint32_t m, int bc);
+
+/* G2 Klein-Gordon Gautschi (nlsolvers/device/include/kg_single.cuh:49-86,
+ * kg_driver_dev_{2d,3d}.cpp: operator -div(c grad), m(x), Neumann BC on u after
+ * every step when bc != 0); u, u_past, v updated in place. */
+int oracle_kg_steps(const oracle_grid *g, const double *c, const double *mfield,
+                    double *u, double *u_past, double *v, double dt,
+                    uint32_t nsteps, uint32_t m, int bc);
+int oracle_neumann_bc_r(const oracle_grid *g, double *u);
 
 /* sine-Gordon Gautschi (sg_solver.hpp:53-74); u, u_past updated in place. */
 int oracle_sg_steps(const oracle_grid *g, double *u, double *u_past,

@@ -169,6 +169,26 @@ def nlse_sewi_steps(dim, nx, ny, nz, dx, dy, c, mfield, u, u_prev, dt, first_ste
     return u, up
 
 
+def kg_steps(dim, nx, ny, nz, dx, dy, c, mfield, u, u_past, dt, nsteps, m, bc=True):
+    """G2 Klein-Gordon Gautschi (kg_single.cuh:49-86) on -div(c grad) + BC."""
+    A = -aniso_laplacian(dim, nx, ny, nz, dx, dy, c)
+    ap = lambda x: A @ x
+    mf = np.asarray(mfield, dtype=np.float64).ravel()
+    u = np.asarray(u, dtype=np.float64).ravel().copy()
+    up = np.asarray(u_past, dtype=np.float64).ravel().copy()
+    v = np.zeros_like(u)
+    for _ in range(nsteps):
+        c2 = 2.0 * krylov(ap, u, dt, m, F_COS_SQRT)
+        s = krylov(ap, -mf * u * u * u, dt, m, F_SINC2_SQRT)
+        new = (c2 - up) + s * (dt * dt)
+        up = u
+        u = new
+        v = (u - up) / dt
+        if bc:
+            u = neumann_bc(dim, nx, ny, nz, u)
+    return u, up, v
+
+
 def laplacian_apply(dim, nx, ny, nz, dx, dy, x):
     """Vectorised matrix-free application (same operator, flat-index form)."""
     x = np.asarray(x).ravel()

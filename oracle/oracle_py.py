@@ -47,6 +47,8 @@ def lib():
         L.oracle_neumann_bc_c.argtypes = [g, dp]
         L.oracle_nlse_g2_steps.argtypes = [g, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
                                            C.c_int]
+        L.oracle_kg_steps.argtypes = [g, dp, dp, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32, C.c_int]
+        L.oracle_neumann_bc_r.argtypes = [g, dp]
         L.oracle_nlse_sewi_steps.argtypes = [g, dp, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
                                              C.c_uint32, C.c_int]
     return _LIB
@@ -165,3 +167,18 @@ def nlse_sewi_steps(g, c, mfield, u, u_prev, dt, first_step, nsteps, m, bc=True)
     _check(lib().oracle_nlse_sewi_steps(C.byref(g), _r(c), _r(mfield), ui, pi, dt, first_step, nsteps, m,
                                         1 if bc else 0))
     return ui.view(np.complex128), pi.view(np.complex128)
+
+
+def kg_steps(g, c, mfield, u, u_past, dt, nsteps, m, bc=True):
+    """G2 Klein-Gordon Gautschi steps; returns (u, u_past, v)."""
+    u = _r(u).copy()
+    up = _r(u_past).copy()
+    v = np.zeros_like(u)
+    _check(lib().oracle_kg_steps(C.byref(g), _r(c), _r(mfield), u, up, v, dt, nsteps, m, 1 if bc else 0))
+    return u, up, v
+
+
+def neumann_bc_r(g, u):
+    ui = _r(u).copy()
+    _check(lib().oracle_neumann_bc_r(C.byref(g), ui))
+    return ui

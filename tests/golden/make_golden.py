@@ -121,6 +121,22 @@ def main():
     tw, twp = np_ref.nlse_sewi_steps(3, n, n, n, dx, dx, cf, mf, u0, None, dt, 1, steps, m, bc=True)
     assert np.linalg.norm(out - tw) / np.linalg.norm(tw) < 1e-12
     cases["sewi_3d"] = dict(dim=3, n=n, dx=dx, dt=dt, steps=steps, m=m, u0=u0, c=cf, mfield=mf, u=out, u_prev=outp)
+    # --- G2 Klein-Gordon Gautschi (kg_driver_dev_3d.cpp: m=10), BC after steps --
+    n, m, steps, L, kdt = 10, 10, 8, 3.0, 5e-3
+    dx = 2 * L / (n - 1)
+    rng = np.random.default_rng(31)
+    x = np.linspace(-L, L, n)
+    Z, Y, X = np.meshgrid(x, x, x, indexing="ij")
+    ku0 = (np.exp(-(X ** 2 + Y ** 2 + Z ** 2)) + 1e-3 * rng.standard_normal(X.shape)).ravel()
+    kv0 = (0.1 * np.sin(X) * np.exp(-(Y ** 2 + Z ** 2))).ravel()
+    cf = 1.0 + 0.3 * np.sin(0.5 * X + 0.2 * Z).ravel()
+    mf = 1.0 + 0.2 * np.cos(Y).ravel()
+    g = O.grid(3, n, n, n, dx, dx)
+    ku, kup, kv = O.kg_steps(g, cf, mf, ku0, ku0 - kdt * kv0, kdt, steps, m, bc=True)
+    tu, tup, tv = np_ref.kg_steps(3, n, n, n, dx, dx, cf, mf, ku0, ku0 - kdt * kv0, kdt, steps, m, bc=True)
+    assert np.linalg.norm(ku - tu) / np.linalg.norm(tu) < 1e-12
+    cases["kg_3d"] = dict(dim=3, n=n, dx=dx, dt=kdt, steps=steps, m=m, u0=ku0, v0=kv0, c=cf, mfield=mf,
+                          u=ku, u_past=kup, v=kv)
     for name, d in cases.items():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **{k: np.asarray(v) for k, v in d.items()})
     total = sum(os.path.getsize(os.path.join(HERE, f"{k}.npz")) for k in cases)

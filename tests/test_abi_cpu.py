@@ -48,7 +48,7 @@ def test_config_default_matches_reference_defaults():
 @pytest.mark.parametrize("kw,msg", [
     (dict(m=0), "krylov_m"), (dict(m=33), "krylov_m"), (dict(dim=4), "dim"),
     (dict(nx=1), "grid too small"), (dict(dx=0.0), "dx"), (dict(nranks=2), "rccl_id"),
-    (dict(equation=4), "unknown equation"), (dict(equation=3, nx=2), "G2 NLSE needs >= 3"),
+    (dict(equation=5), "unknown equation"), (dict(equation=3, nx=2), "need >= 3 cells"), (dict(equation=4, ny=2), "need >= 3 cells"),
     (dict(equation=3, dim=3, nz=3, nranks=2, group=True), "2 planes per rank"),
 ])
 def test_invalid_config_rejected_before_device(kw, msg):
@@ -128,7 +128,8 @@ def test_npy_codec_rejects_wrong_dtype(tmp_path):
 
 
 @pytest.mark.parametrize("prog,npos", [("nlse_3d_dev", 13), ("nlse_2d_dev", 11), ("nlse_sewi_3d_dev", 13),
-                                      ("nlse_sewi_2d_dev", 11)])
+                                      ("nlse_sewi_2d_dev", 11), ("kg_gautschi_3d_dev", 15),
+                                      ("kg_gautschi_2d_dev", 13)])
 def test_g2_driver_usage(prog, npos):
     for k in (0, npos - 2, npos - 1, npos + 1):   # nlse_cubic_driver_3d.cpp:20-31 (argc != 14)
         r = run([os.path.join(BIN, prog)] + ["8"] * k)

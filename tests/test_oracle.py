@@ -304,3 +304,43 @@ def test_golden_sewi():
     u, up = O.nlse_sewi_steps(g, d["c"], d["mfield"], d["u0"], None, float(d["dt"]), 1, int(d["steps"]),
                               int(d["m"]))
     assert rel_l2(u, d["u"]) < 1e-13 and rel_l2(up, d["u_prev"]) < 1e-13
+
+
+@pytest.mark.parametrize("dim,n", [(2, 14), (3, 7)])
+def test_kg_oracle_matches_numpy_twin(dim, n):
+    """G2 Klein-Gordon Gautschi (kg_single.cuh:49-86) on -div(c grad), two restatements;
+    the velocity is a difference quotient, so it carries an extra 1/dt."""
+    rng = np.random.default_rng(21 + dim)
+    N = n ** dim
+    c = rng.uniform(0.5, 2.0, N)
+    mf = rng.uniform(0.5, 1.5, N)
+    u = rng.standard_normal(N)
+    dt = 1e-2
+    up = u - dt * 0.1 * rng.standard_normal(N)
+    g = O.grid(dim, n, n, n, 0.6, 0.6)
+    a = O.kg_steps(g, c, mf, u, up, dt, 4, 10, bc=True)
+    b = np_ref.kg_steps(dim, n, n, n, 0.6, 0.6, c, mf, u, up, dt, 4, 10, bc=True)
+    assert rel_l2(a[0], b[0]) < 1e-12 and rel_l2(a[1], b[1]) < 1e-12 and rel_l2(a[2], b[2]) < 1e-10
+
+
+def test_kg_operator_sign_is_immaterial():
+    """The KG drivers pass -div(c grad); cos / sinc^2 of t sqrt|lambda| are even in the
+    operator sign (T -> -S T S), so +L gives the same action up to rounding."""
+    n = 9
+    g = O.grid(2, n, n, 1, 0.5, 0.5)
+    rng = np.random.default_rng(4)
+    c = rng.uniform(0.5, 2.0, n * n)
+    u = rng.standard_normal(n * n)
+    A = np_ref.aniso_laplacian(2, n, n, 1, 0.5, 0.5, c)
+    for f in (np_ref.F_COS_SQRT, np_ref.F_SINC2_SQRT):
+        assert rel_l2(np_ref.krylov(lambda x: A @ x, u, 0.05, 8, f),
+                      np_ref.krylov(lambda x: -(A @ x), u, 0.05, 8, f)) < 1e-13
+
+
+def test_golden_kg():
+    d = np.load(os.path.join(GOLD, "kg_3d.npz"))
+    n, dt = int(d["n"]), float(d["dt"])
+    g = O.grid(3, n, n, n, float(d["dx"]), float(d["dx"]))
+    u, up, v = O.kg_steps(g, d["c"], d["mfield"], d["u0"], d["u0"] - dt * d["v0"], dt, int(d["steps"]),
+                          int(d["m"]))
+    assert rel_l2(u, d["u"]) < 1e-13 and rel_l2(up, d["u_past"]) < 1e-13 and rel_l2(v, d["v"]) < 1e-11
