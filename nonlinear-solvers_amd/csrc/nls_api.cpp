@@ -102,6 +102,7 @@ struct nls_handle {
   void *scratch = nullptr;  // nloc elements
   cplx *partA = nullptr, *partU = nullptr;
   int grid_alpha = 1, grid_lap = 1, grid_pw = 1;
+  int kz_alpha = 4;
   UpdPlan plan[MMAX];
   bool field_set = false, w0_ready = false;
   double w0_dt = 0.0;  // dt the live start vector W_0 = N(u) was built with
@@ -438,10 +439,12 @@ void reduce_final(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
 void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
   const int m = h->m;
   Geo g = h->geo;
+  Geo ga = g;  // the alpha pass has its own tile depth
+  ga.kz = h->kz_alpha;
   const void *fa = kernel_alpha(h->cplx_, (int)h->cfg.dim, h->ani);
   {
     void *v0 = vec_ptr(h, b, 0);
-    void *args[] = {&v0, &g, &h->partA};
+    void *args[] = {&v0, &ga, &h->partA};
     launch(h, 0, 0, fa, h->grid_alpha, args);
   }
   reduce_iter(h, b, 0);
@@ -453,7 +456,7 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
     if (j >= 1) {
       halo_wait(h);
       void *vj = vec_ptr(h, b, j);
-      void *args[] = {&vj, &g, &h->partA};
+      void *args[] = {&vj, &ga, &h->partA};
       launch(h, 0, j, fa, h->grid_alpha, args);
       reduce_iter(h, b, j);
     }
@@ -522,6 +525,11 @@ void setup_geometry(nls_handle *h) {
   // tile depth: 3D planes per tile, 2D rows per wave (tile = 4 waves)
   g.kz = c.dim == 3 ? 32 : 16;
   if (const char *e = std::getenv("NLS_KZ")) g.kz = std::max(1, std::atoi(e));
+  // alpha pass on large 3D slabs (one-tile-per-workgroup grids, see
+  // occupancy_grid): shallower tiles, -9 % alpha time at 512^3 with kz 4 vs
+  // 16-32; on small slabs (persistent grids) it is slower (tools/exp_kz.sh)
+  h->kz_alpha = (c.dim == 3 && g.nloc > (int64_t(1) << 25)) ? 4 : g.kz;
+  if (const char *e = std::getenv("NLS_KZ_ALPHA")) h->kz_alpha = std::max(1, std::atoi(e));
   g.remap = 0;
   if (const char *e = std::getenv("NLS_TILE_REMAP")) g.remap = std::atoi(e) != 0;
   // Pad the vector stride so the m streams of one update pass do not start on
@@ -569,9 +577,10 @@ void alloc_all(nls_handle *h) {
   const bool c = h->cplx_;
   const int dim = h->cfg.dim;
   const bool ani = h->ani;
-  const int64_t ta = stencil_tiles(g, dim, alpha_rows_per_thread());
-  h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim, ani), ta);
-  h->grid_lap = occupancy_grid(h, kernel_lap(c, dim, ani), ta);
+  Geo ga = g;
+  ga.kz = h->kz_alpha;
+  h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim, ani), stencil_tiles(ga, dim, alpha_rows_per_thread()));
+  h->grid_lap = occupancy_grid(h, kernel_lap(c, dim, ani), stencil_tiles(g, dim, alpha_rows_per_thread()));
   int64_t cap = 2 * (int64_t)h->grid_alpha;
   for (int j = 0; j + 1 < h->m; ++j) {
     const void *fu = kernel_update(c, dim, j, ani);
