@@ -146,11 +146,32 @@ def max_over_ranks(x, dist=None):
 
 
 def cpu_baseline(args):
-    """Oracle (single-threaded restatement of nlse_driver.cpp -> NLSESolver::step ->
-    expm_multiply) on a bounded sample of the workload."""
+    """The oracle (C++ restatement of nlse_driver.cpp -> NLSESolver::step ->
+    expm_multiply) on a bounded sample of the workload, timed twice on the host:
+    all cores (OpenMP build, SURVEY 8(d) "all cores" mode; reported as `value`)
+    and single-threaded (the reference's own Eigen path is single-threaded)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
 
+    one = _cpu_sample(args, oracle_py)
+    out = dict(one)
+    try:
+        oracle_py.use_openmp(True)
+        nthr = oracle_py.threads()
+        if nthr > 1:
+            allc = _cpu_sample(args, oracle_py)
+            out = dict(allc)
+            out["cores"] = nthr
+            out["sample"] = allc["sample"].replace("1 thread", f"OpenMP {nthr} threads")
+            out["single_thread"] = {"value": one["value"], "seconds": one["seconds"]}
+    except (OSError, FileNotFoundError):
+        pass
+    finally:
+        oracle_py.use_openmp(False)
+    return out
+
+
+def _cpu_sample(args, oracle_py):
     w = dict(WORKLOADS[args.workload])
     if w.get("sewi"):
         ns, steps = 48, 3
@@ -202,7 +223,7 @@ def cpu_baseline(args):
         oracle_py.sg_steps(g, u, up, mf, w["dt"], steps, w["m"])
         el = time.perf_counter() - t0
         cells = ns * ns
-        sample = f"2D sine-Gordon {ns}^2 m={w['m']}, {steps} Gautschi steps (sub-grid of the workload)"
+        sample = f"2D sine-Gordon {ns}^2 m={w['m']}, {steps} Gautschi steps (sub-grid of the workload, 1 thread)"
     else:
         ns = 128 if w["dim"] == 3 else 1024
         steps = args.cpu_steps

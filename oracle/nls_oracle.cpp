@@ -14,6 +14,16 @@
 #include <cstring>
 #include <vector>
 
+#ifdef _OPENMP
+#include <omp.h>
+// Built a second time with -fopenmp (liboracle_nls_omp.so) for the all-cores
+// CPU baseline only: the vector loops run in parallel and the reductions sum
+// per-thread partials in thread order.  The checker is the serial build.
+#define ORACLE_PFOR _Pragma("omp parallel for schedule(static)")
+#else
+#define ORACLE_PFOR
+#endif
+
 namespace {
 
 using cd = std::complex<double>;
@@ -55,6 +65,7 @@ void lap_apply(const Grid &G, const S *x, S *y) {
   const double d_in = G.dim == 2 ? -4.0 : -6.0;
   const double d_bd = G.dim == 2 ? -3.0 : -5.0;
   const double sd_in = d_in * s, sd_bd = d_bd * s;
+  ORACLE_PFOR
   for (uint64_t idx = 0; idx < N; ++idx) {
     const uint64_t i = idx % nx, j = (idx / nx) % ny, k = idx / P;
     bool bnd = (i == 0 || i == nx - 1 || j == 0 || j == ny - 1);
@@ -93,6 +104,7 @@ template <class S>
 void lap_aniso_apply(const Grid &G, const double *c, const S *x, S *y) {
   const uint64_t nx = G.nx, N = G.N, P = G.nx * G.ny;
   const double s = G.scale;
+  ORACLE_PFOR
   for (uint64_t idx = 0; idx < N; ++idx) {
     const uint64_t i = idx % nx;
     const bool ezm = G.dim == 3 && idx >= P, ezp = G.dim == 3 && idx + P < N;
@@ -156,18 +168,37 @@ inline double abs2_s(cd x) { return x.real() * x.real() + x.imag() * x.imag(); }
 inline double re_s(double x) { return x; }
 inline double re_s(cd x) { return x.real(); }
 
+// serial sum, or (OpenMP build) per-thread partial sums added in thread order
+template <class T, class F> T reduce_sum(uint64_t n, F term) {
+#ifdef _OPENMP
+  const int nt = omp_get_max_threads();
+  if (nt > 1 && n > 4096) {
+    std::vector<T> part(nt, T(0));
+#pragma omp parallel
+    {
+      T acc = T(0);
+#pragma omp for schedule(static)
+      for (uint64_t p = 0; p < n; ++p) acc += term(p);
+      part[omp_get_thread_num()] = acc;
+    }
+    T acc = T(0);
+    for (int t = 0; t < nt; ++t) acc += part[t];
+    return acc;
+  }
+#endif
+  T acc = T(0);
+  for (uint64_t p = 0; p < n; ++p) acc += term(p);
+  return acc;
+}
+
 template <class S> double norm2(const S *x, uint64_t n) {
-  double acc = 0.0;
-  for (uint64_t p = 0; p < n; ++p) acc += abs2_s(x[p]);
-  return std::sqrt(acc);
+  return std::sqrt(reduce_sum<double>(n, [&](uint64_t p) { return abs2_s(x[p]); }));
 }
 
 // <a, b> = a^H b  (Eigen: V.col(i).adjoint() * w, eigen_krylov_complex.hpp:30;
 // for the real path w.dot(V.col(i)) is the same number, eigen_krylov_real.hpp:29)
 template <class S> S dot(const S *a, const S *b, uint64_t n) {
-  S acc = S(0);
-  for (uint64_t p = 0; p < n; ++p) acc += conj_s(a[p]) * b[p];
-  return acc;
+  return reduce_sum<S>(n, [&](uint64_t p) { return conj_s(a[p]) * b[p]; });
 }
 
 // lanczos_L  (eigen_krylov_complex.hpp:10-53, eigen_krylov_real.hpp:5-51)
@@ -182,6 +213,7 @@ void lanczos(const Op &op, const S *u, uint32_t m, std::vector<S> &V,
   T.assign((size_t)m * m, S(0));
   auto Tm = [&](uint32_t r, uint32_t c) -> S & { return T[(size_t)c * m + r]; };
   beta = norm2(u, n);
+  ORACLE_PFOR
   for (uint64_t p = 0; p < n; ++p) V[p] = u[p] / beta;
   std::vector<S> w(n);
   for (uint32_t j = 0; j + 1 < m; ++j) {
@@ -190,23 +222,27 @@ void lanczos(const Op &op, const S *u, uint32_t m, std::vector<S> &V,
     if (j > 0) {
       const S b = Tm(j - 1, j);
       const S *vjm = &V[(uint64_t)(j - 1) * n];
+      ORACLE_PFOR
       for (uint64_t p = 0; p < n; ++p) w[p] -= b * vjm[p];
     }
     Tm(j, j) = dot(vj, w.data(), n);
     {
       const S a = Tm(j, j);
+      ORACLE_PFOR
       for (uint64_t p = 0; p < n; ++p) w[p] -= a * vj[p];
     }
     // full MGS re-orthogonalisation (eigen_krylov_complex.hpp:29-37)
     for (uint32_t i = 0; i <= j; ++i) {
       const S *vi = &V[(uint64_t)i * n];
       const S c = dot(vi, w.data(), n);
+      ORACLE_PFOR
       for (uint64_t p = 0; p < n; ++p) w[p] -= c * vi[p];
     }
     const double nb = norm2(w.data(), n);
     Tm(j + 1, j) = S(nb);
     Tm(j, j + 1) = S(nb);
     S *vn = &V[(uint64_t)(j + 1) * n];
+    ORACLE_PFOR
     for (uint64_t p = 0; p < n; ++p) vn[p] = w[p] / nb;
   }
 }
@@ -318,6 +354,7 @@ void krylov_apply(const Op &op, const S *u, cd t, uint32_t m, int func, S *out) 
   }
   std::vector<S> c(m);
   for (uint32_t i = 0; i < m; ++i) assign(c[i], coef[i]);
+  ORACLE_PFOR
   for (uint64_t p = 0; p < n; ++p) {
     S acc = S(0);
     for (uint32_t k = 0; k < m; ++k) acc += (beta * V[(uint64_t)k * n + p]) * c[k];
@@ -336,6 +373,7 @@ void nonlin_half(cd *u, uint64_t n, double dt, int nonlin, const double *sg) {
   const cd tau(0.0, dt);
   const cd mt = -.5 * tau;
   if (nonlin == 0) {
+    ORACLE_PFOR
     for (uint64_t p = 0; p < n; ++p) {
       const double x = u[p].real() * u[p].real() + u[p].imag() * u[p].imag();
       u[p] = std::exp(mt * cd(x)) * u[p];
@@ -393,6 +431,14 @@ template <class S> void neumann_bc(const Grid &G, S *u) {
 }  // namespace
 
 extern "C" {
+
+int oracle_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
 
 int oracle_laplacian_apply_c(const oracle_grid *g, const double *x, double *y) {
   Grid G;

@@ -49,6 +49,10 @@ enum {
   ORACLE_F_SINC = 7       /* sinc(t*lambda) (G2 "sinc") nlsolvers/device/include/matfunc_complex.hpp:290-300 */
 };
 
+/* threads the loops use: 1 for the serial checker build, OpenMP's count for
+ * liboracle_nls_omp.so (all-cores CPU baseline) */
+int oracle_threads(void);
+
 int oracle_laplacian_apply_c(const oracle_grid *g, const double *x, double *y);
 int oracle_laplacian_apply_r(const oracle_grid *g, const double *x, double *y);
 

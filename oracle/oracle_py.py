@@ -18,16 +18,27 @@ class OracleGrid(C.Structure):
                 ("dx", C.c_double), ("dy", C.c_double)]
 
 
+def use_openmp(on: bool = True):
+    """Switch to the OpenMP build (all-cores CPU baseline timing only)."""
+    global _LIB, _NAME
+    _NAME = "liboracle_nls_omp.so" if on else "liboracle_nls.so"
+    _LIB = None
+
+
+_NAME = "liboracle_nls.so"
+
+
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liboracle_nls.so")
+        path = os.path.join(_HERE, _NAME)
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
         _LIB = C.CDLL(path)
         dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
         g = C.POINTER(OracleGrid)
         L = _LIB
+        L.oracle_threads.restype = C.c_int
         L.oracle_laplacian_apply_c.argtypes = [g, dp, dp]
         L.oracle_laplacian_apply_r.argtypes = [g, dp, dp]
         L.oracle_lanczos_c.argtypes = [g, dp, C.c_uint32, dp, dp, C.POINTER(C.c_double)]
@@ -52,6 +63,10 @@ def lib():
         L.oracle_nlse_sewi_steps.argtypes = [g, dp, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
                                              C.c_uint32, C.c_int]
     return _LIB
+
+
+def threads():
+    return int(lib().oracle_threads())
 
 
 def grid(dim, nx, ny, nz, dx, dy):
