@@ -218,6 +218,11 @@ __device__ cplx eval_f(int func, double lam, double t_re, double t_im) {
 
 __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf, int f0, int f1,
                                          double t_re, double t_im);
+#ifndef NLS_EIGEN_JACOBI
+#define NLS_EIGEN_JACOBI 1
+#endif
+__device__ __noinline__ void eigen_phase_jacobi(KState *__restrict__ st, int m, int nf, int f0,
+                                                int f1, double t_re, double t_im);
 
 // After the last k_update<m-2>: sums[0..m-1] = g_0..g_{m-2}, nn.  Completes
 // T (T(m-1,m-1) = 0, eigen_krylov_complex.hpp:21), diagonalises it with
@@ -250,7 +255,144 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_final(KState *__restrict__ 
   }
   if (threadIdx.x == 0) st->Td[m - 1] = 0.0;
   __syncthreads();
+#if NLS_EIGEN_JACOBI
+  eigen_phase_jacobi(st, m, nf, f0, f1, t_re, t_im);
+#else
   if (threadIdx.x < 64) eigen_phase(st, m, nf, f0, f1, t_re, t_im);
+#endif
+}
+
+// Parallel cyclic Jacobi on the whole workgroup (the algorithm of the oracle,
+// oracle/nls_oracle.cpp jacobi_eig, with a round-robin ordering so that the
+// m/2 rotations of a round are disjoint and applied at once).  Per round: one
+// thread per pair computes (c, s); then all threads rotate the column pairs of
+// A and Q, then the row pairs of A.  Sweeps until off(A)^2 <= 1e-34 |A|^2.
+__device__ __noinline__ void eigen_phase_jacobi(KState *__restrict__ st, int m, int nf, int f0,
+                                                int f1, double t_re, double t_im) {
+  __shared__ double A[MMAX][MMAX + 1];
+  __shared__ double Q[MMAX][MMAX + 1];
+  __shared__ double rc[MMAX / 2], rs[MMAX / 2];
+  __shared__ int rp[MMAX / 2], rq[MMAX / 2];
+  __shared__ double red[2][NTHREADS / 64];
+  __shared__ double s_scl;
+  const int t = threadIdx.x;
+  const int mp = (m + 1) & ~1;  // even number of round-robin slots (slot m is a dummy if m is odd)
+  const int npair = mp / 2;
+  // T scaled to max |entry| = 1 (as the QL path and Eigen's solver)
+  if (t < 64) {
+    double v = 0.0;
+    if (t < m) v = fabs(st->Td[t]);
+    if (t < m - 1) v = fmax(v, fabs(st->To[t]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    if (t == 0) s_scl = v > 0.0 ? v : 1.0;
+  }
+  __syncthreads();
+  const double iscl = 1.0 / s_scl;
+  for (int e = t; e < m * m; e += NTHREADS) {
+    const int i = e / m, j = e % m;
+    double a = 0.0;
+    if (i == j) a = st->Td[i] * iscl;
+    else if (i == j + 1) a = st->To[j] * iscl;
+    else if (j == i + 1) a = st->To[i] * iscl;
+    A[i][j] = a;
+    Q[i][j] = i == j ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  for (int sweep = 0; sweep < 100; ++sweep) {
+    // convergence test on the whole matrix (oracle: off <= 1e-34 tot || off == 0)
+    double off = 0.0, tot = 0.0;
+    for (int e = t; e < m * m; e += NTHREADS) {
+      const int i = e / m, j = e % m;
+      const double a2 = A[i][j] * A[i][j];
+      tot += a2;
+      if (i != j) off += a2;
+    }
+    off = wave_sum(off);
+    tot = wave_sum(tot);
+    if ((t & 63) == 0) {
+      red[0][t >> 6] = off;
+      red[1][t >> 6] = tot;
+    }
+    __syncthreads();
+    double so = 0.0, sa = 0.0;
+#pragma unroll
+    for (int w = 0; w < NTHREADS / 64; ++w) {
+      so += red[0][w];
+      sa += red[1][w];
+    }
+    __syncthreads();
+    if (so <= 1e-34 * sa || so == 0.0) break;  // uniform across the workgroup
+    for (int r = 0; r < mp - 1; ++r) {
+      if (t < npair) {  // circle method: slot 0 fixed, the others rotate
+        const int a = t == 0 ? 0 : 1 + (t - 1 + r) % (mp - 1);
+        const int b = 1 + (mp - 2 - t + r) % (mp - 1);
+        const int p = a < b ? a : b, q = a < b ? b : a;
+        double c = 1.0, sn = 0.0;
+        if (q < m) {
+          const double apq = A[p][q];
+          if (apq != 0.0) {
+            const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+            const double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+            c = 1.0 / sqrt(tt * tt + 1.0);
+            sn = tt * c;
+          }
+        }
+        rp[t] = p;
+        rq[t] = q < m ? q : p;  // dummy pair: identity rotation on p
+        rc[t] = c;
+        rs[t] = q < m ? sn : 0.0;
+      }
+      __syncthreads();
+      // A <- J^T A J and Q <- Q J in one phase: the pairs are disjoint, so each
+      // 2x2 block A[{pa,qa}][{pb,qb}] (and each Q row segment) has one owner.
+      // The annihilated entry of a diagonal block is set to exactly zero (else
+      // rounding keeps off(A) above the stopping threshold for ever).
+      for (int e = t; e < npair * npair + m * npair; e += NTHREADS) {
+        if (e < npair * npair) {
+          const int a = e / npair, b = e % npair;
+          const int pa = rp[a], qa = rq[a], pb = rp[b], qb = rq[b];
+          const double ca = rc[a], sa = rs[a], cb = rc[b], sb = rs[b];
+          const bool va = pa != qa, vb = pb != qb;
+          const double b00 = A[pa][pb], b01 = vb ? A[pa][qb] : 0.0;
+          const double b10 = va ? A[qa][pb] : 0.0, b11 = (va && vb) ? A[qa][qb] : 0.0;
+          // rows: [[ca, -sa], [sa, ca]] * B
+          const double r00 = ca * b00 - sa * b10, r01 = ca * b01 - sa * b11;
+          const double r10 = sa * b00 + ca * b10, r11 = sa * b01 + ca * b11;
+          // columns: * [[cb, sb], [-sb, cb]]
+          double n00 = r00 * cb - r01 * sb, n01 = r00 * sb + r01 * cb;
+          double n10 = r10 * cb - r11 * sb, n11 = r10 * sb + r11 * cb;
+          if (a == b && va) n01 = n10 = 0.0;
+          A[pa][pb] = n00;
+          if (vb) A[pa][qb] = n01;
+          if (va) A[qa][pb] = n10;
+          if (va && vb) A[qa][qb] = n11;
+        } else {
+          const int e2 = e - npair * npair;
+          const int k = e2 / npair, b = e2 % npair;
+          const int p = rp[b], q = rq[b];
+          if (p == q) continue;
+          const double c = rc[b], sn = rs[b];
+          const double qkp = Q[k][p], qkq = Q[k][q];
+          Q[k][p] = c * qkp - sn * qkq;
+          Q[k][q] = sn * qkp + c * qkq;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // fin[f][r] = s0 / s_r * sum_k Q[r][k] Q[0][k] f(lambda_k)
+  if (t < m) {
+    st->lam[t] = A[t][t] * s_scl;
+    const double s0 = st->s[0];
+    const double isr = inv_or_zero(st->s[t]);
+    for (int fi = 0; fi < nf; ++fi) {
+      const int func = fi == 0 ? f0 : f1;
+      cplx c = {0.0, 0.0};
+      for (int k = 0; k < m; ++k) c += (Q[t][k] * Q[0][k]) * eval_f(func, A[k][k] * s_scl, t_re, t_im);
+      st->fin[fi][t] = (s0 * isr) * c;
+    }
+  }
 }
 
 // Wave-0 part of k_reduce_final.  Lane k holds d[k] and e[k] in registers; the
