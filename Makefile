@@ -13,7 +13,8 @@ LDFLAGS  := -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 LIB      := $(LIBDIR)/libnls_amd.so
 STENCIL  := iso2 iso3 ani2 ani3
 OBJS     := $(BUILD)/nls_kernels.o $(BUILD)/nls_api.o $(STENCIL:%=$(BUILD)/nls_stencil_%.o)
-DEVHDR   := $(CSRC)/nls_device.hpp $(CSRC)/nls_kernels.hpp $(CSRC)/nls_stencil.hpp
+DEVHDR   := $(CSRC)/nls_device.hpp $(CSRC)/nls_kernels.hpp $(CSRC)/nls_stencil.hpp \
+            $(CSRC)/nls_common.hpp $(CSRC)/nls_reduce.hpp
 
 all: $(LIB) drivers oracle
 

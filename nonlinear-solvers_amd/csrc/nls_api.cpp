@@ -379,6 +379,14 @@ void colsum(nls_handle *h, int b, int j, const cplx *pA, int nbA, int ncA, int n
   launch(h, 2, j, kernel_colsum(), ncA + ncU, args);
 }
 
+// Launch k_alpha<j> on vector j of basis b
+void alpha_pass(nls_handle *h, int b, int j, const Geo &ga) {
+  void *vj = vec_ptr(h, b, j);
+  Geo gg = ga;
+  void *args[] = {&vj, &gg, &h->partA};
+  launch(h, 0, j, kernel_alpha(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_alpha, args);
+}
+
 void reduce_iter(nls_handle *h, int b, int j) {
   KState *st = h->B[b].st;
   int nbA = h->grid_alpha, nbU = j >= 1 ? h->plan[j - 1].total : 0;
@@ -441,12 +449,7 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   Geo g = h->geo;
   Geo ga = g;  // the alpha pass has its own tile depth
   ga.kz = h->kz_alpha;
-  const void *fa = kernel_alpha(h->cplx_, (int)h->cfg.dim, h->ani);
-  {
-    void *v0 = vec_ptr(h, b, 0);
-    void *args[] = {&v0, &ga, &h->partA};
-    launch(h, 0, 0, fa, h->grid_alpha, args);
-  }
+  alpha_pass(h, b, 0, ga);
   reduce_iter(h, b, 0);
   void *W = vec_ptr(h, b, 0);
   int64_t vs = h->vs;
@@ -455,9 +458,7 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
     void *out = vec_ptr(h, b, j + 1);
     if (j >= 1) {
       halo_wait(h);
-      void *vj = vec_ptr(h, b, j);
-      void *args[] = {&vj, &ga, &h->partA};
-      launch(h, 0, j, fa, h->grid_alpha, args);
+      alpha_pass(h, b, j, ga);
       reduce_iter(h, b, j);
     }
     const void *fu = kernel_update(h->cplx_, (int)h->cfg.dim, j, h->ani);
