@@ -594,7 +594,7 @@ void alloc_all(nls_handle *h) {
       const int i = pl.n++;
       pl.qa[i] = qa;
       pl.qb[i] = qb;
-      pl.grid[i] = occupancy_grid(h, fu, stencil_tiles(gi, dim, update_rows_per_thread(j)));
+      pl.grid[i] = occupancy_grid(h, fu, stencil_tiles(gi, dim, update_rows_per_thread(j, ani)));
       pl.off[i] = pl.total;
       pl.total += pl.grid[i];
       if (bnd) pl.nbnd = pl.n;

@@ -46,7 +46,7 @@ int64_t stencil_tiles(const Geo &g, int dim, int rb) {
   }
   return a * b * c;
 }
-int update_rows_per_thread(int J) { return upd_rb(J); }
+int update_rows_per_thread(int J, bool ani) { return upd_rb(J, ani); }
 int alpha_rows_per_thread() { return RB_ALPHA; }
 
 // ---------------------------------------------------------------------------

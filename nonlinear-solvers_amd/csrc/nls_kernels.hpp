@@ -15,7 +15,7 @@ const void *kernel_update(bool complex_, int dim, int J, bool ani);
 const void *kernel_alpha(bool complex_, int dim, bool ani);
 const void *kernel_lap(bool complex_, int dim, bool ani);
 int64_t stencil_tiles(const Geo &g, int dim, int rows_per_thread);
-int update_rows_per_thread(int J);
+int update_rows_per_thread(int J, bool ani);
 int alpha_rows_per_thread();
 
 // per-variant tables (nls_stencil.hip, one object per operator x dimension)

@@ -271,13 +271,17 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
 #ifndef NLS_COEF_LDS
 #define NLS_COEF_LDS 1
 #endif
-__host__ __device__ constexpr int upd_rb(int J) {
-  return NLS_UPD_RB_MODE == 0 ? (J <= 2 ? 4 : (J <= 6 ? 2 : 1))
+#ifndef NLS_ANI_RB1_FROM
+#define NLS_ANI_RB1_FROM 13  // anisotropic passes with J >= this: one row per thread (G2 256^3 m=25: -5 % update time)
+#endif
+__host__ __device__ constexpr int upd_rb(int J, bool ani = false) {
+  return (ani && J >= NLS_ANI_RB1_FROM) ? 1
+       : NLS_UPD_RB_MODE == 0 ? (J <= 2 ? 4 : (J <= 6 ? 2 : 1))
        : NLS_UPD_RB_MODE == 1 ? (J <= 2 ? 4 : 2)
        : NLS_UPD_RB_MODE == 2 ? (J <= 6 ? 4 : 2)
                               : (J <= 2 ? 4 : (J <= 6 ? 2 : (J <= 18 ? 2 : 1)));
 }
-template <int J> struct UpdRB { static constexpr int v = upd_rb(J); };
+template <int J, bool ANI> struct UpdRB { static constexpr int v = upd_rb(J, ANI); };
 constexpr int RB_ALPHA = 4;
 
 // y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
@@ -484,7 +488,7 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
 #define NLS_RELOAD() ((void)0)
 #endif
   const S *__restrict__ VJ = W + (int64_t)J * vs;
-  constexpr int RB = UpdRB<J>::v;
+  constexpr int RB = UpdRB<J, ANI>::v;
   march<S, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
     // every streamed load of every row first ...
     S wk[RB][J > 0 ? J : 1];
