@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define NLS_ABI_VERSION 1
+#define NLS_ABI_VERSION 2
 #define NLS_MAX_KRYLOV 32
 
 enum nls_status {
@@ -215,6 +215,7 @@ typedef struct nls_timing {
   double update_ms[NLS_MAX_KRYLOV];
   uint64_t update_count[NLS_MAX_KRYLOV];
   uint64_t steps;
+  uint64_t graph_steps; /* steps replayed from a captured hipGraph (NLS_GRAPH) */
 } nls_timing;
 int nls_set_timing(nls_handle *h, int32_t enable);
 int nls_get_timing(nls_handle *h, nls_timing *out); /* synchronises */

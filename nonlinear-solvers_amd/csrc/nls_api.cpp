@@ -135,6 +135,11 @@ struct nls_handle {
   hipEvent_t stepev[RA_MAX] = {};
   int runahead = 0;  // NLS_RUNAHEAD=k: off by default (no measured effect, tools/exp_runahead.sh)
   uint64_t steps_issued = 0;
+  // hipGraph replay of steady-state steps (single-rank handles): one graph
+  // launch per step instead of ~3m kernel launches; keyed by dt
+  bool use_graph = false;
+  hipGraphExec_t gexec = nullptr;
+  double gdt = 0.0;
 };
 
 namespace {
@@ -718,6 +723,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   h->nranks = c.nranks;
   if (const char *e = std::getenv("NLS_RUNAHEAD"))
     h->runahead = std::min(nls_handle::RA_MAX, std::max(0, std::atoi(e)));
+  if (const char *e = std::getenv("NLS_GRAPH")) h->use_graph = std::atoi(e) != 0;
   if (c.device >= 0) {
     h->dev = c.device;
   } else if (hipGetDevice(&h->dev) != hipSuccess) {
@@ -782,6 +788,7 @@ int nls_destroy(nls_handle *h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->cstream) (void)hipStreamSynchronize(h->cstream);
   if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_snap, h->ev_snap_done})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->stepev)
@@ -990,65 +997,115 @@ int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number) {
   });
 }
 
+// Device work of one nls_step step (every equation but sEWI).
+void issue_step(nls_handle *h, double dt) {
+  const int m = h->m;
+  const int64_t n = h->geo.nloc;
+  int64_t vs = h->vs;
+  if (h->cplx_) {
+    ss2_step(h, dt);
+  } else if (h->kg) {
+    // KGESolver::step (nlsolvers/device/include/kg_single.cuh:49-86): sinc^2 basis
+    // of g = -m u^3, cos basis of u (the operator sign is immaterial: both
+    // functions depend on sqrt|lambda| only)
+    {
+      void *u = vec_ptr(h, 0, 0);
+      void *g0 = vec_ptr(h, 1, 0);
+      void *args[] = {&u, &h->mf, &g0, (void *)&n};
+      pw_launch(h, 3, kernel_kg_g(), args);
+      halo(h, 1, 0);
+    }
+    run_lanczos(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
+    run_lanczos(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0);
+    {
+      void *W = vec_ptr(h, 0, 0);
+      void *W2 = vec_ptr(h, 1, 0);
+      KState *st = h->B[0].st, *st2 = h->B[1].st;
+      void *args[] = {&W, &W2, &vs, (void *)&n, &st, &st2, &h->up, &h->vel, &dt};
+      pw_launch(h, 3, kernel_kg_end(m), args);
+      halo(h, 0, 0);
+    }
+    h->vel_valid = true;
+  } else {
+    // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u
+    run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0);
+    {
+      void *W = vec_ptr(h, 0, 0);
+      void *g0 = vec_ptr(h, 1, 0);
+      KState *st = h->B[0].st;
+      void *args[] = {&W, &vs, (void *)&n, &st, &h->mf, &h->up, &g0};
+      pw_launch(h, 3, kernel_sg_mid(m), args);
+      halo(h, 1, 0);
+    }
+    run_lanczos(h, 1, 1, NLS_F_SINC2_HALF, 0, dt, 0.0);
+    {
+      void *W2 = vec_ptr(h, 1, 0);
+      void *u = vec_ptr(h, 0, 0);
+      KState *st = h->B[1].st;
+      void *args[] = {&W2, &vs, (void *)&n, &st, &u, &h->up, &dt};
+      pw_launch(h, 3, kernel_sg_end(m), args);
+      halo(h, 0, 0);
+    }
+  }
+}
+
+// Host-side state a step leaves behind (what issue_step sets besides the launches).
+void finish_step_flags(nls_handle *h, double dt) {
+  if (h->cplx_) {
+    h->w0_ready = true;
+    h->w0_dt = dt;
+  } else if (h->kg) {
+    h->vel_valid = true;
+  }
+}
+
+// A step whose launch sequence is fixed can replay a captured graph: single
+// rank (no RCCL / local-transport exchanges in the step), no per-kernel timing
+// events, and for the NLSE a live start vector W_0 built with this dt (otherwise
+// the step begins with k_nl_init).  The graph is captured on first use per dt.
+bool graph_ready(nls_handle *h, double dt) {
+  if (!h->use_graph || h->collective || h->timing || h->runahead > 0) return false;
+  if (h->cplx_ && (!h->w0_ready || h->w0_dt != dt)) return false;
+  if (h->gexec && h->gdt == dt) return true;
+  if (h->gexec) {
+    hip_check(h, hipGraphExecDestroy(h->gexec), "hipGraphExecDestroy");
+    h->gexec = nullptr;
+  }
+  hipGraph_t g = nullptr;
+  hip_check(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+  try {
+    issue_step(h, dt);
+  } catch (...) {
+    (void)hipStreamEndCapture(h->stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+    throw;
+  }
+  hip_check(h, hipStreamEndCapture(h->stream, &g), "hipStreamEndCapture");
+  const hipError_t e = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  hip_check(h, e, "hipGraphInstantiate");
+  h->gdt = dt;
+  return true;
+}
+
 int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
   return guarded(h, [&] {
     if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
     if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");
     if (h->kg && !(dt > 0.0)) fail(h, NLS_ERR_ARG, "KG: dt must be > 0 (v = (u - u_past)/dt)");
-    const int m = h->m;
-    const int64_t n = h->geo.nloc;
-    int64_t vs = h->vs;
     for (uint32_t s = 0; s < nsteps; ++s) {
       // Optionally keep the host at most `runahead` steps ahead of the device
       // (bounded queue depth for callers that enqueue thousands of steps).
       const int ra = h->runahead;
       if (ra > 0 && h->steps_issued >= (uint64_t)ra)
         hip_check(h, hipEventSynchronize(h->stepev[h->steps_issued % ra]), "hipEventSynchronize");
-      if (h->cplx_) {
-        ss2_step(h, dt);
-      } else if (h->kg) {
-        // KGESolver::step (nlsolvers/device/include/kg_single.cuh:49-86): sinc^2 basis
-        // of g = -m u^3, cos basis of u (the operator sign is immaterial: both
-        // functions depend on sqrt|lambda| only)
-        {
-          void *u = vec_ptr(h, 0, 0);
-          void *g0 = vec_ptr(h, 1, 0);
-          void *args[] = {&u, &h->mf, &g0, (void *)&n};
-          pw_launch(h, 3, kernel_kg_g(), args);
-          halo(h, 1, 0);
-        }
-        run_lanczos(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
-        run_lanczos(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0);
-        {
-          void *W = vec_ptr(h, 0, 0);
-          void *W2 = vec_ptr(h, 1, 0);
-          KState *st = h->B[0].st, *st2 = h->B[1].st;
-          void *args[] = {&W, &W2, &vs, (void *)&n, &st, &st2, &h->up, &h->vel, &dt};
-          pw_launch(h, 3, kernel_kg_end(m), args);
-          halo(h, 0, 0);
-        }
-        h->vel_valid = true;
+      if (graph_ready(h, dt)) {
+        hip_check(h, hipGraphLaunch(h->gexec, h->stream), "hipGraphLaunch");
+        finish_step_flags(h, dt);
+        h->tacc.graph_steps += 1;
       } else {
-        // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u
-        run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0);
-        {
-          void *W = vec_ptr(h, 0, 0);
-          void *g0 = vec_ptr(h, 1, 0);
-          KState *st = h->B[0].st;
-          void *args[] = {&W, &vs, (void *)&n, &st, &h->mf, &h->up, &g0};
-          pw_launch(h, 3, kernel_sg_mid(m), args);
-          halo(h, 1, 0);
-        }
-        run_lanczos(h, 1, 1, NLS_F_SINC2_HALF, 0, dt, 0.0);
-        {
-          void *W2 = vec_ptr(h, 1, 0);
-          void *u = vec_ptr(h, 0, 0);
-          KState *st = h->B[1].st;
-          void *args[] = {&W2, &vs, (void *)&n, &st, &u, &h->up, &dt};
-          pw_launch(h, 3, kernel_sg_end(m), args);
-          halo(h, 0, 0);
-        }
+        issue_step(h, dt);
       }
       h->tacc.steps += 1;
       if (ra > 0) {

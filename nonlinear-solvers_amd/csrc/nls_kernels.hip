@@ -212,7 +212,8 @@ __device__ __noinline__ void eigen_phase_jacobi(KState *__restrict__ st, int m, 
     Q[i][j] = i == j ? 1.0 : 0.0;
   }
   __syncthreads();
-  for (int sweep = 0; sweep < 100; ++sweep) {
+  int sweep = 0;
+  for (; sweep < 100; ++sweep) {
     // convergence test on the whole matrix (oracle: off <= 1e-34 tot || off == 0)
     double off = 0.0, tot = 0.0;
     for (int e = t; e < m * m; e += NTHREADS) {
@@ -294,6 +295,9 @@ __device__ __noinline__ void eigen_phase_jacobi(KState *__restrict__ st, int m, 
       __syncthreads();
     }
   }
+#ifdef NLS_EIG_DEBUG
+  if (t == 0) printf("[jacobi] m=%d sweeps=%d\n", m, sweep);
+#endif
   // fin[f][r] = s0 / s_r * sum_k Q[r][k] Q[0][k] f(lambda_k)
   if (t < m) {
     st->lam[t] = A[t][t] * s_scl;
@@ -337,6 +341,9 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
     for (int c = 0; c < m; ++c) Q[lane][c] = lane == c ? 1.0 : 0.0;
   auto setd = [&](int i, double v) { if (lane == i) dl = v; };
   auto sete = [&](int i, double v) { if (lane == i) el = v; };
+#ifdef NLS_EIG_DEBUG
+  int tot_iter = 0, tot_rot = 0;
+#endif
   for (int l = 0; l < m; ++l) {
     int iter = 0;
     for (;;) {
@@ -347,6 +354,10 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
       }
       if (mm == l) break;
       if (++iter > 64) break;
+#ifdef NLS_EIG_DEBUG
+      ++tot_iter;
+      tot_rot += mm - l;
+#endif
       const double dlv = rdlane(dl, l), el_l = rdlane(el, l);
       double gg = (rdlane(dl, l + 1) - dlv) / (2.0 * el_l);
       double rr = hypot(gg, 1.0);
@@ -384,6 +395,9 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
       sete(mm, 0.0);
     }
   }
+#ifdef NLS_EIG_DEBUG
+  if (lane == 0) printf("[ql] m=%d iters=%d rotations=%d\n", m, tot_iter, tot_rot);
+#endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const double lam_l = dl * scl;
   if (lane < m) {

@@ -57,7 +57,7 @@ class Timing(C.Structure):
     _fields_ = [
         ("class_ms", C.c_double * 5), ("class_count", C.c_uint64 * 5),
         ("update_ms", C.c_double * MAX_KRYLOV), ("update_count", C.c_uint64 * MAX_KRYLOV),
-        ("steps", C.c_uint64),
+        ("steps", C.c_uint64), ("graph_steps", C.c_uint64),
     ]
 
 
@@ -113,7 +113,7 @@ def lib():
     L.nls_set_timing.argtypes = [H, C.c_int32]
     L.nls_get_timing.argtypes = [H, C.POINTER(Timing)]
     L.nls_reset_timing.argtypes = [H]
-    if L.nls_abi_version() != 1:
+    if L.nls_abi_version() != 2:
         raise RuntimeError("libnls_amd ABI mismatch")
     _LIB = L
     return L
@@ -319,4 +319,5 @@ class Solver:
             "update_ms": [t.update_ms[j] for j in range(MAX_KRYLOV)],
             "update_count": [int(t.update_count[j]) for j in range(MAX_KRYLOV)],
             "steps": int(t.steps),
+            "graph_steps": int(t.graph_steps),
         }
