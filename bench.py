@@ -242,16 +242,17 @@ def _cpu_sample(args, oracle_py):
             "kind": "port", "sample": sample, "seconds": el}
 
 
-def load_traffic(workload, m):
+def load_traffic(workload, m, kernel_prefix):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary
-    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950 read-side x2 correction)."""
+    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950 read-side x2 correction); None
+    unless the summary was taken on the same m and the same dominant kernel."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("m") != m:
+        if d.get("m") != m or not str(d.get("dominant_kernel", "")).startswith(kernel_prefix):
             return None
         return d.get("bytes_per_launch")
     except Exception:
@@ -349,14 +350,28 @@ def main():
     value = cells_total * args.steps / el / 1e6
     n_local = s.n_local
 
-    # dominant kernel: k_update<J = m-2>
-    J = max(m - 2, 0)
-    cnt = tm["update_count"][J]
-    avg_ms = tm["update_ms"][J] / cnt if cnt else float("nan")
+    # dominant kernel: the fused final pass k_final_fused<m> when the step uses it
+    # (NLSE, m >= 3: W_0..W_{m-2} read, u and the next W_0 written, + m(x) on G2),
+    # else the largest update pass k_update<J = m-2> (J+1 reads + 1 write)
     esz = 8 if w["eq"] in (2, 4) else 16
-    bytes_launch = (J + 2) * esz * n_local
+    fcnt = tm["class_count"].get("final", 0)
+    if fcnt:
+        J = m - 2
+        cnt = fcnt
+        avg_ms = tm["class_ms"]["final"] / fcnt
+        bytes_launch = ((m + 1) * esz + (8 if w["eq"] == 3 else 0)) * n_local
+        kname = f"k_final_fused<{m}> (stencil + last Lanczos vector + combination + N(1/2) x2, " \
+                f"{m - 1} reads + 2 writes)"
+        kprefix = "k_final_fused<"
+    else:
+        J = max(m - 2, 0)
+        cnt = tm["update_count"][J]
+        avg_ms = tm["update_ms"][J] / cnt if cnt else float("nan")
+        bytes_launch = (J + 2) * esz * n_local
+        kname = f"k_update<J={J}> (stencil + CGS + write, {J + 1} reads + 1 write)"
+        kprefix = "k_update<"
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if cnt else None
-    traffic = load_traffic(args.workload, m) if world == 1 else None
+    traffic = load_traffic(args.workload, m, kprefix) if world == 1 else None
     step_bytes = algorithmic_bytes_per_cell_step(m, w["eq"], w.get("sewi", False)) * n_local
     step_ms = el * 1e3 / args.steps
     result = {
@@ -379,7 +394,7 @@ def main():
                    "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
         "roofline": {
             "bound": "hbm",
-            "kernel": f"k_update<J={J}> (stencil + CGS + write, {J + 1} reads + 1 write)",
+            "kernel": kname,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define NLS_ABI_VERSION 2
+#define NLS_ABI_VERSION 3
 #define NLS_MAX_KRYLOV 32
 
 enum nls_status {
@@ -207,11 +207,12 @@ int nls_group_destroy(nls_group *g);
 
 /* Instrumentation: HIP-event timing around every launch on the handle's
  * stream.  Classes: 0 alpha (stencil + dot), 1 update (stencil + CGS +
- * write), 2 reduce/eigen, 3 nonlinear/final, 4 halo exchange.  For the
+ * write), 2 reduce/eigen, 3 nonlinear/pointwise, 4 halo exchange, 5 fused
+ * final pass (last Lanczos vector + combination + nonlinear steps).  For the
  * update class the per-j times are also kept (index = j). */
 typedef struct nls_timing {
-  double class_ms[5];
-  uint64_t class_count[5];
+  double class_ms[6];
+  uint64_t class_count[6];
   double update_ms[NLS_MAX_KRYLOV];
   uint64_t update_count[NLS_MAX_KRYLOV];
   uint64_t steps;

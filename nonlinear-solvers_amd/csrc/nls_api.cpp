@@ -103,6 +103,10 @@ struct nls_handle {
   cplx *partA = nullptr, *partU = nullptr;
   int grid_alpha = 1, grid_lap = 1, grid_pw = 1;
   int kz_alpha = 4;
+  // fused tail (NLSE SS2, m >= 3): the last update pass and the final
+  // combination are one pass, k_final_fused (NLS_FUSED_TAIL=0 disables)
+  bool fused_tail = false;
+  int grid_alpha2 = 1, kz_alpha2 = 8, grid_fused = 1;
   UpdPlan plan[MMAX];
   bool field_set = false, w0_ready = false;
   double w0_dt = 0.0;  // dt the live start vector W_0 = N(u) was built with
@@ -384,6 +388,15 @@ void colsum(nls_handle *h, int b, int j, const cplx *pA, int nbA, int ncA, int n
   launch(h, 2, j, kernel_colsum(), ncA + ncU, args);
 }
 
+// Last alpha pass of a fused-tail basis: k_alpha_l2 (also ||L W_j||^2)
+void alpha_l2_pass(nls_handle *h, int b, int j) {
+  void *vj = vec_ptr(h, b, j);
+  Geo gg = h->geo;
+  gg.kz = h->kz_alpha2;
+  void *args[] = {&vj, &gg, &h->partA};
+  launch(h, 0, j, kernel_alpha_l2(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_alpha2, args);
+}
+
 // Launch k_alpha<j> on vector j of basis b
 void alpha_pass(nls_handle *h, int b, int j, const Geo &ga) {
   void *vj = vec_ptr(h, b, j);
@@ -392,64 +405,75 @@ void alpha_pass(nls_handle *h, int b, int j, const Geo &ga) {
   launch(h, 0, j, kernel_alpha(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_alpha, args);
 }
 
-void reduce_iter(nls_handle *h, int b, int j) {
+// ncA = 2 after k_alpha, 3 after k_alpha_l2 (fused tail)
+void reduce_iter(nls_handle *h, int b, int j, int ncA = 2) {
   KState *st = h->B[b].st;
-  int nbA = h->grid_alpha, nbU = j >= 1 ? h->plan[j - 1].total : 0;
+  int nbA = ncA == 3 ? h->grid_alpha2 : h->grid_alpha, nbU = j >= 1 ? h->plan[j - 1].total : 0;
   const void *fn = kernel_reduce_iter();
+  const int ncols = ncA + (j >= 1 ? j + 1 : 0);
   if (nbA > COLSUM_MIN || nbU > COLSUM_MIN) {
-    colsum(h, b, j, h->partA, nbA, 2, nbU, j >= 1 ? j + 1 : 0);
-    if (h->collective) allreduce_sums(h, b, 2 + (j >= 1 ? j + 1 : 0));
+    colsum(h, b, j, h->partA, nbA, ncA, nbU, j >= 1 ? j + 1 : 0);
+    if (h->collective) allreduce_sums(h, b, ncols);
     int ds = 0, dc = 1;
-    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc};
+    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA};
     launch(h, 2, j, fn, 1, args);
     return;
   }
   if (!h->collective) {
     int ds = 1, dc = 1;
-    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc};
+    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA};
     launch(h, 2, j, fn, 1, args);
   } else {
     int ds = 1, dc = 0;
-    void *a1[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc};
+    void *a1[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA};
     launch(h, 2, j, fn, 1, a1);
-    allreduce_sums(h, b, 2 + (j >= 1 ? j + 1 : 0));
+    allreduce_sums(h, b, ncols);
     ds = 0;
     dc = 1;
-    void *a2[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc};
+    void *a2[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA};
     launch(h, 2, j, fn, 1, a2);
   }
 }
 
-void reduce_final(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
+void reduce_final(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti, int tail = 0) {
   KState *st = h->B[b].st;
   int m = h->m, nbU = m >= 2 ? h->plan[m - 2].total : 0;
   const void *fn = kernel_reduce_final();
+  if (tail) {  // s_{m-1} already set by the last reduce_iter; no sums
+    int ds = 0, dc = 1;
+    void *args[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti, &tail};
+    launch(h, 2, m, fn, 1, args);
+    return;
+  }
   if (nbU > COLSUM_MIN) {
     colsum(h, b, m, nullptr, 0, 0, nbU, m);
     if (h->collective) allreduce_sums(h, b, m);
     int ds = 0, dc = 1;
-    void *args[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti};
+    void *args[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti, &tail};
     launch(h, 2, m, fn, 1, args);
     return;
   }
   if (!h->collective) {
     int ds = 1, dc = 1;
-    void *args[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti};
+    void *args[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti, &tail};
     launch(h, 2, m, fn, 1, args);
   } else {
     int ds = 1, dc = 0;
-    void *a1[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti};
+    void *a1[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti, &tail};
     launch(h, 2, m, fn, 1, a1);
     if (m >= 2) allreduce_sums(h, b, m);
     ds = 0;
     dc = 1;
-    void *a2[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti};
+    void *a2[] = {&st, &h->partU, &nbU, &m, &ds, &dc, &nf, &f0, &f1, &tr, &ti, &tail};
     launch(h, 2, m, fn, 1, a2);
   }
 }
 
 // Precondition: vector 0 of basis b holds the start vector and its halo.
-void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
+// tail = true (m >= 3): stop after the alpha pass of W_{m-2} (k_alpha_l2); the
+// last vector W_{m-1} is recomputed inside the caller's k_final_fused.
+void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti,
+                 bool tail = false) {
   const int m = h->m;
   Geo g = h->geo;
   Geo ga = g;  // the alpha pass has its own tile depth
@@ -463,6 +487,12 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
     void *out = vec_ptr(h, b, j + 1);
     if (j >= 1) {
       halo_wait(h);
+      if (tail && j + 2 == m) {
+        alpha_l2_pass(h, b, j);
+        reduce_iter(h, b, j, 3);
+        reduce_final(h, b, nf, f0, f1, tr, ti, 1);
+        return;
+      }
       alpha_pass(h, b, j, ga);
       reduce_iter(h, b, j);
     }
@@ -588,6 +618,16 @@ void alloc_all(nls_handle *h) {
   h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim, ani), stencil_tiles(ga, dim, alpha_rows_per_thread()));
   h->grid_lap = occupancy_grid(h, kernel_lap(c, dim, ani), stencil_tiles(g, dim, alpha_rows_per_thread()));
   int64_t cap = 2 * (int64_t)h->grid_alpha;
+  h->fused_tail = c && h->m >= 3;
+  if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && std::atoi(e) != 0;
+  if (h->fused_tail) {
+    Geo g2 = g;
+    if (const char *e = std::getenv("NLS_KZ_ALPHA2")) h->kz_alpha2 = std::max(1, std::atoi(e));
+    g2.kz = h->kz_alpha2;
+    h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_rows_per_thread()));
+    const void *ff = kernel_final_fused(dim, h->m, ani);
+    h->grid_fused = occupancy_grid(h, ff, stencil_tiles(g, dim, fused_rows_per_thread()));
+  }
   for (int j = 0; j + 1 < h->m; ++j) {
     const void *fu = kernel_update(c, dim, j, ani);
     UpdPlan &pl = h->plan[j];
@@ -614,7 +654,8 @@ void alloc_all(nls_handle *h) {
     }
     cap = std::max<int64_t>(cap, (int64_t)pl.total * (j + 2));
   }
-  hip_check(h, hipMalloc(&h->partA, 2 * (size_t)h->grid_alpha * sizeof(cplx)), "hipMalloc(partA)");
+  const size_t na = std::max<size_t>(2 * (size_t)h->grid_alpha, h->fused_tail ? 3 * (size_t)h->grid_alpha2 : 0);
+  hip_check(h, hipMalloc(&h->partA, na * sizeof(cplx)), "hipMalloc(partA)");
   hip_check(h, hipMalloc(&h->partU, (size_t)cap * sizeof(cplx)), "hipMalloc(partU)");
   h->grid_pw = (int)std::max<int64_t>(1, std::min<int64_t>((g.nloc + NTHREADS - 1) / NTHREADS, 8192));
 }
@@ -934,13 +975,20 @@ void ss2_step(nls_handle *h, double dt) {
     pw_launch(h, 3, kernel_nl_init(), args);
     halo(h, 0, 0);
   }
-  if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt);
-  else run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt);
+  const bool tail = h->fused_tail;
+  if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt, tail);
+  else run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt, tail);
   void *W = vec_ptr(h, 0, 0);
   KState *st = h->B[0].st;
   int nl = h->nonlin;
-  void *args[] = {&W, &vs, (void *)&n, &st, &h->u, &h->mf, &dt, &nl, &h->s1, &h->s2};
-  pw_launch(h, 3, kernel_final_nlse(m), args);
+  if (tail) {
+    Geo g = h->geo;
+    void *args[] = {&W, &vs, &g, &st, &h->u, &h->mf, &dt, &nl, &h->s1, &h->s2};
+    launch(h, 5, m, kernel_final_fused((int)h->cfg.dim, m, h->ani), h->grid_fused, args);
+  } else {
+    void *args[] = {&W, &vs, (void *)&n, &st, &h->u, &h->mf, &dt, &nl, &h->s1, &h->s2};
+    pw_launch(h, 3, kernel_final_nlse(m), args);
+  }
   halo(h, 0, 0);
   h->w0_ready = true;
   h->w0_dt = dt;

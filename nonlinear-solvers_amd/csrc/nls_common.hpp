@@ -71,4 +71,66 @@ __device__ __forceinline__ double bcast(double v, int l) { return __shfl(v, l, 6
 __device__ __forceinline__ cplx bcast(cplx v, int l) { return {__shfl(v.re, l, 64), __shfl(v.im, l, 64)}; }
 
 
+// ---------------------------------------------------------------------------
+// Nonlinear half step, tau = 1j*dt
+//  0 cubic (nlse_solver.hpp:66-69): out = exp(-0.5*tau*rho) u, rho = re^2 + im^2
+//  1 cubic-quintic (device/nlse_cq_solver.hpp:16-39): d = |u|*|u|, rho = s1 d + s2 d^2
+//  2 G2 cubic with focusing field (nlsolvers/device/include/nlse_dev.hpp:20-40):
+//    out = u * exp(0.5*tau * m|u|^2)   (note the sign: G2 integrates with +tau)
+//
+// sin/cos of the phase without OCML's sincos, whose large-argument (Payne-Hanek)
+// path needs so many registers that it sets the register budget of every
+// streaming kernel ending in this step (k_final_fused: 1 wave/SIMD instead of 2).
+// Cody-Waite reduction r = x - n pi/2 with a two-term FMA split of pi/2 (absolute
+// error ~1e-16 for every |x| < 2^53), then Taylor polynomials on |r| <= pi/4 to
+// r^17 / r^18 (truncation < 1e-19); ~1 ulp against libm in the common case of a
+// small phase (dt |u|^2 / 2), where n = 0 and r = x exactly.
+__device__ __forceinline__ void nl_sincos(double x, double &sn, double &cs) {
+  const double n = rint(x * 0.63661977236758134308);
+  double r = fma(-n, 1.5707963267948966, x);
+  r = fma(-n, 6.123233995736766e-17, r);
+  const double z = r * r;
+  double ps = 1.0 / 355687428096000.0;            //  1/17!
+  ps = fma(ps, z, -1.0 / 1307674368000.0);        // -1/15!
+  ps = fma(ps, z, 1.0 / 6227020800.0);            //  1/13!
+  ps = fma(ps, z, -1.0 / 39916800.0);             // -1/11!
+  ps = fma(ps, z, 1.0 / 362880.0);                //  1/9!
+  ps = fma(ps, z, -1.0 / 5040.0);                 // -1/7!
+  ps = fma(ps, z, 1.0 / 120.0);                   //  1/5!
+  ps = fma(ps, z, -1.0 / 6.0);                    // -1/3!
+  const double s = fma(r * z, ps, r);
+  double pc = 1.0 / 6402373705728000.0;           //  1/18!
+  pc = fma(pc, z, -1.0 / 20922789888000.0);       // -1/16!
+  pc = fma(pc, z, 1.0 / 87178291200.0);           //  1/14!
+  pc = fma(pc, z, -1.0 / 479001600.0);            // -1/12!
+  pc = fma(pc, z, 1.0 / 3628800.0);               //  1/10!
+  pc = fma(pc, z, -1.0 / 40320.0);                // -1/8!
+  pc = fma(pc, z, 1.0 / 720.0);                   //  1/6!
+  pc = fma(pc, z, -1.0 / 24.0);                   // -1/4!  (times -z^2 below)
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;                      // fdlibm-style split of 1 - z/2
+  const double c = w + (((1.0 - w) - hz) - (z * z) * pc);
+  const int q = (int)(n - 4.0 * floor(0.25 * n));  // quadrant, 0..3
+  sn = q == 0 ? s : q == 1 ? c : q == 2 ? -s : -c;
+  cs = q == 0 ? c : q == 1 ? -s : q == 2 ? -c : s;
+}
+
+__device__ __forceinline__ cplx nl_half(cplx u, double mval, double dt, int nonlin, cplx s1, cplx s2) {
+  if (nonlin == 0 || nonlin == 2) {
+    const double x = u.re * u.re + u.im * u.im;
+    const double ph = nonlin == 0 ? (-0.5 * dt) * x : (0.5 * dt) * (mval * x);
+    double sn, cs;
+    nl_sincos(ph, sn, cs);
+    return {cs * u.re - sn * u.im, cs * u.im + sn * u.re};
+  }
+  const double a = hypot(u.re, u.im);
+  const double d = a * a;
+  const cplx rho = d * s1 + (d * d) * s2;
+  const cplx z = cmul({-0.0, -0.5 * dt}, rho);
+  const double er = exp(z.re);
+  double sn, cs;
+  nl_sincos(z.im, sn, cs);
+  return cmul({er * cs, er * sn}, u);
+}
+
 }  // namespace nls

@@ -48,6 +48,7 @@ int64_t stencil_tiles(const Geo &g, int dim, int rb) {
 }
 int update_rows_per_thread(int J, bool ani) { return upd_rb(J, ani); }
 int alpha_rows_per_thread() { return RB_ALPHA; }
+int fused_rows_per_thread() { return FUSED_RB; }
 
 // ---------------------------------------------------------------------------
 // single-workgroup reductions + coefficient math + m x m eigensolve
@@ -85,8 +86,8 @@ const void *kernel_colsum() { return reinterpret_cast<const void *>(&k_colsum); 
 __global__ __launch_bounds__(NTHREADS) void k_reduce_iter(KState *__restrict__ st,
                                                           const cplx *__restrict__ partA, int nbA,
                                                           const cplx *__restrict__ partU, int nbU,
-                                                          int j, int do_sum, int do_coef) {
-  reduce_iter_body(st, partA, nbA, partU, nbU, j, do_sum, do_coef);
+                                                          int j, int do_sum, int do_coef, int ncA) {
+  reduce_iter_body(st, partA, nbA, partU, nbU, j, do_sum, do_coef, ncA);
 }
 
 __device__ __forceinline__ double sinc_ref(double x) {  // eigen_krylov_real.hpp:95-97
@@ -137,7 +138,8 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
 __device__ __noinline__ void eigen_phase_jacobi(KState *__restrict__ st, int m, int nf, int f0,
                                                 int f1, double t_re, double t_im);
 
-// After the last k_update<m-2>: sums[0..m-1] = g_0..g_{m-2}, nn.  Completes
+// After the last k_update<m-2>: sums[0..m-1] = g_0..g_{m-2}, nn (tail = 1: no
+// last update, s_{m-1} already set by the last k_reduce_iter).  Completes
 // T (T(m-1,m-1) = 0, eigen_krylov_complex.hpp:21), diagonalises it with
 // implicit-shift QL on wave 0 (lane r owns row r of Q) and writes
 //   fin[f][k] = s_0 * (Q f(Lambda) Q^T e_1)_k / s_k
@@ -146,9 +148,11 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_final(KState *__restrict__ 
                                                            const cplx *__restrict__ partU, int nbU,
                                                            int m, int do_sum, int do_coef, int nf,
                                                            int f0, int f1, double t_re,
-                                                           double t_im) {
+                                                           double t_im, int tail) {
   __shared__ cplx ssum[MMAX];
-  if (do_sum && m >= 2) {
+  if (tail) {
+    // fused tail: s_{m-1} was set by k_reduce_iter<m-2> (ncA = 3), no sums here
+  } else if (do_sum && m >= 2) {
     sum_partials(partU, nbU, m, ssum);
     __syncthreads();
     if (!do_coef) {
@@ -160,7 +164,7 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_final(KState *__restrict__ 
     __syncthreads();
   }
   if (!do_coef) return;
-  if (threadIdx.x == 0 && m >= 2) {
+  if (threadIdx.x == 0 && m >= 2 && !tail) {
     const double s = sqrt(ssum[m - 1].re);
     st->s[m - 1] = s;
     st->To[m - 2] = s;
@@ -415,29 +419,6 @@ __device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf,
 
 // ---------------------------------------------------------------------------
 // pointwise kernels
-
-// Nonlinear half step, tau = 1j*dt
-//  0 cubic (nlse_solver.hpp:66-69): out = exp(-0.5*tau*rho) u, rho = re^2 + im^2
-//  1 cubic-quintic (device/nlse_cq_solver.hpp:16-39): d = |u|*|u|, rho = s1 d + s2 d^2
-//  2 G2 cubic with focusing field (nlsolvers/device/include/nlse_dev.hpp:20-40):
-//    out = u * exp(0.5*tau * m|u|^2)   (note the sign: G2 integrates with +tau)
-__device__ __forceinline__ cplx nl_half(cplx u, double mval, double dt, int nonlin, cplx s1, cplx s2) {
-  if (nonlin == 0 || nonlin == 2) {
-    const double x = u.re * u.re + u.im * u.im;
-    const double ph = nonlin == 0 ? (-0.5 * dt) * x : (0.5 * dt) * (mval * x);
-    double sn, cs;
-    sincos(ph, &sn, &cs);
-    return {cs * u.re - sn * u.im, cs * u.im + sn * u.re};
-  }
-  const double a = hypot(u.re, u.im);
-  const double d = a * a;
-  const cplx rho = d * s1 + (d * d) * s2;
-  const cplx z = cmul({-0.0, -0.5 * dt}, rho);
-  const double er = exp(z.re);
-  double sn, cs;
-  sincos(z.im, &sn, &cs);
-  return cmul({er * cs, er * sn}, u);
-}
 
 __global__ __launch_bounds__(NTHREADS) void k_nl_init(const cplx *__restrict__ u, cplx *__restrict__ w0,
                                                       const double *__restrict__ mf, int64_t n,
@@ -781,6 +762,10 @@ Table table(int dim, bool ani) {
 const void *kernel_update(bool cplx_, int dim, int J, bool ani) { return table(dim, ani)(NLS_KIND_UPDATE, cplx_, J); }
 const void *kernel_alpha(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_ALPHA, cplx_, 0); }
 const void *kernel_lap(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_LAP, cplx_, 0); }
+const void *kernel_alpha_l2(bool cplx_, int dim, bool ani) {
+  return table(dim, ani)(NLS_KIND_ALPHA_L2, cplx_, 0);
+}
+const void *kernel_final_fused(int dim, int M, bool ani) { return table(dim, ani)(NLS_KIND_FINAL, true, M); }
 
 // local-transport all-reduce: dst[v] = sum_r pub[r][parity][v] in rank order
 __global__ __launch_bounds__(NTHREADS) void k_sum_ranks(cplx *__restrict__ dst, const cplx *__restrict__ pub,

@@ -17,9 +17,16 @@ const void *kernel_lap(bool complex_, int dim, bool ani);
 int64_t stencil_tiles(const Geo &g, int dim, int rows_per_thread);
 int update_rows_per_thread(int J, bool ani);
 int alpha_rows_per_thread();
+int fused_rows_per_thread();
 
 // per-variant tables (nls_stencil.hip, one object per operator x dimension)
-enum { NLS_KIND_UPDATE = 0, NLS_KIND_ALPHA = 1, NLS_KIND_LAP = 2 };
+enum { NLS_KIND_UPDATE = 0, NLS_KIND_ALPHA = 1, NLS_KIND_LAP = 2, NLS_KIND_ALPHA_L2 = 3,
+       NLS_KIND_FINAL = 4 };
+//   alpha_l2 : (const S* V, Geo g, cplx* part)  -- 3 partial columns: a, ||V||^2, ||L V||^2
+//   final_fused(M): (cplx* W, int64_t vs, Geo g, const KState*, cplx* u, const double* mf,
+//                    double dt, int nonlin, cplx s1, cplx s2)   -- complex, 3 <= M <= 32
+const void *kernel_alpha_l2(bool complex_, int dim, bool ani);
+const void *kernel_final_fused(int dim, int M, bool ani);
 const void *stencil_table_iso2(int kind, bool complex_, int J);
 const void *stencil_table_iso3(int kind, bool complex_, int J);
 const void *stencil_table_ani2(int kind, bool complex_, int J);
@@ -27,9 +34,9 @@ const void *stencil_table_ani3(int kind, bool complex_, int J);
 
 // single workgroup:
 //   reduce_iter  : (KState*, const cplx* partA, int nbA, const cplx* partU, int nbU, int j,
-//                   int do_sum, int do_coef)
+//                   int do_sum, int do_coef, int ncA)     -- ncA = 3 after k_alpha_l2
 //   reduce_final : (KState*, const cplx* partU, int nbU, int m, int do_sum, int do_coef,
-//                   int nf, int f0, int f1, double t_re, double t_im)
+//                   int nf, int f0, int f1, double t_re, double t_im, int tail)
 const void *kernel_reduce_iter();
 //   sum_ranks    : (cplx* dst, const cplx* pub, int nranks, int parity, int n, int stride)
 const void *kernel_sum_ranks();

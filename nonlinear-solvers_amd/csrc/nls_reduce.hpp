@@ -30,20 +30,27 @@ __device__ inline void sum_partials(const cplx *__restrict__ part, int nb, int n
 __device__ __forceinline__ double inv_or_zero(double s) { return s > 0.0 ? 1.0 / s : 0.0; }
 
 // After k_alpha<j> (and k_update<j-1>): sums layout
-//   sums[0] = a_j, sums[1] = ||W_j||^2 (A pass), sums[2 .. 2+j] = g_0..g_{j-1}, nn (U pass)
+//   sums[0] = a_j, sums[1] = ||W_j||^2 (A pass), [sums[2] = ||L W_j||^2 if ncA == 3],
+//   sums[ncA .. ncA+j] = g_0..g_{j-1}, nn (U pass)
 // Coefficients of k_update<j> (all from the Gram column of W_j and the
 // Hessenberg columns already known; see DESIGN.md "Lanczos reformulation"):
 //   H[j][j] = alpha_j = a_j / s_j^2
 //   H[j][k] = sum_{l<=k} conj(H[k][l]) G[j][l] + s_{k+1} G[j][k+1]   (k < j)
 //   coef[k] = H[j][k] / s_k,  coef[j+1] = 1 / s_j
+// ncA == 3 (fused tail, j = m-2: W_{j+1} is never stored): the norm of the last
+// vector from the Krylov relation of the orthonormal basis,
+//   s_{j+1}^2 = ||L v_j||^2 - sum_{k<=j} |H[j][k]|^2,
+// exact up to rounding of order eps ||L||^2 / s_{j+1}^2; s_{j+1} only enters the
+// last (smallest) coefficient of f(T) e_1, so that error is far below the
+// tolerance of the path.  A non-positive value is a breakdown (column zero).
 __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__restrict__ partA,
                                         int nbA, const cplx *__restrict__ partU, int nbU, int j,
-                                        int do_sum, int do_coef) {
+                                        int do_sum, int do_coef, int ncA) {
   __shared__ cplx ssum[2 * MMAX + 8];
-  const int ncols = 2 + (j >= 1 ? j + 1 : 0);
+  const int ncols = ncA + (j >= 1 ? j + 1 : 0);
   if (do_sum) {
-    sum_partials(partA, nbA, 2, ssum);
-    if (j >= 1) sum_partials(partU, nbU, j + 1, ssum + 2);
+    sum_partials(partA, nbA, ncA, ssum);
+    if (j >= 1) sum_partials(partU, nbU, j + 1, ssum + ncA);
     __syncthreads();
     if (!do_coef) {
       for (int v = threadIdx.x; v < ncols; v += NTHREADS) st->sums[v] = ssum[v];
@@ -66,11 +73,11 @@ __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__r
     const int k = e / MMAX, l = e % MMAX;
     if (l <= k) s_H[k][l] = st->H[k][l];
   }
-  const double sj = sqrt(j == 0 ? ssum[1].re : ssum[2 + j].re);
+  const double sj = sqrt(j == 0 ? ssum[1].re : ssum[ncA + j].re);
   const double isj = inv_or_zero(sj);
   if (t == 0) s_s[j] = sj;
   __syncthreads();
-  for (int k = t; k < j; k += NTHREADS) s_G[k] = (inv_or_zero(s_s[k]) * isj) * ssum[2 + k];
+  for (int k = t; k < j; k += NTHREADS) s_G[k] = (inv_or_zero(s_s[k]) * isj) * ssum[ncA + k];
   if (t == 0) s_G[j] = {sj > 0.0 ? 1.0 : 0.0, 0.0};
   __syncthreads();
   const cplx alpha = (isj * isj) * ssum[0];
@@ -88,6 +95,7 @@ __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__r
     st->H[j][k] = h;
     st->G[j][k] = s_G[k];
     st->coef[k] = inv_or_zero(s_s[k]) * h;
+    if (ncA == 3) s_H[j][k] = h;
   }
   if (t == 0) {
     st->s[j] = sj;
@@ -98,6 +106,18 @@ __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__r
     } else {
       st->To[j - 1] = sj;
       if (!(sj > 0.0) && st->breakdown == 0) st->breakdown = j + 1;
+    }
+  }
+  if (ncA == 3) {
+    __syncthreads();
+    if (t == 0) {
+      double h2 = 0.0;
+      for (int k = 0; k <= j; ++k) h2 += abs2(s_H[j][k]);
+      const double r2 = ssum[2].re * (isj * isj) - h2;
+      const double sn = r2 > 0.0 && sj > 0.0 ? sqrt(r2) : 0.0;
+      st->s[j + 1] = sn;
+      st->To[j] = sn;
+      if (!(sn > 0.0) && st->breakdown == 0) st->breakdown = j + 2;
     }
   }
 }

@@ -283,6 +283,10 @@ __host__ __device__ constexpr int upd_rb(int J, bool ani = false) {
 }
 template <int J, bool ANI> struct UpdRB { static constexpr int v = upd_rb(J, ANI); };
 constexpr int RB_ALPHA = 4;
+#ifndef NLS_FUSED_RB
+#define NLS_FUSED_RB 1
+#endif
+constexpr int FUSED_RB = NLS_FUSED_RB;  // rows per thread of k_final_fused
 
 // y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
 template <class S, int DIM, bool ANI>
@@ -524,9 +528,87 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
 #undef NLS_RELOAD
 }
 
+// Last alpha pass of a fused-tail Lanczos (see k_final_fused): full stencil per
+// cell, so besides a = V^H L V and ||V||^2 it also reduces ||L V||^2, from which
+// the norm of the never-stored last vector follows (k_reduce_iter, ncA = 3).
+template <class S, int DIM, bool ANI>
+__global__ __launch_bounds__(NTHREADS) void k_alpha_l2(const S *__restrict__ V, Geo g,
+                                                       cplx *__restrict__ part) {
+  double a = 0.0, n2 = 0.0, l2 = 0.0;
+  march<S, DIM, RB_ALPHA, false, ANI>(V, g, [&](int, const S &c, const S &lap) {
+    a += to_c(cj_mul(c, lap)).re;
+    n2 += abs2(c);
+    l2 += abs2(lap);
+  });
+  cplx v[3] = {{a, 0.0}, {n2, 0.0}, {l2, 0.0}};
+  block_store<3>(v, part, gridDim.x, 0);
+}
+
+// Fused tail of an NLSE step (complex, M >= 3): the last Lanczos vector is
+// never stored.  With J = M-2, the pass marches W_J with the stencil and
+// streams W_0..W_{J-1}.  The last vector k_update<J> would have written,
+//   W_{M-1} = a L W_J - sum_{k<=J} b_k W_k      (a = 1/s_J, b_k = H[J][k]/s_k),
+// enters the final combination  y = sum_{k<M-1} fin_k W_k + fin_{M-1} W_{M-1}
+// (k_final_nlse's value) only linearly, so the pass evaluates
+//   y = (fin_{M-1} a) L W_J + sum_{k<=J} (fin_k - fin_{M-1} b_k) W_k
+// with the M coefficients folded once per workgroup, then u = N(y) and
+// W_0 <- N(u) for the next step, in place (W_0 is read only at the thread's own
+// cell).  Replaces k_update<M-2> + k_final_nlse<M>: M+1 streams instead of 2M+2.
+// The norm s_{M-1} the eigensolve needs comes from the last alpha pass:
+// ||W_{M-1}||^2 = ||L v_J||^2 - sum_k |H[J][k]|^2 (orthonormal basis).
+template <int DIM, int M, bool ANI>
+__global__ __launch_bounds__(NTHREADS) void k_final_fused(cplx *__restrict__ W, int64_t vs, Geo g,
+                                                          const KState *__restrict__ st,
+                                                          cplx *__restrict__ u,
+                                                          const double *__restrict__ mf, double dt,
+                                                          int nonlin, cplx s1, cplx s2) {
+  static_assert(M >= 3, "the stencil vector must not be W_0 (updated in place)");
+  constexpr int J = M - 2;
+  __shared__ cplx cf[MMAX + 1];  // cf[k] for W_k (k <= J), cf[J+1] for L W_J
+  if (threadIdx.x <= J + 1) {
+    const cplx fl = st->fin[0][J + 1];
+    const int k = threadIdx.x;
+    cf[k] = k <= J ? st->fin[0][k] - cmul(fl, st->coef[k]) : st->coef[J + 1].re * fl;
+  }
+  __syncthreads();
+  const cplx *__restrict__ VJ = W + (int64_t)J * vs;
+  // one row per thread: with the nonlinear steps at the end of the combination,
+  // two rows no longer fit in the 256 registers of two waves per SIMD
+  constexpr int RB = FUSED_RB;
+  march<cplx, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const cplx *cur, const cplx *lap, const bool *ok) {
+    cplx wk[RB][J];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const cplx *__restrict__ src = W + p[r];
+#pragma unroll
+      for (int k = 0; k < J; ++k) {
+        wk[r][k] = ok[r] ? ld_nt(src) : zero<cplx>();
+        src += vs;
+      }
+    }
+    asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (!ok[r]) continue;
+      cplx y = zero<cplx>();
+#pragma unroll
+      for (int k = 0; k < J; ++k) y += cmul(cf[k], wk[r][k]);
+      y += cmul(cf[J], cur[r]);
+      y += cmul(cf[J + 1], lap[r]);
+      const double mv = nonlin == 2 ? mf[p[r]] : 0.0;
+      const cplx un = nl_half(y, mv, dt, nonlin, s1, s2);
+      st_nt(u + p[r], un);
+      st_nt(W + p[r], nl_half(un, mv, dt, nonlin, s1, s2));
+    }
+  });
+}
+
 #define NLS_J_LIST(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
   X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) \
   X(28) X(29) X(30)
+#define NLS_MF_LIST(X) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) \
+  X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) \
+  X(29) X(30) X(31) X(32)
 #define NLS_M_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) \
   X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) \
   X(29) X(30) X(31) X(32)

@@ -55,7 +55,7 @@ class Config(C.Structure):
 
 class Timing(C.Structure):
     _fields_ = [
-        ("class_ms", C.c_double * 5), ("class_count", C.c_uint64 * 5),
+        ("class_ms", C.c_double * 6), ("class_count", C.c_uint64 * 6),
         ("update_ms", C.c_double * MAX_KRYLOV), ("update_count", C.c_uint64 * MAX_KRYLOV),
         ("steps", C.c_uint64), ("graph_steps", C.c_uint64),
     ]
@@ -113,7 +113,7 @@ def lib():
     L.nls_set_timing.argtypes = [H, C.c_int32]
     L.nls_get_timing.argtypes = [H, C.POINTER(Timing)]
     L.nls_reset_timing.argtypes = [H]
-    if L.nls_abi_version() != 2:
+    if L.nls_abi_version() != 3:
         raise RuntimeError("libnls_amd ABI mismatch")
     _LIB = L
     return L
@@ -312,7 +312,7 @@ class Solver:
     def timing(self) -> dict:
         t = Timing()
         self._call(lib().nls_get_timing, C.byref(t))
-        names = ["alpha", "update", "reduce", "pointwise", "halo"]
+        names = ["alpha", "update", "reduce", "pointwise", "halo", "final"]
         return {
             "class_ms": {n: t.class_ms[i] for i, n in enumerate(names)},
             "class_count": {n: int(t.class_count[i]) for i, n in enumerate(names)},

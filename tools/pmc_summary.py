@@ -45,12 +45,17 @@ def main():
             h, mi = c["TCC_HIT_sum"], c["TCC_MISS_sum"]
             e["l2_hit_rate"] = h / max(h + mi, 1)
         kernels[name] = e
-    dom = next((k for k in kernels if re.fullmatch(rf"k_update<[^,]*, [23], {J}(, (true|false))?>", k)), None)
+    # dominant kernel: the fused final pass when the step has one, else k_update<m-2>
+    dom = next((k for k in kernels if re.fullmatch(rf"k_final_fused<[23], {m}, (true|false)>", k)), None)
+    alg = (m + 1) * esz * cells
+    if dom is None:
+        dom = next((k for k in kernels if re.fullmatch(rf"k_update<[^,]*, [23], {J}(, (true|false))?>", k)), None)
+        alg = (J + 2) * esz * cells
     res = {
         "workload": workload, "m": m, "cells": cells,
         "dominant_kernel": dom,
         "bytes_per_launch": (kernels[dom]["read_bytes"] + kernels[dom]["write_bytes"]) if dom else None,
-        "algorithmic_bytes_per_launch": (J + 2) * esz * cells,
+        "algorithmic_bytes_per_launch": alg,
         "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-counting of wide streaming reads); "
                       "write = WRITE_SIZE x 1024; separate --pmc passes",
         "kernels": kernels,
