@@ -355,7 +355,7 @@ def main():
     # else the largest update pass k_update<J = m-2> (J+1 reads + 1 write)
     esz = 8 if w["eq"] in (2, 4) else 16
     fcnt = tm["class_count"].get("final", 0)
-    if fcnt:
+    if fcnt and w["eq"] in (0, 1, 3) and not w.get("sewi"):
         J = m - 2
         cnt = fcnt
         avg_ms = tm["class_ms"]["final"] / fcnt
@@ -363,8 +363,8 @@ def main():
         kname = f"k_final_fused<{m}> (stencil + last Lanczos vector + combination + N(1/2) x2, " \
                 f"{m - 1} reads + 2 writes)"
         kprefix = "k_final_fused<"
-    else:
-        J = max(m - 2, 0)
+    else:  # the largest update pass that ran (m-3 where the basis ends in a fused tail)
+        J = max([j for j, c in enumerate(tm["update_count"]) if c] or [0])
         cnt = tm["update_count"][J]
         avg_ms = tm["update_ms"][J] / cnt if cnt else float("nan")
         bytes_launch = (J + 2) * esz * n_local

@@ -103,10 +103,11 @@ struct nls_handle {
   cplx *partA = nullptr, *partU = nullptr;
   int grid_alpha = 1, grid_lap = 1, grid_pw = 1;
   int kz_alpha = 4;
-  // fused tail (NLSE SS2, m >= 3): the last update pass and the final
-  // combination are one pass, k_final_fused (NLS_FUSED_TAIL=0 disables)
+  // fused tail (m >= 3): the last update pass of a basis and the combination
+  // that ends the step are one pass, k_tail (NLS_FUSED_TAIL=0 disables)
   bool fused_tail = false;
-  int grid_alpha2 = 1, kz_alpha2 = 8, grid_fused = 1;
+  int grid_alpha2 = 1, kz_alpha2 = 8, kz_fused = 0;  // kz_fused 0: geo.kz
+  int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   UpdPlan plan[MMAX];
   bool field_set = false, w0_ready = false;
   double w0_dt = 0.0;  // dt the live start vector W_0 = N(u) was built with
@@ -575,6 +576,10 @@ void setup_geometry(nls_handle *h) {
   h->vs = (g.nzl + 2) * g.P + pad;
 }
 
+bool tail_complex(int mode) {
+  return mode == TAIL_NLSE || mode == TAIL_COMBINE_W0 || mode == TAIL_COMBINE || mode == TAIL_SEWI_END;
+}
+
 void alloc_all(nls_handle *h) {
   const Geo &g = h->geo;
   // NLS_U_SLOT=1 [NLS_U_OFF=k]: keep the NLSE state u in an extra slot after
@@ -618,15 +623,20 @@ void alloc_all(nls_handle *h) {
   h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim, ani), stencil_tiles(ga, dim, alpha_rows_per_thread()));
   h->grid_lap = occupancy_grid(h, kernel_lap(c, dim, ani), stencil_tiles(g, dim, alpha_rows_per_thread()));
   int64_t cap = 2 * (int64_t)h->grid_alpha;
-  h->fused_tail = c && h->m >= 3;
+  h->fused_tail = h->m >= 3;
   if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && std::atoi(e) != 0;
   if (h->fused_tail) {
     Geo g2 = g;
     if (const char *e = std::getenv("NLS_KZ_ALPHA2")) h->kz_alpha2 = std::max(1, std::atoi(e));
     g2.kz = h->kz_alpha2;
     h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_rows_per_thread()));
-    const void *ff = kernel_final_fused(dim, h->m, ani);
-    h->grid_fused = occupancy_grid(h, ff, stencil_tiles(g, dim, fused_rows_per_thread()));
+    if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
+    Geo gf = g;
+    if (h->kz_fused) gf.kz = h->kz_fused;
+    for (int mode = 0; mode < 8; ++mode) {
+      const void *ft = kernel_tail(tail_complex(mode), dim, mode, h->m, ani);
+      if (ft) h->tail_grid[mode] = occupancy_grid(h, ft, stencil_tiles(gf, dim, fused_rows_per_thread()));
+    }
   }
   for (int j = 0; j + 1 < h->m; ++j) {
     const void *fu = kernel_update(c, dim, j, ani);
@@ -964,6 +974,29 @@ int nls_apply_bc(nls_handle *h) {
 // G2 (nlsolvers/device/include/nlse_dev.hpp:187-203): N uses +tau/2 m|u|^2
 // and the linear flow is exp(t*lambda) with t = +tau
 // (nlsolvers/device/include/matfunc_complex.hpp:281-287).
+// Does the step end this basis with the fused tail k_tail<mode>?
+bool use_tail(const nls_handle *h, int mode) { return h->fused_tail && h->tail_grid[mode] > 0; }
+
+void tail_launch(nls_handle *h, int mode, TailArgs ta) {
+  Geo g = h->geo;
+  if (h->kz_fused) g.kz = h->kz_fused;
+  void *args[] = {&ta, &g};
+  launch(h, 5, h->m, kernel_tail(tail_complex(mode), (int)h->cfg.dim, mode, h->m, h->ani),
+         h->tail_grid[mode], args);
+}
+
+TailArgs tail_args(nls_handle *h, int b) {
+  TailArgs ta{};
+  ta.W = vec_ptr(h, b, 0);
+  ta.vs = h->vs;
+  ta.st = h->B[b].st;
+  ta.mf = h->mf;
+  ta.nonlin = h->nonlin;
+  ta.s1 = h->s1;
+  ta.s2 = h->s2;
+  return ta;
+}
+
 void ss2_step(nls_handle *h, double dt) {
   const int m = h->m;
   const int64_t n = h->geo.nloc;
@@ -975,16 +1008,17 @@ void ss2_step(nls_handle *h, double dt) {
     pw_launch(h, 3, kernel_nl_init(), args);
     halo(h, 0, 0);
   }
-  const bool tail = h->fused_tail;
+  const bool tail = use_tail(h, TAIL_NLSE);
   if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt, tail);
   else run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt, tail);
   void *W = vec_ptr(h, 0, 0);
   KState *st = h->B[0].st;
   int nl = h->nonlin;
   if (tail) {
-    Geo g = h->geo;
-    void *args[] = {&W, &vs, &g, &st, &h->u, &h->mf, &dt, &nl, &h->s1, &h->s2};
-    launch(h, 5, m, kernel_final_fused((int)h->cfg.dim, m, h->ani), h->grid_fused, args);
+    TailArgs ta = tail_args(h, 0);
+    ta.u = h->u;
+    ta.dt = dt;
+    tail_launch(h, TAIL_NLSE, ta);
   } else {
     void *args[] = {&W, &vs, (void *)&n, &st, &h->u, &h->mf, &dt, &nl, &h->s1, &h->s2};
     pw_launch(h, 3, kernel_final_nlse(m), args);
@@ -1019,22 +1053,39 @@ int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number) {
         pw_launch(h, 3, kernel_sewi_b(), args);
         halo(h, 0, 0);
       }
-      run_lanczos(h, 0, 1, NLS_F_SINC, 0, dt, 0.0);
-      {
+      // each of the three actions may end in a fused tail (k_tail)
+      bool tail = use_tail(h, TAIL_COMBINE_W0);
+      run_lanczos(h, 0, 1, NLS_F_SINC, 0, dt, 0.0, tail);
+      if (tail) {
+        tail_launch(h, TAIL_COMBINE_W0, tail_args(h, 0));
+      } else {
         void *args[] = {&W, &vs, &n, &st};
         pw_launch(h, 3, kernel_combine_w0(m), args);
-        halo(h, 0, 0);
       }
-      run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt);
-      {
+      halo(h, 0, 0);
+      tail = use_tail(h, TAIL_COMBINE);
+      run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt, tail);
+      if (tail) {
+        TailArgs ta = tail_args(h, 0);
+        ta.out = h->scratch;
+        tail_launch(h, TAIL_COMBINE, ta);
+      } else {
         void *args[] = {&W, &vs, &n, &st, &h->scratch};
         pw_launch(h, 3, kernel_combine(true, m), args);
       }
       // exp(2 tau L) u_prev, then u = that - 2 tau e, u_prev <- old u
       hip_check(h, hipMemcpyAsync(W, h->uprev, bytes, hipMemcpyDeviceToDevice, h->stream), "D2D");
       halo(h, 0, 0);
-      run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, 2.0 * dt);
-      {
+      tail = use_tail(h, TAIL_SEWI_END);
+      run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, 2.0 * dt, tail);
+      if (tail) {
+        TailArgs ta = tail_args(h, 0);
+        ta.u = h->u;
+        ta.up = h->uprev;
+        ta.e = h->scratch;
+        ta.dt = dt;
+        tail_launch(h, TAIL_SEWI_END, ta);
+      } else {
         void *args[] = {&W, &vs, &n, &st, &h->u, &h->uprev, &h->scratch, &dt};
         pw_launch(h, 3, kernel_sewi_end(m), args);
       }
@@ -1063,37 +1114,60 @@ void issue_step(nls_handle *h, double dt) {
       pw_launch(h, 3, kernel_kg_g(), args);
       halo(h, 1, 0);
     }
+    // the sinc^2 basis is stored in full; the cos basis may end in the fused tail
+    const bool tail = use_tail(h, TAIL_KG_END);
     run_lanczos(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
-    run_lanczos(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0);
-    {
+    run_lanczos(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0, tail);
+    if (tail) {
+      TailArgs ta = tail_args(h, 0);
+      ta.W2 = vec_ptr(h, 1, 0);
+      ta.st2 = h->B[1].st;
+      ta.up = h->up;
+      ta.v = h->vel;
+      ta.dt = dt;
+      tail_launch(h, TAIL_KG_END, ta);
+    } else {
       void *W = vec_ptr(h, 0, 0);
       void *W2 = vec_ptr(h, 1, 0);
       KState *st = h->B[0].st, *st2 = h->B[1].st;
       void *args[] = {&W, &W2, &vs, (void *)&n, &st, &st2, &h->up, &h->vel, &dt};
       pw_launch(h, 3, kernel_kg_end(m), args);
-      halo(h, 0, 0);
     }
+    halo(h, 0, 0);
     h->vel_valid = true;
   } else {
     // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u
-    run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0);
-    {
+    bool tail = use_tail(h, TAIL_SG_MID);
+    run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0, tail);
+    if (tail) {
+      TailArgs ta = tail_args(h, 0);
+      ta.out = vec_ptr(h, 1, 0);
+      ta.up = h->up;
+      tail_launch(h, TAIL_SG_MID, ta);
+    } else {
       void *W = vec_ptr(h, 0, 0);
       void *g0 = vec_ptr(h, 1, 0);
       KState *st = h->B[0].st;
       void *args[] = {&W, &vs, (void *)&n, &st, &h->mf, &h->up, &g0};
       pw_launch(h, 3, kernel_sg_mid(m), args);
-      halo(h, 1, 0);
     }
-    run_lanczos(h, 1, 1, NLS_F_SINC2_HALF, 0, dt, 0.0);
-    {
+    halo(h, 1, 0);
+    tail = use_tail(h, TAIL_SG_END);
+    run_lanczos(h, 1, 1, NLS_F_SINC2_HALF, 0, dt, 0.0, tail);
+    if (tail) {
+      TailArgs ta = tail_args(h, 1);
+      ta.u = vec_ptr(h, 0, 0);
+      ta.up = h->up;
+      ta.dt = dt;
+      tail_launch(h, TAIL_SG_END, ta);
+    } else {
       void *W2 = vec_ptr(h, 1, 0);
       void *u = vec_ptr(h, 0, 0);
       KState *st = h->B[1].st;
       void *args[] = {&W2, &vs, (void *)&n, &st, &u, &h->up, &dt};
       pw_launch(h, 3, kernel_sg_end(m), args);
-      halo(h, 0, 0);
     }
+    halo(h, 0, 0);
   }
 }
 

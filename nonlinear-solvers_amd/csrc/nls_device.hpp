@@ -22,6 +22,9 @@ __host__ __device__ inline cplx cmul(cplx a, cplx b) {
   return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
 __host__ __device__ inline cplx cconj(cplx a) { return {a.re, -a.im}; }
+// product of two scalars of the same type (real or complex)
+__host__ __device__ inline double smul(double a, double b) { return a * b; }
+__host__ __device__ inline cplx smul(cplx a, cplx b) { return cmul(a, b); }
 
 // conj(a) * b  -- the Lanczos inner product v^H w
 __host__ __device__ inline double cj_mul(double a, double b) { return a * b; }
@@ -78,6 +81,32 @@ struct KState {
   double lam[MMAX];         // Ritz values of the last eigensolve
   int32_t breakdown;        // first j with s_j == 0 (+1), 0 if none
   int32_t pad[3];
+};
+
+// Epilogues of the fused tail pass k_tail (nls_stencil.hpp) and its arguments.
+enum TailMode {
+  TAIL_NLSE = 0,        // u = N(y); W_0 <- N(u)       (k_final_nlse; nlse_solver_dev.hpp:94-111)
+  TAIL_SG_MID = 1,      // g_0 = m (-sin y_id); up <- 2 y_cos - up   (k_sg_mid; sg_solver.hpp:60-71)
+  TAIL_SG_END = 2,      // u <- up + dt^2 y; up <- old u             (k_sg_end; sg_solver.hpp:71-73)
+  TAIL_KG_END = 3,      // Gautschi update with the stored sinc^2 basis W2 (k_kg_end; kg_single.cuh:49-86)
+  TAIL_COMBINE_W0 = 4,  // W_0 <- y                                  (k_combine_w0; sEWI)
+  TAIL_COMBINE = 5,     // out <- y                                  (k_combine; sEWI)
+  TAIL_SEWI_END = 6,    // u <- y - 2 tau e; up <- old u             (k_sewi_end; nlse_dev.hpp:52-63)
+};
+constexpr int tail_nf(int mode) { return mode == TAIL_SG_MID ? 2 : 1; }
+
+struct TailArgs {
+  void *W;              // the tail basis (local plane 0 of W_0)
+  const void *W2;       // KG: the fully stored sinc^2 basis
+  int64_t vs;
+  const KState *st;     // state of the tail basis (coef of the last update, fin)
+  const KState *st2;    // KG: state of W2
+  void *u, *up, *v, *out;
+  const void *e;
+  const double *mf;
+  double dt;
+  int nonlin;
+  cplx s1, s2;
 };
 
 }  // namespace nls

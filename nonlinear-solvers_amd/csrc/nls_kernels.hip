@@ -765,7 +765,9 @@ const void *kernel_lap(bool cplx_, int dim, bool ani) { return table(dim, ani)(N
 const void *kernel_alpha_l2(bool cplx_, int dim, bool ani) {
   return table(dim, ani)(NLS_KIND_ALPHA_L2, cplx_, 0);
 }
-const void *kernel_final_fused(int dim, int M, bool ani) { return table(dim, ani)(NLS_KIND_FINAL, true, M); }
+const void *kernel_tail(bool cplx_, int dim, int mode, int M, bool ani) {
+  return table(dim, ani)(NLS_KIND_FINAL, cplx_, mode * 64 + M);
+}
 
 // local-transport all-reduce: dst[v] = sum_r pub[r][parity][v] in rank order
 __global__ __launch_bounds__(NTHREADS) void k_sum_ranks(cplx *__restrict__ dst, const cplx *__restrict__ pub,

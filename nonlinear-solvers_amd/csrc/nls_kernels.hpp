@@ -23,10 +23,10 @@ int fused_rows_per_thread();
 enum { NLS_KIND_UPDATE = 0, NLS_KIND_ALPHA = 1, NLS_KIND_LAP = 2, NLS_KIND_ALPHA_L2 = 3,
        NLS_KIND_FINAL = 4 };
 //   alpha_l2 : (const S* V, Geo g, cplx* part)  -- 3 partial columns: a, ||V||^2, ||L V||^2
-//   final_fused(M): (cplx* W, int64_t vs, Geo g, const KState*, cplx* u, const double* mf,
-//                    double dt, int nonlin, cplx s1, cplx s2)   -- complex, 3 <= M <= 32
+//   tail(mode, M): (TailArgs a, Geo g)   -- nls_stencil.hpp TailMode, 3 <= M <= 32;
+//                  nullptr where the variant has no such tail (then the unfused path runs)
 const void *kernel_alpha_l2(bool complex_, int dim, bool ani);
-const void *kernel_final_fused(int dim, int M, bool ani);
+const void *kernel_tail(bool complex_, int dim, int mode, int M, bool ani);
 const void *stencil_table_iso2(int kind, bool complex_, int J);
 const void *stencil_table_iso3(int kind, bool complex_, int J);
 const void *stencil_table_ani2(int kind, bool complex_, int J);

@@ -1,5 +1,5 @@
 // nls_stencil.hip -- kernel tables of the stencil passes (k_update<J>, k_alpha,
-// k_lap, k_alpha_l2, k_final_fused) for ONE operator variant and dimension.  The Makefile compiles this
+// k_lap, k_alpha_l2, k_tail) for ONE operator variant and dimension.  The Makefile compiles this
 // file four times (NLS_ANI = 0/1 x NLS_DIM = 2/3) so the ~250 instantiations
 // build in parallel; nls_kernels.hip dispatches between the four tables.
 //   NLS_ANI 0: G1 isotropic operator, f64 (sine-Gordon) and c128 (NLSE)
@@ -24,18 +24,43 @@ template <class S> const void *update_fn(int J) {
     default: return nullptr;
   }
 }
-const void *fused_fn(int M) {
+// tail kernels: J encodes mode * 64 + M.  G1 (iso) tables hold the NLSE and
+// sine-Gordon tails, G2 (ani) tables the NLSE, Klein-Gordon and sEWI tails.
+template <class S, int MODE> const void *tail_m(int M) {
   switch (M) {
-#define X(M) case M: return reinterpret_cast<const void *>(&k_final_fused<NLS_DIM, M, (NLS_ANI != 0)>);
+#define X(M) case M: return reinterpret_cast<const void *>(&k_tail<S, NLS_DIM, M, (NLS_ANI != 0), MODE>);
     NLS_MF_LIST(X)
 #undef X
+    default: return nullptr;
+  }
+}
+const void *tail_fn(bool complex_, int code) {
+  const int mode = code / 64, M = code % 64;
+  if (complex_) {
+    switch (mode) {
+      case TAIL_NLSE: return tail_m<cplx, TAIL_NLSE>(M);
+#if NLS_ANI
+      case TAIL_COMBINE_W0: return tail_m<cplx, TAIL_COMBINE_W0>(M);
+      case TAIL_COMBINE: return tail_m<cplx, TAIL_COMBINE>(M);
+      case TAIL_SEWI_END: return tail_m<cplx, TAIL_SEWI_END>(M);
+#endif
+      default: return nullptr;
+    }
+  }
+  switch (mode) {
+#if NLS_ANI
+    case TAIL_KG_END: return tail_m<double, TAIL_KG_END>(M);
+#else
+    case TAIL_SG_MID: return tail_m<double, TAIL_SG_MID>(M);
+    case TAIL_SG_END: return tail_m<double, TAIL_SG_END>(M);
+#endif
     default: return nullptr;
   }
 }
 template <class S> const void *pick(int kind, int J) {
   switch (kind) {
     case NLS_KIND_ALPHA_L2: return reinterpret_cast<const void *>(&k_alpha_l2<S, NLS_DIM, (NLS_ANI != 0)>);
-    case NLS_KIND_FINAL: return std::is_same<S, cplx>::value ? fused_fn(J) : nullptr;
+    case NLS_KIND_FINAL: return tail_fn(std::is_same<S, cplx>::value, J);
     case NLS_KIND_UPDATE: return update_fn<S>(J);
     case NLS_KIND_ALPHA: return reinterpret_cast<const void *>(&k_alpha<S, NLS_DIM, (NLS_ANI != 0)>);
     case NLS_KIND_LAP: return reinterpret_cast<const void *>(&k_lap<S, NLS_DIM, (NLS_ANI != 0)>);

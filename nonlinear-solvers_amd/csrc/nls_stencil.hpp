@@ -11,6 +11,7 @@
 //        -sum(w), i.e.  (L v)_p = s * sum_{q ~ p} w_pq (v_q - v_p).
 //        c is marched alongside the vector (one extra f64 stream per pass).
 #pragma once
+#include <type_traits>
 #include <utility>
 
 #include "nls_common.hpp"
@@ -286,7 +287,7 @@ constexpr int RB_ALPHA = 4;
 #ifndef NLS_FUSED_RB
 #define NLS_FUSED_RB 1
 #endif
-constexpr int FUSED_RB = NLS_FUSED_RB;  // rows per thread of k_final_fused
+constexpr int FUSED_RB = NLS_FUSED_RB;  // rows per thread of k_tail
 
 // y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
 template <class S, int DIM, bool ANI>
@@ -544,61 +545,129 @@ __global__ __launch_bounds__(NTHREADS) void k_alpha_l2(const S *__restrict__ V, 
   block_store<3>(v, part, gridDim.x, 0);
 }
 
-// Fused tail of an NLSE step (complex, M >= 3): the last Lanczos vector is
-// never stored.  With J = M-2, the pass marches W_J with the stencil and
-// streams W_0..W_{J-1}.  The last vector k_update<J> would have written,
+// Fused tail of a Krylov basis (M >= 3): the last Lanczos vector is never
+// stored.  With J = M-2, the pass marches W_J with the stencil and streams
+// W_0..W_{J-1}.  The last vector k_update<J> would have written,
 //   W_{M-1} = a L W_J - sum_{k<=J} b_k W_k      (a = 1/s_J, b_k = H[J][k]/s_k),
-// enters the final combination  y = sum_{k<M-1} fin_k W_k + fin_{M-1} W_{M-1}
-// (k_final_nlse's value) only linearly, so the pass evaluates
-//   y = (fin_{M-1} a) L W_J + sum_{k<=J} (fin_k - fin_{M-1} b_k) W_k
-// with the M coefficients folded once per workgroup, then u = N(y) and
-// W_0 <- N(u) for the next step, in place (W_0 is read only at the thread's own
-// cell).  Replaces k_update<M-2> + k_final_nlse<M>: M+1 streams instead of 2M+2.
-// The norm s_{M-1} the eigensolve needs comes from the last alpha pass:
-// ||W_{M-1}||^2 = ||L v_J||^2 - sum_k |H[J][k]|^2 (orthonormal basis).
-template <int DIM, int M, bool ANI>
-__global__ __launch_bounds__(NTHREADS) void k_final_fused(cplx *__restrict__ W, int64_t vs, Geo g,
-                                                          const KState *__restrict__ st,
-                                                          cplx *__restrict__ u,
-                                                          const double *__restrict__ mf, double dt,
-                                                          int nonlin, cplx s1, cplx s2) {
+// enters each final combination  y_f = sum_{k<M} fin_f[k] W_k  only linearly, so
+// the pass evaluates
+//   y_f = (fin_f[M-1] a) L W_J + sum_{k<=J} (fin_f[k] - fin_f[M-1] b_k) W_k
+// with the coefficients folded once per workgroup, and hands y_f to the step's
+// epilogue (MODE).  This replaces k_update<M-2> plus the combination kernel of
+// the step: M+1 (NLSE) streams instead of 2M+2.  The norm s_{M-1} the eigensolve
+// needs comes from the last alpha pass, ||W_{M-1}||^2 = ||L v_J||^2 - sum_k
+// |H[J][k]|^2 (orthonormal basis; k_alpha_l2 + k_reduce_iter with ncA = 3).
+// Modes and arguments: TailMode / TailArgs (nls_device.hpp).
+// Writes go to the thread's own cell only; W_0 of the tail basis may be
+// updated in place (it is read only at that cell, the stencil vector is W_J).
+// sin via the register-light reduction of nl_sincos (sine-Gordon's -sin(id u))
+__device__ __forceinline__ double sin_rl(double x) {
+  double sn, cs;
+  nl_sincos(x, sn, cs);
+  return sn;
+}
+
+template <class S, int DIM, int M, bool ANI, int MODE>
+__global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
   static_assert(M >= 3, "the stencil vector must not be W_0 (updated in place)");
   constexpr int J = M - 2;
-  __shared__ cplx cf[MMAX + 1];  // cf[k] for W_k (k <= J), cf[J+1] for L W_J
+  constexpr int NF = tail_nf(MODE);
+  constexpr bool KG = MODE == TAIL_KG_END;
+  constexpr int M2 = KG ? M : 1;
+  __shared__ S cf[NF][MMAX + 1];  // cf[f][k] for W_k (k <= J), cf[f][J+1] for L W_J
+  __shared__ double c2[MMAX];     // KG: combination of the stored basis
+  const KState *__restrict__ st = ta.st;
   if (threadIdx.x <= J + 1) {
-    const cplx fl = st->fin[0][J + 1];
     const int k = threadIdx.x;
-    cf[k] = k <= J ? st->fin[0][k] - cmul(fl, st->coef[k]) : st->coef[J + 1].re * fl;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const cplx fl = st->fin[f][J + 1];
+      const cplx c = k <= J ? st->fin[f][k] - cmul(fl, st->coef[k]) : st->coef[J + 1].re * fl;
+      if constexpr (std::is_same<S, cplx>::value) cf[f][k] = c;
+      else cf[f][k] = c.re;
+    }
+  }
+  if constexpr (KG) {
+    for (int k = threadIdx.x; k < M; k += NTHREADS) c2[k] = ta.st2->fin[0][k].re;
   }
   __syncthreads();
-  const cplx *__restrict__ VJ = W + (int64_t)J * vs;
-  // one row per thread: with the nonlinear steps at the end of the combination,
-  // two rows no longer fit in the 256 registers of two waves per SIMD
+  S *__restrict__ W = static_cast<S *>(ta.W);
+  const double *__restrict__ W2 = static_cast<const double *>(ta.W2);
+  const int64_t vs = ta.vs;
+  const S *__restrict__ VJ = W + (int64_t)J * vs;
+  // one row per thread: with the epilogue at the end of the combination, two
+  // rows no longer fit in the 256 registers of two waves per SIMD
   constexpr int RB = FUSED_RB;
-  march<cplx, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const cplx *cur, const cplx *lap, const bool *ok) {
-    cplx wk[RB][J];
+  march<S, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
+    S wk[RB][J];
+    double w2[RB][M2];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const cplx *__restrict__ src = W + p[r];
+      const S *__restrict__ src = W + p[r];
 #pragma unroll
       for (int k = 0; k < J; ++k) {
-        wk[r][k] = ok[r] ? ld_nt(src) : zero<cplx>();
+        wk[r][k] = ok[r] ? ld_nt(src) : zero<S>();
         src += vs;
+      }
+      if constexpr (KG) {
+        const double *__restrict__ s2 = W2 + p[r];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          w2[r][k] = ok[r] ? ld_nt(s2) : 0.0;
+          s2 += vs;
+        }
       }
     }
     asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
       if (!ok[r]) continue;
-      cplx y = zero<cplx>();
+      S y[NF];
 #pragma unroll
-      for (int k = 0; k < J; ++k) y += cmul(cf[k], wk[r][k]);
-      y += cmul(cf[J], cur[r]);
-      y += cmul(cf[J + 1], lap[r]);
-      const double mv = nonlin == 2 ? mf[p[r]] : 0.0;
-      const cplx un = nl_half(y, mv, dt, nonlin, s1, s2);
-      st_nt(u + p[r], un);
-      st_nt(W + p[r], nl_half(un, mv, dt, nonlin, s1, s2));
+      for (int f = 0; f < NF; ++f) {
+        S acc = zero<S>();
+#pragma unroll
+        for (int k = 0; k < J; ++k) acc = acc + smul(cf[f][k], wk[r][k]);
+        acc = acc + smul(cf[f][J], cur[r]);
+        acc = acc + smul(cf[f][J + 1], lap[r]);
+        y[f] = acc;
+      }
+      const int q = p[r];
+      if constexpr (MODE == TAIL_NLSE) {
+        const double mv = ta.nonlin == 2 ? ta.mf[q] : 0.0;
+        const cplx un = nl_half(to_c(y[0]), mv, ta.dt, ta.nonlin, ta.s1, ta.s2);
+        st_nt(static_cast<cplx *>(ta.u) + q, un);
+        st_nt(reinterpret_cast<cplx *>(W) + q, nl_half(un, mv, ta.dt, ta.nonlin, ta.s1, ta.s2));
+      } else if constexpr (MODE == TAIL_SG_MID) {
+        double *__restrict__ up = static_cast<double *>(ta.up);
+        st_nt(static_cast<double *>(ta.out) + q, ta.mf[q] * (-sin_rl(to_c(y[0]).re)));
+        st_nt(up + q, 2 * to_c(y[1]).re - up[q]);
+      } else if constexpr (MODE == TAIL_SG_END) {
+        double *__restrict__ u = static_cast<double *>(ta.u);
+        double *__restrict__ up = static_cast<double *>(ta.up);
+        const double uo = u[q];
+        u[q] = up[q] + (ta.dt * ta.dt) * to_c(y[0]).re;
+        up[q] = uo;
+      } else if constexpr (MODE == TAIL_KG_END) {
+        double ys = 0.0;
+#pragma unroll
+        for (int k = 0; k < M2; ++k) ys += c2[k] * w2[r][k];
+        double *__restrict__ up = static_cast<double *>(ta.up);
+        const double uo = to_c(wk[r][0]).re;  // u is W_0 of the tail (cos) basis
+        const double un = (to_c(y[0]).re * 2.0 - up[q]) + ys * (ta.dt * ta.dt);
+        reinterpret_cast<double *>(W)[q] = un;
+        up[q] = uo;
+        static_cast<double *>(ta.v)[q] = (un - uo) / ta.dt;
+      } else if constexpr (MODE == TAIL_COMBINE_W0) {
+        reinterpret_cast<cplx *>(W)[q] = to_c(y[0]);
+      } else if constexpr (MODE == TAIL_COMBINE) {
+        static_cast<cplx *>(ta.out)[q] = to_c(y[0]);
+      } else {  // TAIL_SEWI_END
+        cplx *__restrict__ u = static_cast<cplx *>(ta.u);
+        const cplx uo = u[q];
+        u[q] = to_c(y[0]) - cmul({0.0, 2.0 * ta.dt}, static_cast<const cplx *>(ta.e)[q]);
+        static_cast<cplx *>(ta.up)[q] = uo;
+      }
     }
   });
 }
