@@ -360,9 +360,9 @@ def main():
         cnt = fcnt
         avg_ms = tm["class_ms"]["final"] / fcnt
         bytes_launch = ((m + 1) * esz + (8 if w["eq"] == 3 else 0)) * n_local
-        kname = f"k_final_fused<{m}> (stencil + last Lanczos vector + combination + N(1/2) x2, " \
-                f"{m - 1} reads + 2 writes)"
-        kprefix = "k_final_fused<"
+        kname = f"k_tail<NLSE, M={m}> (fused tail: stencil + last Lanczos vector + combination " \
+                f"+ N(1/2) x2, {m - 1} reads + 2 writes)"
+        kprefix = "k_tail<"
     else:  # the largest update pass that ran (m-3 where the basis ends in a fused tail)
         J = max([j for j, c in enumerate(tm["update_count"]) if c] or [0])
         cnt = tm["update_count"][J]

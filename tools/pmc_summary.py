@@ -46,7 +46,7 @@ def main():
             e["l2_hit_rate"] = h / max(h + mi, 1)
         kernels[name] = e
     # dominant kernel: the fused final pass when the step has one, else k_update<m-2>
-    dom = next((k for k in kernels if re.fullmatch(rf"k_final_fused<[23], {m}, (true|false)>", k)), None)
+    dom = next((k for k in kernels if re.fullmatch(rf"k_tail<cplx, [23], {m}, (true|false), 0>", k)), None)
     alg = (m + 1) * esz * cells
     if dom is None:
         dom = next((k for k in kernels if re.fullmatch(rf"k_update<[^,]*, [23], {J}(, (true|false))?>", k)), None)
