@@ -108,6 +108,12 @@ struct nls_handle {
   bool fused_tail = false;
   int grid_alpha2 = 1, kz_alpha2 = 8, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
+  // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
+  // the alpha pass j+1 is skipped (march_q; NLS_FUSED_ALPHA=0 disables)
+  bool fused_alpha = false;
+  int qgrid[MMAX] = {};  // grid of k_update<j, QA>
+  int grid_alpha_cond = 1;  // persistent grid of the conditional alpha pass
+  void *xedge = nullptr;    // x-tile seam values of L W_j (folded alpha, k_xpairs)
   UpdPlan plan[MMAX];
   bool field_set = false, w0_ready = false;
   double w0_dt = 0.0;  // dt the live start vector W_0 = N(u) was built with
@@ -406,32 +412,35 @@ void alpha_pass(nls_handle *h, int b, int j, const Geo &ga) {
   launch(h, 0, j, kernel_alpha(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_alpha, args);
 }
 
-// ncA = 2 after k_alpha, 3 after k_alpha_l2 (fused tail)
-void reduce_iter(nls_handle *h, int b, int j, int ncA = 2) {
+// ncA = 2 after k_alpha, 3 after k_alpha_l2 (fused tail); qa = 1: no alpha pass,
+// alpha_j from the q column of k_update<j-1, QA> (ncA = 0)
+void reduce_iter(nls_handle *h, int b, int j, int ncA = 2, int qa = 0) {
   KState *st = h->B[b].st;
-  int nbA = ncA == 3 ? h->grid_alpha2 : h->grid_alpha, nbU = j >= 1 ? h->plan[j - 1].total : 0;
+  int nbA = qa ? 0 : (ncA == 3 ? h->grid_alpha2 : h->grid_alpha);
+  int nbU = j >= 1 ? (qa ? h->qgrid[j - 1] : h->plan[j - 1].total) : 0;
   const void *fn = kernel_reduce_iter();
-  const int ncols = ncA + (j >= 1 ? j + 1 : 0);
+  const int ncU = j >= 1 ? j + 1 + 3 * qa : 0;
+  const int ncols = ncA + ncU;
   if (nbA > COLSUM_MIN || nbU > COLSUM_MIN) {
-    colsum(h, b, j, h->partA, nbA, ncA, nbU, j >= 1 ? j + 1 : 0);
+    colsum(h, b, j, h->partA, nbA, ncA, nbU, ncU);
     if (h->collective) allreduce_sums(h, b, ncols);
     int ds = 0, dc = 1;
-    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA};
+    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa};
     launch(h, 2, j, fn, 1, args);
     return;
   }
   if (!h->collective) {
     int ds = 1, dc = 1;
-    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA};
+    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa};
     launch(h, 2, j, fn, 1, args);
   } else {
     int ds = 1, dc = 0;
-    void *a1[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA};
+    void *a1[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa};
     launch(h, 2, j, fn, 1, a1);
     allreduce_sums(h, b, ncols);
     ds = 0;
     dc = 1;
-    void *a2[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA};
+    void *a2[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa};
     launch(h, 2, j, fn, 1, a2);
   }
 }
@@ -484,6 +493,7 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   void *W = vec_ptr(h, b, 0);
   int64_t vs = h->vs;
   KState *st = h->B[b].st;
+  bool prev_qa = false;
   for (int j = 0; j + 1 < m; ++j) {
     void *out = vec_ptr(h, b, j + 1);
     if (j >= 1) {
@@ -494,8 +504,52 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
         reduce_final(h, b, nf, f0, f1, tr, ti, 1);
         return;
       }
-      alpha_pass(h, b, j, ga);
-      reduce_iter(h, b, j);
+      if (prev_qa) {
+        reduce_iter(h, b, j, 0, 1);
+        {  // fallback when the folded alpha is ill-conditioned (near breakdown): no-ops otherwise
+          void *vj = vec_ptr(h, b, j);
+          Geo gg = ga;
+          void *a1[] = {&vj, &gg, &h->partA, &st};
+          launch(h, 2, j, kernel_alpha_cond(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_alpha_cond, a1);
+          int nbA = h->grid_alpha_cond, jj = j;
+          void *a2[] = {&st, &h->partA, &nbA, &jj};
+          launch(h, 2, j, kernel_reduce_fix(), 1, a2);
+        }
+        if (std::getenv("NLS_DEBUG_ALPHA")) {  // debug: folded vs directly reduced alpha_j
+          KState hs;
+          hip_check(h, hipStreamSynchronize(h->stream), "sync");
+          hip_check(h, hipMemcpy(&hs, st, sizeof(KState), hipMemcpyDeviceToHost), "d2h");
+          alpha_pass(h, b, j, ga);
+          hip_check(h, hipStreamSynchronize(h->stream), "sync");
+          std::vector<cplx> pa(2 * (size_t)h->grid_alpha);
+          hip_check(h, hipMemcpy(pa.data(), h->partA, pa.size() * sizeof(cplx), hipMemcpyDeviceToHost), "d2h");
+          double a = 0.0;
+          for (int q = 0; q < h->grid_alpha; ++q) a += pa[q].re;
+          std::fprintf(stderr, "[alpha j=%d] folded %.17e direct %.17e rel %.3e\n", j, hs.Td[j],
+                       a / (hs.s[j] * hs.s[j]), std::fabs(hs.Td[j] - a / (hs.s[j] * hs.s[j])) / std::fabs(hs.Td[j]));
+        }
+      } else {
+        alpha_pass(h, b, j, ga);
+        reduce_iter(h, b, j);
+      }
+    }
+    // fold the next alpha into this pass unless the next iteration has none or
+    // is the fused tail's k_alpha_l2
+    const bool qa = h->fused_alpha && j + 2 < m && !(tail && j + 3 == m);
+    prev_qa = qa;
+    if (qa) {
+      const int dim = (int)h->cfg.dim;
+      const void *fq = kernel_update(h->cplx_, dim, j, h->ani, true);
+      int ps = h->qgrid[j], po = 0;
+      void *args[] = {&W, &out, &vs, &g, &st, &h->partU, &ps, &po, &h->xedge};
+      launch(h, 1, j, fq, h->qgrid[j], args);
+      // x-tile seam pairs of q: column j+4 of the pass's partials
+      const int rb = update_rows_per_thread(j, h->ani, true);
+      int ntx = (int)xtiles(g, dim, rb), tw = dim == 3 ? 64 : 64 * rb;
+      cplx *px = h->partU + (int64_t)(j + 4) * ps;
+      void *ax[] = {&h->xedge, &g, &ntx, &tw, &px};
+      launch(h, 2, j, kernel_xpairs(h->cplx_, dim, h->ani), h->qgrid[j], ax);
+      continue;
     }
     const void *fu = kernel_update(h->cplx_, (int)h->cfg.dim, j, h->ani);
     const UpdPlan &pl = h->plan[j];
@@ -505,7 +559,8 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
       gi.qa = pl.qa[i];
       gi.qb = pl.qb[i];
       int ps = pl.total, po = pl.off[i];
-      void *args[] = {&W, &out, &vs, &gi, &st, &h->partU, &ps, &po};
+      void *nul = nullptr;
+      void *args[] = {&W, &out, &vs, &gi, &st, &h->partU, &ps, &po, &nul};
       launch(h, 1, j, fu, pl.grid[i], args);
       if (need_halo && i + 1 == pl.nbnd) halo_begin(h, b, j + 1);
     }
@@ -638,6 +693,25 @@ void alloc_all(nls_handle *h) {
       if (ft) h->tail_grid[mode] = occupancy_grid(h, ft, stencil_tiles(gf, dim, fused_rows_per_thread()));
     }
   }
+  // On by default for large slabs only: each folded pass costs ~0.1-0.3 ms more than
+  // the plain update plus three small launches (seam pairs, conditional fallback),
+  // which the saved alpha pass (0.37 ms at 512^3) outweighs only on large slabs
+  // (measured: 512^3 -6 %, SG 8192^2 -2 % step time; 4096^2 and 256^3 +3-4 %).
+  // NLS_FUSED_ALPHA=1/0 forces it on/off for single-rank handles.
+  h->fused_alpha = !h->collective && g.nloc > (int64_t(1) << 25);
+  if (const char *e = std::getenv("NLS_FUSED_ALPHA")) h->fused_alpha = !h->collective && std::atoi(e) != 0;
+  if (h->fused_alpha) {  // seam buffer for the narrowest x tiles (64 wide)
+    const size_t xe = 2 * (size_t)g.nzl * (size_t)g.nyp * (size_t)xtiles(g, dim, 1) * h->esize;
+    hip_check(h, hipMalloc(&h->xedge, xe), "hipMalloc(xedge)");
+  }
+  if (h->fused_alpha) {  // a persistent grid: the pass is a no-op unless a folded alpha is ill-conditioned
+    const void *fc = kernel_alpha_cond(c, dim, ani);
+    int per_cu = 0, ncu = 0;
+    hip_check(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fc, NTHREADS, 0), "occupancy");
+    hip_check(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev), "attr");
+    h->grid_alpha_cond = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)std::max(per_cu, 1) * ncu,
+                                                                      stencil_tiles(ga, dim, alpha_rows_per_thread())));
+  }
   for (int j = 0; j + 1 < h->m; ++j) {
     const void *fu = kernel_update(c, dim, j, ani);
     UpdPlan &pl = h->plan[j];
@@ -663,8 +737,15 @@ void alloc_all(nls_handle *h) {
       add(0, nzl, false);
     }
     cap = std::max<int64_t>(cap, (int64_t)pl.total * (j + 2));
+    if (h->fused_alpha) {
+      const void *fq = kernel_update(c, dim, j, ani, true);
+      h->qgrid[j] = fq ? occupancy_grid(h, fq, stencil_tiles(g, dim, update_rows_per_thread(j, ani, true))) : 0;
+      if (!fq) h->fused_alpha = false;
+      cap = std::max<int64_t>(cap, (int64_t)h->qgrid[j] * (j + 5));
+    }
   }
-  const size_t na = std::max<size_t>(2 * (size_t)h->grid_alpha, h->fused_tail ? 3 * (size_t)h->grid_alpha2 : 0);
+  const size_t na = std::max<size_t>({2 * (size_t)h->grid_alpha, h->fused_tail ? 3 * (size_t)h->grid_alpha2 : 0,
+                                       h->fused_alpha ? 2 * (size_t)h->grid_alpha_cond : 0});
   hip_check(h, hipMalloc(&h->partA, na * sizeof(cplx)), "hipMalloc(partA)");
   hip_check(h, hipMalloc(&h->partU, (size_t)cap * sizeof(cplx)), "hipMalloc(partU)");
   h->grid_pw = (int)std::max<int64_t>(1, std::min<int64_t>((g.nloc + NTHREADS - 1) / NTHREADS, 8192));
@@ -678,11 +759,12 @@ void free_all(nls_handle *h) {
   }
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
-                  (void *)h->vel,
+                  (void *)h->vel, h->xedge,
                   (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
   h->u = h->scratch = h->snap = h->uprev = nullptr;
   h->up = h->mf = h->cfb = h->vel = nullptr;
+  h->xedge = nullptr;
   h->partA = h->partU = nullptr;
 }
 

@@ -80,7 +80,8 @@ struct KState {
   cplx sums[2 * MMAX + 8];  // reduced sums (written by the sum phase)
   double lam[MMAX];         // Ritz values of the last eigensolve
   int32_t breakdown;        // first j with s_j == 0 (+1), 0 if none
-  int32_t pad[3];
+  int32_t need_alpha;       // folded alpha ill-conditioned: run the (conditional) alpha pass
+  int32_t pad[2];
 };
 
 // Epilogues of the fused tail pass k_tail (nls_stencil.hpp) and its arguments.

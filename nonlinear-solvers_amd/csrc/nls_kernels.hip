@@ -46,7 +46,10 @@ int64_t stencil_tiles(const Geo &g, int dim, int rb) {
   }
   return a * b * c;
 }
-int update_rows_per_thread(int J, bool ani) { return upd_rb(J, ani); }
+int update_rows_per_thread(int J, bool ani, bool qa) {
+  if (!qa) return upd_rb(J, ani);
+  return J >= NLS_QA_RB1_FROM ? 1 : (upd_rb(J, ani) > 2 ? 2 : upd_rb(J, ani));
+}
 int alpha_rows_per_thread() { return RB_ALPHA; }
 int fused_rows_per_thread() { return FUSED_RB; }
 
@@ -83,11 +86,27 @@ __global__ __launch_bounds__(NTHREADS) void k_colsum(const cplx *__restrict__ pa
 }
 const void *kernel_colsum() { return reinterpret_cast<const void *>(&k_colsum); }
 
+// Fallback of a folded alpha (nls_reduce.hpp, need_alpha): after the conditional
+// alpha pass over W_j, redo iteration j's coefficients from the directly reduced
+// a_j = W_j^H L W_j (the U sums of the folded call sit at sums[2..j+2]).
+__global__ __launch_bounds__(NTHREADS) void k_reduce_fix(KState *__restrict__ st,
+                                                         const cplx *__restrict__ partA, int nbA, int j) {
+  if (st->need_alpha == 0) return;  // uniform
+  __shared__ cplx sa[2];
+  sum_partials(partA, nbA, 2, sa);
+  __syncthreads();
+  if (threadIdx.x < 2) st->sums[threadIdx.x] = sa[threadIdx.x];
+  __syncthreads();
+  reduce_iter_body(st, nullptr, 0, nullptr, 0, j, 0, 1, 2, 0);
+}
+const void *kernel_reduce_fix() { return reinterpret_cast<const void *>(&k_reduce_fix); }
+
 __global__ __launch_bounds__(NTHREADS) void k_reduce_iter(KState *__restrict__ st,
                                                           const cplx *__restrict__ partA, int nbA,
                                                           const cplx *__restrict__ partU, int nbU,
-                                                          int j, int do_sum, int do_coef, int ncA) {
-  reduce_iter_body(st, partA, nbA, partU, nbU, j, do_sum, do_coef, ncA);
+                                                          int j, int do_sum, int do_coef, int ncA,
+                                                          int qa) {
+  reduce_iter_body(st, partA, nbA, partU, nbU, j, do_sum, do_coef, ncA, qa);
 }
 
 __device__ __forceinline__ double sinc_ref(double x) {  // eigen_krylov_real.hpp:95-97
@@ -759,9 +778,16 @@ Table table(int dim, bool ani) {
 }
 }  // namespace
 
-const void *kernel_update(bool cplx_, int dim, int J, bool ani) { return table(dim, ani)(NLS_KIND_UPDATE, cplx_, J); }
+const void *kernel_update(bool cplx_, int dim, int J, bool ani, bool qa) {
+  return table(dim, ani)(NLS_KIND_UPDATE, cplx_, (qa ? 64 : 0) + J);
+}
 const void *kernel_alpha(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_ALPHA, cplx_, 0); }
 const void *kernel_lap(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_LAP, cplx_, 0); }
+const void *kernel_xpairs(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_XPAIRS, cplx_, 0); }
+int64_t xtiles(const Geo &g, int dim, int rb) { return dim == 3 ? cdiv(g.nx, 64) : cdiv(g.nx, 64 * (int64_t)rb); }
+const void *kernel_alpha_cond(bool cplx_, int dim, bool ani) {
+  return table(dim, ani)(NLS_KIND_ALPHA_COND, cplx_, 0);
+}
 const void *kernel_alpha_l2(bool cplx_, int dim, bool ani) {
   return table(dim, ani)(NLS_KIND_ALPHA_L2, cplx_, 0);
 }

@@ -7,25 +7,34 @@ namespace nls {
 
 // stencil kernels (tiled march), argument lists:
 //   update : (const S* W, S* out, int64_t vs, Geo g, const KState* st, cplx* part,
-//             int part_stride, int part_off)   -- partials at part[k*stride + off + block]
+//             int part_stride, int part_off, S* E)   -- partials at part[k*stride + off + block];
+//             E: x-seam edge buffer of the QA variant (unused otherwise)
 //   alpha  : (const S* V, Geo g, cplx* part)
 //   lap    : (const S* V, Geo g, S* out)
 // ani = true: the G2 anisotropic operator (complex only; Geo::cf = c field)
-const void *kernel_update(bool complex_, int dim, int J, bool ani);
+const void *kernel_update(bool complex_, int dim, int J, bool ani, bool qa = false);
 const void *kernel_alpha(bool complex_, int dim, bool ani);
 const void *kernel_lap(bool complex_, int dim, bool ani);
 int64_t stencil_tiles(const Geo &g, int dim, int rows_per_thread);
-int update_rows_per_thread(int J, bool ani);
+int update_rows_per_thread(int J, bool ani, bool qa = false);
 int alpha_rows_per_thread();
 int fused_rows_per_thread();
 
 // per-variant tables (nls_stencil.hip, one object per operator x dimension)
 enum { NLS_KIND_UPDATE = 0, NLS_KIND_ALPHA = 1, NLS_KIND_LAP = 2, NLS_KIND_ALPHA_L2 = 3,
-       NLS_KIND_FINAL = 4 };
+       NLS_KIND_FINAL = 4, NLS_KIND_ALPHA_COND = 5, NLS_KIND_XPAIRS = 6 };
+//   xpairs : (const S* E, Geo g, int ntx, int tw, cplx* part) -- x-tile seam pairs of the
+//            folded alpha (one partial column, grid = the QA update pass's grid)
+const void *kernel_xpairs(bool complex_, int dim, bool ani);
+// tiles of a QA update pass along x (3D: 64 wide; 2D: 64 * rows-per-thread wide)
+int64_t xtiles(const Geo &g, int dim, int rows_per_thread);
 //   alpha_l2 : (const S* V, Geo g, cplx* part)  -- 3 partial columns: a, ||V||^2, ||L V||^2
 //   tail(mode, M): (TailArgs a, Geo g)   -- nls_stencil.hpp TailMode, 3 <= M <= 32;
 //                  nullptr where the variant has no such tail (then the unfused path runs)
 const void *kernel_alpha_l2(bool complex_, int dim, bool ani);
+//   alpha_cond : (const S* V, Geo g, cplx* part, const KState* st) -- k_alpha, or nothing
+//                unless st->need_alpha (fallback of the folded alpha)
+const void *kernel_alpha_cond(bool complex_, int dim, bool ani);
 const void *kernel_tail(bool complex_, int dim, int mode, int M, bool ani);
 const void *stencil_table_iso2(int kind, bool complex_, int J);
 const void *stencil_table_iso3(int kind, bool complex_, int J);
@@ -34,10 +43,13 @@ const void *stencil_table_ani3(int kind, bool complex_, int J);
 
 // single workgroup:
 //   reduce_iter  : (KState*, const cplx* partA, int nbA, const cplx* partU, int nbU, int j,
-//                   int do_sum, int do_coef, int ncA)     -- ncA = 3 after k_alpha_l2
+//                   int do_sum, int do_coef, int ncA, int qa)  -- ncA = 3 after k_alpha_l2;
+//                   qa = 1 (ncA = 0): alpha from the q column of the previous update pass
 //   reduce_final : (KState*, const cplx* partU, int nbU, int m, int do_sum, int do_coef,
 //                   int nf, int f0, int f1, double t_re, double t_im, int tail)
 const void *kernel_reduce_iter();
+//   reduce_fix   : (KState*, const cplx* partA, int nbA, int j)   -- no-op unless need_alpha
+const void *kernel_reduce_fix();
 //   sum_ranks    : (cplx* dst, const cplx* pub, int nranks, int parity, int n, int stride)
 const void *kernel_sum_ranks();
 const void *kernel_reduce_final();

@@ -43,14 +43,35 @@ __device__ __forceinline__ double inv_or_zero(double s) { return s > 0.0 ? 1.0 /
 // exact up to rounding of order eps ||L||^2 / s_{j+1}^2; s_{j+1} only enters the
 // last (smallest) coefficient of f(T) e_1, so that error is far below the
 // tolerance of the path.  A non-positive value is a breakdown (column zero).
+//
+// qa = 1 (no alpha pass: ncA = 0; the update pass i = j-1 also reduced
+// q = y^H L y, y = L W_i, and the measured W_i^H L W_i as columns j+1, j+2;
+// k_xpairs the x-tile seam part of q as column j+3).
+// With Y = y / s_i = L v_i, the coefficients c_k = H[i][k] the pass used
+// (W_j = Y - sum_k c_k v_k exactly, up to the kernel's rounding) and the exact
+// projections A(k,l) = v_k^H L v_l -- off-diagonal H entries (Krylov relation +
+// Gram), diagonal the MEASURED Rayleigh quotients T_d (not the alpha used as a
+// coefficient: that one carries the rounding of its own formula, which would
+// otherwise be amplified ~6x per iteration) --
+//   a_j = W_j^H L W_j = Y^H L Y - 2 Re sum_k conj(c_k) B_k + sum_{k,l} conj(c_k) c_l A(k,l),
+//   B_k = v_k^H L Y = sum_{l<=k} conj(H[k][l]) A(l,i) + s_{k+1} (k < i ? A(k+1,i) : conj(H[j][i])),
+//   H[j][i] = v_i^H L v_j = s_j + sum_{l<=i} conj(c_l) G[j][l]       (Krylov relation of L v_i).
+// The measured diagonal also replaces T_d[i] (the reference's alpha is the
+// Rayleigh quotient v^H L v, eigen_krylov_complex.hpp:27-38).
+// Conditioning: the terms are O(||L||^3) while a_j = s_j^2 alpha_j; near a
+// breakdown (s_j -> 0) the cancellation loses everything.  When the sum of the
+// terms' magnitudes exceeds 1e4 s_j^2 (|alpha_i| + s_i + s_j) (relative error of
+// alpha_j ~1e-12 and worse), need_alpha is set: the conditional alpha pass
+// (k_alpha_cond) then reads W_j and k_reduce_fix redoes the coefficients from the
+// directly reduced a_j (the U sums are kept at sums[2..j+2] for that).
 __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__restrict__ partA,
                                         int nbA, const cplx *__restrict__ partU, int nbU, int j,
-                                        int do_sum, int do_coef, int ncA) {
+                                        int do_sum, int do_coef, int ncA, int qa) {
   __shared__ cplx ssum[2 * MMAX + 8];
-  const int ncols = ncA + (j >= 1 ? j + 1 : 0);
+  const int ncols = ncA + (j >= 1 ? j + 1 + 3 * qa : 0);
   if (do_sum) {
-    sum_partials(partA, nbA, ncA, ssum);
-    if (j >= 1) sum_partials(partU, nbU, j + 1, ssum + ncA);
+    if (ncA > 0) sum_partials(partA, nbA, ncA, ssum);
+    if (j >= 1) sum_partials(partU, nbU, j + 1 + 3 * qa, ssum + ncA);
     __syncthreads();
     if (!do_coef) {
       for (int v = threadIdx.x; v < ncols; v += NTHREADS) st->sums[v] = ssum[v];
@@ -79,8 +100,50 @@ __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__r
   __syncthreads();
   for (int k = t; k < j; k += NTHREADS) s_G[k] = (inv_or_zero(s_s[k]) * isj) * ssum[ncA + k];
   if (t == 0) s_G[j] = {sj > 0.0 ? 1.0 : 0.0, 0.0};
+  __shared__ double s_a;  // a_j (qa) -- ssum[0] is a Gram entry when ncA = 0
+  if (qa) {
+    __shared__ double s_term[MMAX];
+    __shared__ double s_tm[MMAX];  // measured diagonal A(l,l), l <= i
+    const int i = j - 1;
+    const double isi = inv_or_zero(s_s[i]);
+    for (int l = t; l < i; l += NTHREADS) s_tm[l] = st->Td[l];
+    if (t == 0) s_tm[i] = ssum[j + 2].re * (isi * isi);
+    __syncthreads();  // s_G, s_tm
+    // A(k,l) = v_k^H L v_l
+    auto A = [&](int k, int l) -> cplx {
+      if (k == l) return {s_tm[k], 0.0};
+      return k < l ? s_H[l][k] : cconj(s_H[k][l]);
+    };
+    for (int k = t; k <= i; k += NTHREADS) {
+      cplx bk = {0.0, 0.0}, row = {0.0, 0.0};
+      for (int l = 0; l <= k; ++l) bk += cmul(cconj(s_H[k][l]), A(l, i));
+      if (k < i) {
+        bk += s_s[k + 1] * A(k + 1, i);
+      } else {
+        cplx hji = {sj, 0.0};  // H[j][i]
+        for (int l = 0; l <= i; ++l) hji += cmul(cconj(s_H[i][l]), s_G[l]);
+        bk += sj * cconj(hji);
+      }
+      for (int l = 0; l <= i; ++l) row += cmul(s_H[i][l], A(k, l));
+      const cplx ck = s_H[i][k];
+      s_term[k] = -2.0 * cj_mul(ck, bk).re + cj_mul(ck, row).re;
+    }
+    __syncthreads();
+    if (t == 0) {
+      const double q = (ssum[j + 1].re + ssum[j + 3].re) * (isi * isi);  // + x-seam pairs
+      double a = q, mag = fabs(q);
+      for (int k = 0; k <= i; ++k) {  // fixed order
+        a += s_term[k];
+        mag += fabs(s_term[k]);
+      }
+      s_a = a;
+      st->Td[i] = s_tm[i];
+      st->need_alpha = (sj > 0.0 && mag > 1e4 * (sj * sj) * (fabs(s_tm[i]) + s_s[i] + sj)) ? 1 : 0;
+    }
+    for (int v = t; v <= j; v += NTHREADS) st->sums[2 + v] = ssum[v];  // for k_reduce_fix
+  }
   __syncthreads();
-  const cplx alpha = (isj * isj) * ssum[0];
+  const cplx alpha = (isj * isj) * (qa ? cplx{s_a, 0.0} : ssum[0]);
   for (int k = t; k <= j; k += NTHREADS) {
     cplx h;
     if (k == j) {

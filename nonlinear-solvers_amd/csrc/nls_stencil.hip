@@ -16,7 +16,17 @@
 namespace nls {
 
 namespace {
-template <class S> const void *update_fn(int J) {
+// J encodes qa * 64 + J (qa: the next alpha folded into the pass, march_q)
+template <class S> const void *update_fn(int code) {
+  const int J = code % 64;
+  if (code >= 64) {
+    switch (J) {
+#define X(J) case J: return reinterpret_cast<const void *>(&k_update<S, NLS_DIM, J, (NLS_ANI != 0), true>);
+      NLS_J_LIST(X)
+#undef X
+      default: return nullptr;
+    }
+  }
   switch (J) {
 #define X(J) case J: return reinterpret_cast<const void *>(&k_update<S, NLS_DIM, J, (NLS_ANI != 0)>);
     NLS_J_LIST(X)
@@ -59,6 +69,8 @@ const void *tail_fn(bool complex_, int code) {
 }
 template <class S> const void *pick(int kind, int J) {
   switch (kind) {
+    case NLS_KIND_XPAIRS: return reinterpret_cast<const void *>(&k_xpairs<S, NLS_DIM, (NLS_ANI != 0)>);
+    case NLS_KIND_ALPHA_COND: return reinterpret_cast<const void *>(&k_alpha_cond<S, NLS_DIM, (NLS_ANI != 0)>);
     case NLS_KIND_ALPHA_L2: return reinterpret_cast<const void *>(&k_alpha_l2<S, NLS_DIM, (NLS_ANI != 0)>);
     case NLS_KIND_FINAL: return tail_fn(std::is_same<S, cplx>::value, J);
     case NLS_KIND_UPDATE: return update_fn<S>(J);

@@ -266,6 +266,8 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
   }
 }
 
+#include "nls_march_q.hpp"
+
 #ifndef NLS_UPD_RB_MODE
 #define NLS_UPD_RB_MODE 1
 #endif
@@ -283,6 +285,12 @@ __host__ __device__ constexpr int upd_rb(int J, bool ani = false) {
                               : (J <= 2 ? 4 : (J <= 6 ? 2 : (J <= 18 ? 2 : 1)));
 }
 template <int J, bool ANI> struct UpdRB { static constexpr int v = upd_rb(J, ANI); };
+#ifndef NLS_QA_RB1_FROM
+#define NLS_QA_RB1_FROM 99  // update passes with the folded alpha: one row per thread from this J (RB = 1 measured slower)
+#endif
+template <int J, bool ANI> struct UpdRBQ {
+  static constexpr int v = J >= NLS_QA_RB1_FROM ? 1 : (upd_rb(J, ANI) > 2 ? 2 : upd_rb(J, ANI));
+};
 constexpr int RB_ALPHA = 4;
 #ifndef NLS_FUSED_RB
 #define NLS_FUSED_RB 1
@@ -463,14 +471,32 @@ __global__ __launch_bounds__(NTHREADS) void k_alpha(const S *__restrict__ V, Geo
   block_store<2>(v, part, gridDim.x, 0);
 }
 
+// k_alpha behind the folded alpha's conditioning flag (nls_reduce.hpp need_alpha):
+// a no-op launch unless the reduction asked for the direct value
+template <class S, int DIM, bool ANI>
+__global__ __launch_bounds__(NTHREADS) void k_alpha_cond(const S *__restrict__ V, Geo g, cplx *__restrict__ part,
+                                                         const KState *__restrict__ st) {
+  if (st->need_alpha == 0) return;  // uniform
+  double a = 0.0, n2 = 0.0;
+  alpha_tiles<S, DIM, RB_ALPHA, ANI>(V, g, a, n2);
+  cplx v[2] = {{a, 0.0}, {n2, 0.0}};
+  block_store<2>(v, part, gridDim.x, 0);
+}
+
 // W_{J+1} = a * L W_J - sum_{k<=J} b_k W_k ;  partials g_k = W_k^H W_{J+1}, ||W_{J+1}||^2
-template <class S, int DIM, int J, bool ANI>
+// QA: also q = (L W_J)^H L (L W_J) (march_q), from which the reduction gets the
+// next alpha (no separate alpha pass over W_{J+1}), and the measured
+// W_J^H L W_J (every cell has W_J and L W_J in registers): partial columns J+2, J+3.
+// QA also stores the x-tile seam values of L W_J in E (see march_q, k_xpairs).
+template <class S, int DIM, int J, bool ANI, bool QA = false>
 __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S *__restrict__ out,
                                                      int64_t vs, Geo g,
                                                      const KState *__restrict__ st,
-                                                     cplx *__restrict__ part, int pstride, int poff) {
+                                                     cplx *__restrict__ part, int pstride, int poff,
+                                                     S *__restrict__ E) {
   constexpr int NA = J + 2;
   S acc[NA];
+  double qacc = 0.0, ameas = 0.0;
 #pragma unroll
   for (int k = 0; k < NA; ++k) acc[k] = zero<S>();
 #if NLS_COEF_LDS
@@ -493,8 +519,8 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
 #define NLS_RELOAD() ((void)0)
 #endif
   const S *__restrict__ VJ = W + (int64_t)J * vs;
-  constexpr int RB = UpdRB<J, ANI>::v;
-  march<S, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
+  constexpr int RB = QA ? UpdRBQ<J, ANI>::v : UpdRB<J, ANI>::v;
+  auto body = [&](const int *p, const S *cur, const S *lap, const bool *ok) {
     // every streamed load of every row first ...
     S wk[RB][J > 0 ? J : 1];
 #pragma unroll
@@ -519,12 +545,19 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
       for (int k = 0; k < J; ++k) acc[k] = acc[k] + cj_mul(wk[r][k], X);
       acc[J] = acc[J] + cj_mul(cur[r], X);
       acc[J + 1] = acc[J + 1] + from_real<S>(abs2(X));
+      if constexpr (QA) ameas += to_c(cj_mul(cur[r], lap[r])).re;
     }
-  });
-  cplx v[NA];
+  };
+  if constexpr (QA) march_q<S, DIM, RB, ANI>(VJ, g, qacc, E, body);
+  else march<S, DIM, RB, true, ANI>(VJ, g, body);
+  cplx v[NA + (QA ? 2 : 0)];
 #pragma unroll
   for (int k = 0; k < NA; ++k) v[k] = to_c(acc[k]);
-  block_store<NA>(v, part, pstride, poff);
+  if constexpr (QA) {
+    v[NA] = {qacc, 0.0};
+    v[NA + 1] = {ameas, 0.0};
+  }
+  block_store<NA + (QA ? 2 : 0)>(v, part, pstride, poff);
 #undef NLS_B
 #undef NLS_RELOAD
 }

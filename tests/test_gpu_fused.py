@@ -89,3 +89,84 @@ def test_fused_tail_large_phase():
     a, _ = _run(2, nx, ny, 1, dx, u0, dt, 3, 10, nls_amd.NLSE_CUBIC, True)
     ref = O.nlse_steps(O.grid(2, nx, ny, 1, dx, dx), u0, dt, 3, 10)
     assert rel_l2(a, ref) <= 1e-10
+
+
+# ---- folded alpha (march_q): update pass j also reduces q = (L W_j)^H L (L W_j) and
+# the alpha pass of W_{j+1} is skipped (NLS_FUSED_ALPHA, read at handle creation)
+
+def _run_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+# shapes with partial x/y/z tiles, two x-tiles (lane-63 gathers), the 3D y-wrap
+# across tiles and more planes than one tile depth (peek planes)
+SHAPES_QA = [(3, 67, 35, 33), (3, 20, 9, 70), (2, 200, 131, 1), (2, 130, 40, 1)]
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", SHAPES_QA)
+@pytest.mark.parametrize("eq", ["cubic", "g2", "sg", "kg"])
+def test_folded_alpha_matches_alpha_pass(dim, nx, ny, nz, eq):
+    n = nx * ny * (nz if dim == 3 else 1)
+    rng = np.random.default_rng(17)
+    dx = 20.0 / (nx - 1)
+    m = {"cubic": 16, "g2": 12, "sg": 10, "kg": 10}[eq]
+    steps = 4
+    c = rng.uniform(0.6, 1.4, n)
+    mf = rng.uniform(0.5, 1.5, n)
+
+    def run():
+        if eq in ("cubic", "g2"):
+            code = nls_amd.NLSE_CUBIC if eq == "cubic" else nls_amd.NLSE_G2
+            u0 = 0.3 * _field(n, 5)
+            with nls_amd.Solver(dim, nx, ny, nz, dx, dx, equation=code, m=m) as s:
+                if eq == "g2":
+                    s.set_coefficients(mf, c)
+                s.set_field(u0)
+                s.set_timing(True)
+                for _ in range(steps):
+                    s.step(1e-3, 1)
+                    if eq == "g2":
+                        s.apply_bc()
+                return s.get_field(), s.timing()
+        u0 = rng.standard_normal(n) * 0.5
+        code = nls_amd.SG_GAUTSCHI if eq == "sg" else nls_amd.KG_GAUTSCHI
+        with nls_amd.Solver(dim, nx, ny, nz, dx, dx, equation=code, m=m) as s:
+            if eq == "kg":
+                s.set_coefficients(mf, c)
+                s.set_sg_state(u0, u0.copy())
+            else:
+                s.set_sg_state(u0, u0.copy(), -np.ones(n))
+            s.set_timing(True)
+            for _ in range(steps):
+                s.step(1e-2, 1)
+                if eq == "kg":
+                    s.apply_bc()
+            return s.get_field(), s.timing()
+
+    rng_state = rng.bit_generator.state
+    a, ta = _run_env({"NLS_FUSED_ALPHA": "1"}, run)
+    rng.bit_generator.state = rng_state
+    b, tb = _run_env({"NLS_FUSED_ALPHA": "0"}, run)
+    assert ta["class_count"]["alpha"] < tb["class_count"]["alpha"]
+    assert np.all(np.isfinite(a))
+    assert rel_l2(a, b) <= 1e-12
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", SHAPES_QA)
+def test_folded_alpha_nlse_matches_oracle(dim, nx, ny, nz):
+    n = nx * ny * (nz if dim == 3 else 1)
+    dx, dt, steps, m = 20.0 / (nx - 1), 1e-3, 5, 16
+    u0 = 0.3 * _field(n, 23)
+    a, ta = _run_env({"NLS_FUSED_ALPHA": "1"},
+                     lambda: _run(dim, nx, ny, nz, dx, u0, dt, steps, m, nls_amd.NLSE_CUBIC, True))
+    ref = O.nlse_steps(O.grid(dim, nx, ny, nz, dx, dx), u0, dt, steps, m)
+    assert rel_l2(a, ref) <= 1e-10
