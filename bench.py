@@ -259,7 +259,18 @@ def load_traffic(workload, m, kernel_prefix):
         return None
 
 
+def _claim_stdout():
+    """The contract's stdout is ONE JSON line, but native libraries print there too
+    (RCCL's version banner at communicator init): route fd 1 to stderr for the run and
+    return a writer on the original stdout for the result line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(saved, "w")
+
+
 def main():
+    out = _claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -414,7 +425,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -114,6 +114,8 @@ struct nls_handle {
   int qgrid[MMAX] = {};  // grid of k_update<j, QA>
   int grid_alpha_cond = 1;  // persistent grid of the conditional alpha pass
   void *xedge = nullptr;    // x-tile seam values of L W_j (folded alpha, k_xpairs)
+  cplx *partX = nullptr;    // k_xpairs partials (xgrid of them)
+  int xgrid = 1024;  // 4 per CU: the seam pairs (~60 MB at 512^3) at full bandwidth, few partials
   UpdPlan plan[MMAX];
   bool field_set = false, w0_ready = false;
   double w0_dt = 0.0;  // dt the live start vector W_0 = N(u) was built with
@@ -419,28 +421,30 @@ void reduce_iter(nls_handle *h, int b, int j, int ncA = 2, int qa = 0) {
   int nbA = qa ? 0 : (ncA == 3 ? h->grid_alpha2 : h->grid_alpha);
   int nbU = j >= 1 ? (qa ? h->qgrid[j - 1] : h->plan[j - 1].total) : 0;
   const void *fn = kernel_reduce_iter();
-  const int ncU = j >= 1 ? j + 1 + 3 * qa : 0;
+  const int ncU = j >= 1 ? j + 1 + 2 * qa : 0;
+  cplx *px = h->partX;
+  int nbX = h->xgrid;
   const int ncols = ncA + ncU;
   if (nbA > COLSUM_MIN || nbU > COLSUM_MIN) {
     colsum(h, b, j, h->partA, nbA, ncA, nbU, ncU);
     if (h->collective) allreduce_sums(h, b, ncols);
     int ds = 0, dc = 1;
-    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa};
+    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa, &px, &nbX};
     launch(h, 2, j, fn, 1, args);
     return;
   }
   if (!h->collective) {
     int ds = 1, dc = 1;
-    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa};
+    void *args[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa, &px, &nbX};
     launch(h, 2, j, fn, 1, args);
   } else {
     int ds = 1, dc = 0;
-    void *a1[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa};
+    void *a1[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa, &px, &nbX};
     launch(h, 2, j, fn, 1, a1);
     allreduce_sums(h, b, ncols);
     ds = 0;
     dc = 1;
-    void *a2[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa};
+    void *a2[] = {&st, &h->partA, &nbA, &h->partU, &nbU, &j, &ds, &dc, &ncA, &qa, &px, &nbX};
     launch(h, 2, j, fn, 1, a2);
   }
 }
@@ -543,12 +547,11 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
       int ps = h->qgrid[j], po = 0;
       void *args[] = {&W, &out, &vs, &g, &st, &h->partU, &ps, &po, &h->xedge};
       launch(h, 1, j, fq, h->qgrid[j], args);
-      // x-tile seam pairs of q: column j+4 of the pass's partials
+      // x-tile seam pairs of q: xgrid partials in partX (summed by the next reduction)
       const int rb = update_rows_per_thread(j, h->ani, true);
       int ntx = (int)xtiles(g, dim, rb), tw = dim == 3 ? 64 : 64 * rb;
-      cplx *px = h->partU + (int64_t)(j + 4) * ps;
-      void *ax[] = {&h->xedge, &g, &ntx, &tw, &px};
-      launch(h, 2, j, kernel_xpairs(h->cplx_, dim, h->ani), h->qgrid[j], ax);
+      void *ax[] = {&h->xedge, &g, &ntx, &tw, &h->partX};
+      launch(h, 2, j, kernel_xpairs(h->cplx_, dim, h->ani), h->xgrid, ax);
       continue;
     }
     const void *fu = kernel_update(h->cplx_, (int)h->cfg.dim, j, h->ani);
@@ -703,6 +706,7 @@ void alloc_all(nls_handle *h) {
   if (h->fused_alpha) {  // seam buffer for the narrowest x tiles (64 wide)
     const size_t xe = 2 * (size_t)g.nzl * (size_t)g.nyp * (size_t)xtiles(g, dim, 1) * h->esize;
     hip_check(h, hipMalloc(&h->xedge, xe), "hipMalloc(xedge)");
+    hip_check(h, hipMalloc(&h->partX, (size_t)h->xgrid * sizeof(cplx)), "hipMalloc(partX)");
   }
   if (h->fused_alpha) {  // a persistent grid: the pass is a no-op unless a folded alpha is ill-conditioned
     const void *fc = kernel_alpha_cond(c, dim, ani);
@@ -741,7 +745,7 @@ void alloc_all(nls_handle *h) {
       const void *fq = kernel_update(c, dim, j, ani, true);
       h->qgrid[j] = fq ? occupancy_grid(h, fq, stencil_tiles(g, dim, update_rows_per_thread(j, ani, true))) : 0;
       if (!fq) h->fused_alpha = false;
-      cap = std::max<int64_t>(cap, (int64_t)h->qgrid[j] * (j + 5));
+      cap = std::max<int64_t>(cap, (int64_t)h->qgrid[j] * (j + 4));
     }
   }
   const size_t na = std::max<size_t>({2 * (size_t)h->grid_alpha, h->fused_tail ? 3 * (size_t)h->grid_alpha2 : 0,
@@ -759,12 +763,13 @@ void free_all(nls_handle *h) {
   }
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
-                  (void *)h->vel, h->xedge,
+                  (void *)h->vel, h->xedge, (void *)h->partX,
                   (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
   h->u = h->scratch = h->snap = h->uprev = nullptr;
   h->up = h->mf = h->cfb = h->vel = nullptr;
   h->xedge = nullptr;
+  h->partX = nullptr;
   h->partA = h->partU = nullptr;
 }
 

@@ -105,8 +105,8 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_iter(KState *__restrict__ s
                                                           const cplx *__restrict__ partA, int nbA,
                                                           const cplx *__restrict__ partU, int nbU,
                                                           int j, int do_sum, int do_coef, int ncA,
-                                                          int qa) {
-  reduce_iter_body(st, partA, nbA, partU, nbU, j, do_sum, do_coef, ncA, qa);
+                                                          int qa, const cplx *__restrict__ partX, int nbX) {
+  reduce_iter_body(st, partA, nbA, partU, nbU, j, do_sum, do_coef, ncA, qa, partX, nbX);
 }
 
 __device__ __forceinline__ double sinc_ref(double x) {  // eigen_krylov_real.hpp:95-97

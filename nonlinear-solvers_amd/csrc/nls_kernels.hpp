@@ -43,7 +43,8 @@ const void *stencil_table_ani3(int kind, bool complex_, int J);
 
 // single workgroup:
 //   reduce_iter  : (KState*, const cplx* partA, int nbA, const cplx* partU, int nbU, int j,
-//                   int do_sum, int do_coef, int ncA, int qa)  -- ncA = 3 after k_alpha_l2;
+//                   int do_sum, int do_coef, int ncA, int qa, const cplx* partX, int nbX)
+//                                                       -- ncA = 3 after k_alpha_l2;
 //                   qa = 1 (ncA = 0): alpha from the q column of the previous update pass
 //   reduce_final : (KState*, const cplx* partU, int nbU, int m, int do_sum, int do_coef,
 //                   int nf, int f0, int f1, double t_re, double t_im, int tail)

@@ -46,7 +46,7 @@ __device__ __forceinline__ double inv_or_zero(double s) { return s > 0.0 ? 1.0 /
 //
 // qa = 1 (no alpha pass: ncA = 0; the update pass i = j-1 also reduced
 // q = y^H L y, y = L W_i, and the measured W_i^H L W_i as columns j+1, j+2;
-// k_xpairs the x-tile seam part of q as column j+3).
+// k_xpairs the x-tile seam part of q as nbX partials in partX, summed here).
 // With Y = y / s_i = L v_i, the coefficients c_k = H[i][k] the pass used
 // (W_j = Y - sum_k c_k v_k exactly, up to the kernel's rounding) and the exact
 // projections A(k,l) = v_k^H L v_l -- off-diagonal H entries (Krylov relation +
@@ -66,12 +66,15 @@ __device__ __forceinline__ double inv_or_zero(double s) { return s > 0.0 ? 1.0 /
 // directly reduced a_j (the U sums are kept at sums[2..j+2] for that).
 __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__restrict__ partA,
                                         int nbA, const cplx *__restrict__ partU, int nbU, int j,
-                                        int do_sum, int do_coef, int ncA, int qa) {
+                                        int do_sum, int do_coef, int ncA, int qa,
+                                        const cplx *__restrict__ partX = nullptr, int nbX = 0) {
   __shared__ cplx ssum[2 * MMAX + 8];
-  const int ncols = ncA + (j >= 1 ? j + 1 + 3 * qa : 0);
+  __shared__ cplx sx;  // x-seam pairs of q (qa)
+  const int ncols = ncA + (j >= 1 ? j + 1 + 2 * qa : 0);
+  if (qa && do_coef) sum_partials(partX, nbX, 1, &sx);  // wave 0
   if (do_sum) {
     if (ncA > 0) sum_partials(partA, nbA, ncA, ssum);
-    if (j >= 1) sum_partials(partU, nbU, j + 1 + 3 * qa, ssum + ncA);
+    if (j >= 1) sum_partials(partU, nbU, j + 1 + 2 * qa, ssum + ncA);
     __syncthreads();
     if (!do_coef) {
       for (int v = threadIdx.x; v < ncols; v += NTHREADS) st->sums[v] = ssum[v];
@@ -130,7 +133,7 @@ __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__r
     }
     __syncthreads();
     if (t == 0) {
-      const double q = (ssum[j + 1].re + ssum[j + 3].re) * (isi * isi);  // + x-seam pairs
+      const double q = (ssum[j + 1].re + sx.re) * (isi * isi);  // + x-seam pairs
       double a = q, mag = fabs(q);
       for (int k = 0; k <= i; ++k) {  // fixed order
         a += s_term[k];
