@@ -94,7 +94,8 @@ struct nls_handle {
   bool kg = false;          // G2 Klein-Gordon Gautschi (real, ani)
   double *vel = nullptr;    // KG velocity v = (u - u_past)/dt of the last step
   bool vel_valid = false;   //   (set by every KG step, before the driver's BC)
-  bool u_slot = false;      // u stored as slot m of basis 0
+  bool u_slot = false;      // u stored as slot nvec[0] of basis 0
+  int nvec[2] = {0, 0};     // vectors stored per basis (m, or m - 1 with a fused tail)
   void *uprev = nullptr;    // G2 sEWI: u of the previous step (nlse_dev.hpp:206-229)
   bool uprev_set = false;
   int64_t u_off = 0;        // extra element offset of that slot
@@ -634,12 +635,56 @@ void setup_geometry(nls_handle *h) {
   h->vs = (g.nzl + 2) * g.P + pad;
 }
 
-bool tail_complex(int mode) {
-  return mode == TAIL_NLSE || mode == TAIL_COMBINE_W0 || mode == TAIL_COMBINE || mode == TAIL_SEWI_END;
+// scalar type of a tail kernel on this handle: the NLSE and sEWI epilogues are
+// complex, the Gautschi ones real, the plain combinations follow the handle
+bool tail_is_cplx(const nls_handle *h, int mode) {
+  if (mode == TAIL_COMBINE || mode == TAIL_COMBINE_W0) return h->cplx_;
+  return mode == TAIL_NLSE || mode == TAIL_SEWI_END;
+}
+
+// the scratch vector (sEWI's e, API outputs) is allocated on first use only
+void ensure_scratch(nls_handle *h) {
+  if (!h->scratch)
+    hip_check(h, hipMalloc(&h->scratch, (size_t)h->geo.nloc * h->esize), "hipMalloc(scratch)");
 }
 
 void alloc_all(nls_handle *h) {
   const Geo &g = h->geo;
+  const bool c = h->cplx_;
+  const int dim = h->cfg.dim;
+  const bool ani = h->ani;
+  // fused tails first: a basis that always ends in one never stores W_{m-1}
+  h->fused_tail = h->m >= 3;
+  if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && std::atoi(e) != 0;
+  if (h->fused_tail) {
+    Geo g2 = g;
+    if (const char *e = std::getenv("NLS_KZ_ALPHA2")) h->kz_alpha2 = std::max(1, std::atoi(e));
+    g2.kz = h->kz_alpha2;
+    h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_rows_per_thread()));
+    if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
+    Geo gf = g;
+    if (h->kz_fused) gf.kz = h->kz_fused;
+    for (int mode = 0; mode < 8; ++mode) {
+      const void *ft = kernel_tail(tail_is_cplx(h, mode), dim, mode, h->m, ani);
+      if (ft) h->tail_grid[mode] = occupancy_grid(h, ft, stencil_tiles(gf, dim, fused_rows_per_thread()));
+    }
+  }
+  // vectors stored per basis: m - 1 where every Lanczos run on it ends in a fused
+  // tail (its k_tail exists for each use), else m.  1024^3 m=16 NLSE: 15 x 17.2 GB.
+  h->nvec[0] = h->nvec[1] = h->m;
+  if (h->fused_tail) {
+    auto has = [&](int mode) { return h->tail_grid[mode] > 0; };
+    if (c) {
+      bool ok = has(TAIL_NLSE) && has(TAIL_COMBINE);
+      if (ani) ok = ok && has(TAIL_COMBINE_W0) && has(TAIL_SEWI_END);
+      if (ok) h->nvec[0] = h->m - 1;
+    } else if (h->kg) {
+      if (has(TAIL_KG_END)) h->nvec[0] = h->m - 1;  // the sinc^2 basis is stored in full
+    } else if (has(TAIL_SG_MID) && has(TAIL_SG_END) && has(TAIL_COMBINE)) {
+      h->nvec[0] = h->nvec[1] = h->m - 1;
+    }
+  }
+
   // NLS_U_SLOT=1 [NLS_U_OFF=k]: keep the NLSE state u in an extra slot after
   // the basis vectors (+k elements) instead of its own allocation.  Measured:
   // no systematic effect; the final pass is bimodal (6.6 / 7.45 ms at 512^3)
@@ -648,7 +693,7 @@ void alloc_all(nls_handle *h) {
   if (const char *e = std::getenv("NLS_U_SLOT")) h->u_slot = h->cplx_ && std::atoi(e) != 0;
   if (const char *e = std::getenv("NLS_U_OFF")) h->u_off = std::max<int64_t>(0, std::atoll(e));
   for (int b = 0; b < h->nbasis; ++b) {
-    const size_t bytes = (size_t)(h->m + (b == 0 && h->u_slot ? 1 : 0)) * h->vs * h->esize +
+    const size_t bytes = (size_t)(h->nvec[b] + (b == 0 && h->u_slot ? 1 : 0)) * h->vs * h->esize +
                          (b == 0 && h->u_slot ? (size_t)h->u_off * h->esize : 0);
     hip_check(h, hipMalloc(&h->B[b].W, bytes), "hipMalloc(basis)");
     hip_check(h, hipMemsetAsync(h->B[b].W, 0, bytes, h->stream), "hipMemset");
@@ -657,7 +702,7 @@ void alloc_all(nls_handle *h) {
   }
   const size_t nbytes = (size_t)g.nloc * h->esize;
   if (h->cplx_) {
-    if (h->u_slot) h->u = vec_ptr(h, 0, h->m) + h->u_off * (int64_t)h->esize;
+    if (h->u_slot) h->u = vec_ptr(h, 0, h->nvec[0]) + h->u_off * (int64_t)h->esize;
     else hip_check(h, hipMalloc(&h->u, nbytes), "hipMalloc(u)");
     if (h->ani) hip_check(h, hipMalloc(&h->mf, (size_t)g.nloc * sizeof(double)), "hipMalloc(m)");
   } else {
@@ -671,31 +716,12 @@ void alloc_all(nls_handle *h) {
     hip_check(h, hipMemsetAsync(h->cfb, 0, cbytes, h->stream), "hipMemset");
     h->geo.cf = h->cfb + g.P;
   }
-  hip_check(h, hipMalloc(&h->scratch, nbytes), "hipMalloc(scratch)");
   // grid sizes from measured occupancy; partial buffers sized for the largest
-  const bool c = h->cplx_;
-  const int dim = h->cfg.dim;
-  const bool ani = h->ani;
   Geo ga = g;
   ga.kz = h->kz_alpha;
   h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim, ani), stencil_tiles(ga, dim, alpha_rows_per_thread()));
   h->grid_lap = occupancy_grid(h, kernel_lap(c, dim, ani), stencil_tiles(g, dim, alpha_rows_per_thread()));
   int64_t cap = 2 * (int64_t)h->grid_alpha;
-  h->fused_tail = h->m >= 3;
-  if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && std::atoi(e) != 0;
-  if (h->fused_tail) {
-    Geo g2 = g;
-    if (const char *e = std::getenv("NLS_KZ_ALPHA2")) h->kz_alpha2 = std::max(1, std::atoi(e));
-    g2.kz = h->kz_alpha2;
-    h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_rows_per_thread()));
-    if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
-    Geo gf = g;
-    if (h->kz_fused) gf.kz = h->kz_fused;
-    for (int mode = 0; mode < 8; ++mode) {
-      const void *ft = kernel_tail(tail_complex(mode), dim, mode, h->m, ani);
-      if (ft) h->tail_grid[mode] = occupancy_grid(h, ft, stencil_tiles(gf, dim, fused_rows_per_thread()));
-    }
-  }
   // On by default for large slabs only: each folded pass costs ~0.1-0.3 ms more than
   // the plain update plus three small launches (seam pairs, conditional fallback),
   // which the saved alpha pass (0.37 ms at 512^3) outweighs only on large slabs
@@ -1068,7 +1094,7 @@ void tail_launch(nls_handle *h, int mode, TailArgs ta) {
   Geo g = h->geo;
   if (h->kz_fused) g.kz = h->kz_fused;
   void *args[] = {&ta, &g};
-  launch(h, 5, h->m, kernel_tail(tail_complex(mode), (int)h->cfg.dim, mode, h->m, h->ani),
+  launch(h, 5, h->m, kernel_tail(tail_is_cplx(h, mode), (int)h->cfg.dim, mode, h->m, h->ani),
          h->tail_grid[mode], args);
 }
 
@@ -1132,6 +1158,7 @@ int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number) {
       ss2_step(h, dt);
     } else {
       if (!h->uprev_set) fail(h, NLS_ERR_STATE, "sEWI step > 1 before step 1 (no u_prev)");
+      ensure_scratch(h);
       void *W = vec_ptr(h, 0, 0);
       KState *st = h->B[0].st;
       // B(u) -> sinc(dt L) B -> exp(tau L) (.) -> e (scratch)
@@ -1405,6 +1432,7 @@ int nls_get_sg_velocity(nls_handle *h, double dt, double *v, uint64_t n) {
       hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
       return;
     }
+    ensure_scratch(h);
     void *u = vec_ptr(h, 0, 0);
     int64_t nn = (int64_t)n;
     void *args[] = {&u, &h->up, &h->scratch, &nn, &dt};
@@ -1423,15 +1451,23 @@ int nls_krylov_apply(nls_handle *h, const double *in, double t_re, double t_im, 
     if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     check_len(h, n);
     const int b = h->cplx_ ? 0 : 1;  // SG: the scratch basis keeps u intact
+    ensure_scratch(h);
     copy_in_vector(h, b, 0, in);
     if (h->cplx_) h->w0_ready = false;
     halo(h, b, 0);
-    run_lanczos(h, b, 1, func, 0, t_re, t_im);
-    void *W = vec_ptr(h, b, 0);
-    int64_t vs = h->vs, nn = (int64_t)n;
-    KState *st = h->B[b].st;
-    void *args[] = {&W, &vs, &nn, &st, &h->scratch};
-    pw_launch(h, 3, kernel_combine(h->cplx_, h->m), args);
+    const bool tail = use_tail(h, TAIL_COMBINE);
+    run_lanczos(h, b, 1, func, 0, t_re, t_im, tail);
+    if (tail) {
+      TailArgs ta = tail_args(h, b);
+      ta.out = h->scratch;
+      tail_launch(h, TAIL_COMBINE, ta);
+    } else {
+      void *W = vec_ptr(h, b, 0);
+      int64_t vs = h->vs, nn = (int64_t)n;
+      KState *st = h->B[b].st;
+      void *args[] = {&W, &vs, &nn, &st, &h->scratch};
+      pw_launch(h, 3, kernel_combine(h->cplx_, h->m), args);
+    }
     hip_check(h, hipMemcpyAsync(out, h->scratch, (size_t)n * h->esize, hipMemcpyDeviceToHost,
                                 h->stream),
               "hipMemcpy D2H");
@@ -1445,6 +1481,7 @@ int nls_laplacian_apply(nls_handle *h, const double *x, double *y, uint64_t n) {
     if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     check_len(h, n);
     const int b = h->cplx_ ? 0 : 1;
+    ensure_scratch(h);
     copy_in_vector(h, b, 0, x);
     if (h->cplx_) h->w0_ready = false;
     halo(h, b, 0);

@@ -46,12 +46,13 @@ template <class S, int MODE> const void *tail_m(int M) {
 }
 const void *tail_fn(bool complex_, int code) {
   const int mode = code / 64, M = code % 64;
+  if (mode == TAIL_COMBINE)  // every variant: nls_krylov_apply on a basis that stores m-1 vectors
+    return complex_ ? tail_m<cplx, TAIL_COMBINE>(M) : tail_m<double, TAIL_COMBINE>(M);
   if (complex_) {
     switch (mode) {
       case TAIL_NLSE: return tail_m<cplx, TAIL_NLSE>(M);
 #if NLS_ANI
       case TAIL_COMBINE_W0: return tail_m<cplx, TAIL_COMBINE_W0>(M);
-      case TAIL_COMBINE: return tail_m<cplx, TAIL_COMBINE>(M);
       case TAIL_SEWI_END: return tail_m<cplx, TAIL_SEWI_END>(M);
 #endif
       default: return nullptr;

@@ -692,9 +692,9 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
         up[q] = uo;
         static_cast<double *>(ta.v)[q] = (un - uo) / ta.dt;
       } else if constexpr (MODE == TAIL_COMBINE_W0) {
-        reinterpret_cast<cplx *>(W)[q] = to_c(y[0]);
+        W[q] = y[0];
       } else if constexpr (MODE == TAIL_COMBINE) {
-        static_cast<cplx *>(ta.out)[q] = to_c(y[0]);
+        static_cast<S *>(ta.out)[q] = y[0];
       } else {  // TAIL_SEWI_END
         cplx *__restrict__ u = static_cast<cplx *>(ta.u);
         const cplx uo = u[q];
