@@ -630,7 +630,10 @@ void setup_geometry(nls_handle *h) {
   if (const char *e = std::getenv("NLS_TILE_REMAP")) g.remap = std::atoi(e) != 0;
   // Pad the vector stride so the m streams of one update pass do not start on
   // the same HBM channel (strides of 2^k * plane bytes camp on one channel).
-  int64_t pad = 256;  // 4 KiB of complex<double>: +15 % on 16-stream passes (tools/bw_probe.hip)
+  // 4096 elements (64 KiB of complex<double>): same-box A/B sweeps (tools/exp_pad3.sh,
+  // exp_pad4.sh) gave 512^3 update passes -5 % (two boxes), 4096^2 +6 % vs the former
+  // 4 KiB pad, within 1 % elsewhere; no pad at all is ~15 % slower (tools/bw_probe.hip)
+  int64_t pad = 4096;
   if (const char *e = std::getenv("NLS_VEC_PAD")) pad = std::max<int64_t>(0, std::atoll(e));
   h->vs = (g.nzl + 2) * g.P + pad;
 }
