@@ -107,7 +107,7 @@ struct nls_handle {
   // fused tail (m >= 3): the last update pass of a basis and the combination
   // that ends the step are one pass, k_tail (NLS_FUSED_TAIL=0 disables)
   bool fused_tail = false;
-  int grid_alpha2 = 1, kz_alpha2 = 8, kz_fused = 0;  // kz_fused 0: geo.kz
+  int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
   // the alpha pass j+1 is skipped (march_q; NLS_FUSED_ALPHA=0 disables)
@@ -663,7 +663,7 @@ void alloc_all(nls_handle *h) {
     Geo g2 = g;
     if (const char *e = std::getenv("NLS_KZ_ALPHA2")) h->kz_alpha2 = std::max(1, std::atoi(e));
     g2.kz = h->kz_alpha2;
-    h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_rows_per_thread()));
+    h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_l2_rows_per_thread()));
     if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
     Geo gf = g;
     if (h->kz_fused) gf.kz = h->kz_fused;

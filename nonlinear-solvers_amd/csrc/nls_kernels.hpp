@@ -19,6 +19,7 @@ int64_t stencil_tiles(const Geo &g, int dim, int rows_per_thread);
 int update_rows_per_thread(int J, bool ani, bool qa = false);
 int alpha_rows_per_thread();
 int fused_rows_per_thread();
+int alpha_l2_rows_per_thread();
 
 // per-variant tables (nls_stencil.hip, one object per operator x dimension)
 enum { NLS_KIND_UPDATE = 0, NLS_KIND_ALPHA = 1, NLS_KIND_LAP = 2, NLS_KIND_ALPHA_L2 = 3,

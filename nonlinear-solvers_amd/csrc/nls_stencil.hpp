@@ -292,6 +292,10 @@ template <int J, bool ANI> struct UpdRBQ {
   static constexpr int v = J >= NLS_QA_RB1_FROM ? 1 : (upd_rb(J, ANI) > 2 ? 2 : upd_rb(J, ANI));
 };
 constexpr int RB_ALPHA = 4;
+#ifndef NLS_RB_L2
+#define NLS_RB_L2 1  // measured at 512^3: RB 1 / kz 32 0.50 ms vs RB 4 / kz 8 0.58 ms (tools/exp_l2.sh)
+#endif
+constexpr int RB_L2 = NLS_RB_L2;  // rows per thread of k_alpha_l2
 #ifndef NLS_FUSED_RB
 #define NLS_FUSED_RB 1
 #endif
@@ -569,7 +573,7 @@ template <class S, int DIM, bool ANI>
 __global__ __launch_bounds__(NTHREADS) void k_alpha_l2(const S *__restrict__ V, Geo g,
                                                        cplx *__restrict__ part) {
   double a = 0.0, n2 = 0.0, l2 = 0.0;
-  march<S, DIM, RB_ALPHA, false, ANI>(V, g, [&](int, const S &c, const S &lap) {
+  march<S, DIM, RB_L2, false, ANI>(V, g, [&](int, const S &c, const S &lap) {
     a += to_c(cj_mul(c, lap)).re;
     n2 += abs2(c);
     l2 += abs2(lap);
