@@ -113,28 +113,31 @@ SHAPES_QA = [(3, 67, 35, 33), (3, 20, 9, 70), (2, 200, 131, 1), (2, 130, 40, 1)]
 
 
 @pytest.mark.parametrize("dim,nx,ny,nz", SHAPES_QA)
-@pytest.mark.parametrize("eq", ["cubic", "g2", "sg", "kg"])
+@pytest.mark.parametrize("eq", ["cubic", "cq", "g2", "sewi", "sg", "kg"])
 def test_folded_alpha_matches_alpha_pass(dim, nx, ny, nz, eq):
     n = nx * ny * (nz if dim == 3 else 1)
     rng = np.random.default_rng(17)
     dx = 20.0 / (nx - 1)
-    m = {"cubic": 16, "g2": 12, "sg": 10, "kg": 10}[eq]
+    m = {"cubic": 16, "cq": 14, "g2": 12, "sewi": 12, "sg": 10, "kg": 10}[eq]
     steps = 4
     c = rng.uniform(0.6, 1.4, n)
     mf = rng.uniform(0.5, 1.5, n)
 
     def run():
-        if eq in ("cubic", "g2"):
-            code = nls_amd.NLSE_CUBIC if eq == "cubic" else nls_amd.NLSE_G2
+        if eq in ("cubic", "cq", "g2", "sewi"):
+            code = {"cubic": nls_amd.NLSE_CUBIC, "cq": nls_amd.NLSE_CQ}.get(eq, nls_amd.NLSE_G2)
             u0 = 0.3 * _field(n, 5)
             with nls_amd.Solver(dim, nx, ny, nz, dx, dx, equation=code, m=m) as s:
-                if eq == "g2":
+                if eq in ("g2", "sewi"):
                     s.set_coefficients(mf, c)
                 s.set_field(u0)
                 s.set_timing(True)
-                for _ in range(steps):
-                    s.step(1e-3, 1)
-                    if eq == "g2":
+                for i in range(1, steps + 1):
+                    if eq == "sewi":
+                        s.step_sewi(1e-3, i)
+                    else:
+                        s.step(1e-3, 1)
+                    if eq in ("g2", "sewi"):
                         s.apply_bc()
                 return s.get_field(), s.timing()
         u0 = rng.standard_normal(n) * 0.5

@@ -1,5 +1,4 @@
 #!/bin/bash
 set -e
 O=gpurun_out/misc; mkdir -p $O
-timeout -k 10 200 python bench.py --n 256 --no-cpu-baseline --steps 10 > $O/b256.json
-NLS_FORCE_RCCL=1 timeout -k 10 200 python bench.py --n 256 --no-cpu-baseline --steps 10 > $O/b256_rccl.json 2>/dev/null
+timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest_all.log 2>&1
