@@ -113,7 +113,6 @@ struct nls_handle {
   // the alpha pass j+1 is skipped (march_q; NLS_FUSED_ALPHA=0 disables)
   bool fused_alpha = false;
   int qgrid[MMAX] = {};  // grid of k_update<j, QA>
-  int grid_alpha_cond = 1;  // persistent grid of the conditional alpha pass
   void *xedge = nullptr;    // x-tile seam values of L W_j (folded alpha, k_xpairs)
   cplx *partX = nullptr;    // k_xpairs partials (xgrid of them)
   int xgrid = 1024;  // 4 per CU: the seam pairs (~60 MB at 512^3) at full bandwidth, few partials
@@ -415,6 +414,23 @@ void alpha_pass(nls_handle *h, int b, int j, const Geo &ga) {
   launch(h, 0, j, kernel_alpha(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_alpha, args);
 }
 
+// After a folded-alpha pass (single-rank handles): one k_reduce_qa launch (after
+// k_colsum for large grids), which also holds the near-breakdown fallback.
+void reduce_qa(nls_handle *h, int b, int j, const Geo &ga) {
+  KState *st = h->B[b].st;
+  int nbU = h->qgrid[j - 1], ncU = j + 3;
+  int ds = 1;
+  if (nbU > COLSUM_MIN) {
+    colsum(h, b, j, h->partA, 0, 0, nbU, ncU);
+    ds = 0;
+  }
+  const void *vj = vec_ptr(h, b, j);
+  Geo gg = ga;
+  int jj = j, nbX = h->xgrid;
+  void *args[] = {&st, &h->partU, &nbU, &jj, &ds, &h->partX, &nbX, (void *)&vj, &gg};
+  launch(h, 2, j, kernel_reduce_qa(h->cplx_, (int)h->cfg.dim, h->ani), 1, args);
+}
+
 // ncA = 2 after k_alpha, 3 after k_alpha_l2 (fused tail); qa = 1: no alpha pass,
 // alpha_j from the q column of k_update<j-1, QA> (ncA = 0)
 void reduce_iter(nls_handle *h, int b, int j, int ncA = 2, int qa = 0) {
@@ -510,16 +526,7 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
         return;
       }
       if (prev_qa) {
-        reduce_iter(h, b, j, 0, 1);
-        {  // fallback when the folded alpha is ill-conditioned (near breakdown): no-ops otherwise
-          void *vj = vec_ptr(h, b, j);
-          Geo gg = ga;
-          void *a1[] = {&vj, &gg, &h->partA, &st};
-          launch(h, 2, j, kernel_alpha_cond(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_alpha_cond, a1);
-          int nbA = h->grid_alpha_cond, jj = j;
-          void *a2[] = {&st, &h->partA, &nbA, &jj};
-          launch(h, 2, j, kernel_reduce_fix(), 1, a2);
-        }
+        reduce_qa(h, b, j, ga);
         if (std::getenv("NLS_DEBUG_ALPHA")) {  // debug: folded vs directly reduced alpha_j
           KState hs;
           hip_check(h, hipStreamSynchronize(h->stream), "sync");
@@ -725,25 +732,18 @@ void alloc_all(nls_handle *h) {
   h->grid_alpha = occupancy_grid(h, kernel_alpha(c, dim, ani), stencil_tiles(ga, dim, alpha_rows_per_thread()));
   h->grid_lap = occupancy_grid(h, kernel_lap(c, dim, ani), stencil_tiles(g, dim, alpha_rows_per_thread()));
   int64_t cap = 2 * (int64_t)h->grid_alpha;
-  // On by default for large slabs only: each folded pass costs ~0.1-0.3 ms more than
-  // the plain update plus three small launches (seam pairs, conditional fallback),
-  // which the saved alpha pass (0.37 ms at 512^3) outweighs only on large slabs
-  // (measured: 512^3 -6 %, SG 8192^2 -2 % step time; 4096^2 and 256^3 +3-4 %).
-  // NLS_FUSED_ALPHA=1/0 forces it on/off for single-rank handles.
-  h->fused_alpha = !h->collective && g.nloc > (int64_t(1) << 25);
+  // On by default where it was measured to pay: each folded pass costs more than the
+  // plain update (3D: halo row + peek plane, 4-14 %) plus the seam-pair launch, against
+  // the alpha pass it removes.  Same-box A/B (tools/exp_qa2.sh): 512^3 +4.5 %, 384^3
+  // +6 %, 2D 4096^2 +2.4 %, SG 8192^2 +1 %, but 3D 256^3 -3 % -> 3D slabs above 32 M
+  // cells, 2D slabs from 16 M.  NLS_FUSED_ALPHA=1/0 forces it on/off (single rank).
+  h->fused_alpha = !h->collective &&
+                   (g.nloc > (int64_t(1) << 25) || (dim == 2 && g.nloc >= (int64_t(1) << 24)));
   if (const char *e = std::getenv("NLS_FUSED_ALPHA")) h->fused_alpha = !h->collective && std::atoi(e) != 0;
   if (h->fused_alpha) {  // seam buffer for the narrowest x tiles (64 wide)
     const size_t xe = 2 * (size_t)g.nzl * (size_t)g.nyp * (size_t)xtiles(g, dim, 1) * h->esize;
     hip_check(h, hipMalloc(&h->xedge, xe), "hipMalloc(xedge)");
     hip_check(h, hipMalloc(&h->partX, (size_t)h->xgrid * sizeof(cplx)), "hipMalloc(partX)");
-  }
-  if (h->fused_alpha) {  // a persistent grid: the pass is a no-op unless a folded alpha is ill-conditioned
-    const void *fc = kernel_alpha_cond(c, dim, ani);
-    int per_cu = 0, ncu = 0;
-    hip_check(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fc, NTHREADS, 0), "occupancy");
-    hip_check(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev), "attr");
-    h->grid_alpha_cond = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)std::max(per_cu, 1) * ncu,
-                                                                      stencil_tiles(ga, dim, alpha_rows_per_thread())));
   }
   for (int j = 0; j + 1 < h->m; ++j) {
     const void *fu = kernel_update(c, dim, j, ani);
@@ -777,8 +777,7 @@ void alloc_all(nls_handle *h) {
       cap = std::max<int64_t>(cap, (int64_t)h->qgrid[j] * (j + 4));
     }
   }
-  const size_t na = std::max<size_t>({2 * (size_t)h->grid_alpha, h->fused_tail ? 3 * (size_t)h->grid_alpha2 : 0,
-                                       h->fused_alpha ? 2 * (size_t)h->grid_alpha_cond : 0});
+  const size_t na = std::max<size_t>(2 * (size_t)h->grid_alpha, h->fused_tail ? 3 * (size_t)h->grid_alpha2 : 0);
   hip_check(h, hipMalloc(&h->partA, na * sizeof(cplx)), "hipMalloc(partA)");
   hip_check(h, hipMalloc(&h->partU, (size_t)cap * sizeof(cplx)), "hipMalloc(partU)");
   h->grid_pw = (int)std::max<int64_t>(1, std::min<int64_t>((g.nloc + NTHREADS - 1) / NTHREADS, 8192));

@@ -87,20 +87,7 @@ __global__ __launch_bounds__(NTHREADS) void k_colsum(const cplx *__restrict__ pa
 }
 const void *kernel_colsum() { return reinterpret_cast<const void *>(&k_colsum); }
 
-// Fallback of a folded alpha (nls_reduce.hpp, need_alpha): after the conditional
-// alpha pass over W_j, redo iteration j's coefficients from the directly reduced
-// a_j = W_j^H L W_j (the U sums of the folded call sit at sums[2..j+2]).
-__global__ __launch_bounds__(NTHREADS) void k_reduce_fix(KState *__restrict__ st,
-                                                         const cplx *__restrict__ partA, int nbA, int j) {
-  if (st->need_alpha == 0) return;  // uniform
-  __shared__ cplx sa[2];
-  sum_partials(partA, nbA, 2, sa);
-  __syncthreads();
-  if (threadIdx.x < 2) st->sums[threadIdx.x] = sa[threadIdx.x];
-  __syncthreads();
-  reduce_iter_body(st, nullptr, 0, nullptr, 0, j, 0, 1, 2, 0);
-}
-const void *kernel_reduce_fix() { return reinterpret_cast<const void *>(&k_reduce_fix); }
+
 
 __global__ __launch_bounds__(NTHREADS) void k_reduce_iter(KState *__restrict__ st,
                                                           const cplx *__restrict__ partA, int nbA,
@@ -786,8 +773,8 @@ const void *kernel_alpha(bool cplx_, int dim, bool ani) { return table(dim, ani)
 const void *kernel_lap(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_LAP, cplx_, 0); }
 const void *kernel_xpairs(bool cplx_, int dim, bool ani) { return table(dim, ani)(NLS_KIND_XPAIRS, cplx_, 0); }
 int64_t xtiles(const Geo &g, int dim, int rb) { return dim == 3 ? cdiv(g.nx, 64) : cdiv(g.nx, 64 * (int64_t)rb); }
-const void *kernel_alpha_cond(bool cplx_, int dim, bool ani) {
-  return table(dim, ani)(NLS_KIND_ALPHA_COND, cplx_, 0);
+const void *kernel_reduce_qa(bool cplx_, int dim, bool ani) {
+  return table(dim, ani)(NLS_KIND_REDUCE_QA, cplx_, 0);
 }
 const void *kernel_alpha_l2(bool cplx_, int dim, bool ani) {
   return table(dim, ani)(NLS_KIND_ALPHA_L2, cplx_, 0);

@@ -23,7 +23,7 @@ int alpha_l2_rows_per_thread();
 
 // per-variant tables (nls_stencil.hip, one object per operator x dimension)
 enum { NLS_KIND_UPDATE = 0, NLS_KIND_ALPHA = 1, NLS_KIND_LAP = 2, NLS_KIND_ALPHA_L2 = 3,
-       NLS_KIND_FINAL = 4, NLS_KIND_ALPHA_COND = 5, NLS_KIND_XPAIRS = 6 };
+       NLS_KIND_FINAL = 4, NLS_KIND_REDUCE_QA = 5, NLS_KIND_XPAIRS = 6 };
 //   xpairs : (const S* E, Geo g, int ntx, int tw, cplx* part) -- x-tile seam pairs of the
 //            folded alpha (one partial column, grid = the QA update pass's grid)
 const void *kernel_xpairs(bool complex_, int dim, bool ani);
@@ -33,9 +33,10 @@ int64_t xtiles(const Geo &g, int dim, int rows_per_thread);
 //   tail(mode, M): (TailArgs a, Geo g)   -- nls_stencil.hpp TailMode, 3 <= M <= 32;
 //                  nullptr where the variant has no such tail (then the unfused path runs)
 const void *kernel_alpha_l2(bool complex_, int dim, bool ani);
-//   alpha_cond : (const S* V, Geo g, cplx* part, const KState* st) -- k_alpha, or nothing
-//                unless st->need_alpha (fallback of the folded alpha)
-const void *kernel_alpha_cond(bool complex_, int dim, bool ani);
+//   reduce_qa  : (KState*, const cplx* partU, int nbU, int j, int do_sum, const cplx* partX,
+//                 int nbX, const S* W_j, Geo ga) -- single workgroup: the reduction after a
+//                 folded-alpha pass, with the direct alpha of W_j as fallback (need_alpha)
+const void *kernel_reduce_qa(bool complex_, int dim, bool ani);
 const void *kernel_tail(bool complex_, int dim, int mode, int M, bool ani);
 const void *stencil_table_iso2(int kind, bool complex_, int J);
 const void *stencil_table_iso3(int kind, bool complex_, int J);
@@ -50,8 +51,7 @@ const void *stencil_table_ani3(int kind, bool complex_, int J);
 //   reduce_final : (KState*, const cplx* partU, int nbU, int m, int do_sum, int do_coef,
 //                   int nf, int f0, int f1, double t_re, double t_im, int tail)
 const void *kernel_reduce_iter();
-//   reduce_fix   : (KState*, const cplx* partA, int nbA, int j)   -- no-op unless need_alpha
-const void *kernel_reduce_fix();
+
 //   sum_ranks    : (cplx* dst, const cplx* pub, int nranks, int parity, int n, int stride)
 const void *kernel_sum_ranks();
 const void *kernel_reduce_final();

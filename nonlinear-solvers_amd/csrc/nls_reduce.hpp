@@ -62,8 +62,8 @@ __device__ __forceinline__ double inv_or_zero(double s) { return s > 0.0 ? 1.0 /
 // breakdown (s_j -> 0) the cancellation loses everything.  When the sum of the
 // terms' magnitudes exceeds 1e4 s_j^2 (|alpha_i| + s_i + s_j) (relative error of
 // alpha_j ~1e-12 and worse), need_alpha is set: the conditional alpha pass
-// (k_alpha_cond) then reads W_j and k_reduce_fix redoes the coefficients from the
-// directly reduced a_j (the U sums are kept at sums[2..j+2] for that).
+// (k_reduce_qa, the kernel around this body) then reduces a_j directly from W_j and
+// redoes the coefficients (the U sums are kept at sums[2..j+2] for that).
 __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__restrict__ partA,
                                         int nbA, const cplx *__restrict__ partU, int nbU, int j,
                                         int do_sum, int do_coef, int ncA, int qa,
@@ -143,7 +143,7 @@ __device__ inline void reduce_iter_body(KState *__restrict__ st, const cplx *__r
       st->Td[i] = s_tm[i];
       st->need_alpha = (sj > 0.0 && mag > 1e4 * (sj * sj) * (fabs(s_tm[i]) + s_s[i] + sj)) ? 1 : 0;
     }
-    for (int v = t; v <= j; v += NTHREADS) st->sums[2 + v] = ssum[v];  // for k_reduce_fix
+    for (int v = t; v <= j; v += NTHREADS) st->sums[2 + v] = ssum[v];  // for the fallback
   }
   __syncthreads();
   const cplx alpha = (isj * isj) * (qa ? cplx{s_a, 0.0} : ssum[0]);

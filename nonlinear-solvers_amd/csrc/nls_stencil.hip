@@ -4,6 +4,7 @@
 // build in parallel; nls_kernels.hip dispatches between the four tables.
 //   NLS_ANI 0: G1 isotropic operator, f64 (sine-Gordon) and c128 (NLSE)
 //   NLS_ANI 1: G2 anisotropic div(c grad) operator, c128 (NLSE) and f64 (Klein-Gordon)
+#include "nls_reduce.hpp"
 #include "nls_stencil.hpp"
 #include "nls_kernels.hpp"
 
@@ -71,7 +72,7 @@ const void *tail_fn(bool complex_, int code) {
 template <class S> const void *pick(int kind, int J) {
   switch (kind) {
     case NLS_KIND_XPAIRS: return reinterpret_cast<const void *>(&k_xpairs<S, NLS_DIM, (NLS_ANI != 0)>);
-    case NLS_KIND_ALPHA_COND: return reinterpret_cast<const void *>(&k_alpha_cond<S, NLS_DIM, (NLS_ANI != 0)>);
+    case NLS_KIND_REDUCE_QA: return reinterpret_cast<const void *>(&k_reduce_qa<S, NLS_DIM, (NLS_ANI != 0)>);
     case NLS_KIND_ALPHA_L2: return reinterpret_cast<const void *>(&k_alpha_l2<S, NLS_DIM, (NLS_ANI != 0)>);
     case NLS_KIND_FINAL: return tail_fn(std::is_same<S, cplx>::value, J);
     case NLS_KIND_UPDATE: return update_fn<S>(J);

@@ -475,16 +475,40 @@ __global__ __launch_bounds__(NTHREADS) void k_alpha(const S *__restrict__ V, Geo
   block_store<2>(v, part, gridDim.x, 0);
 }
 
-// k_alpha behind the folded alpha's conditioning flag (nls_reduce.hpp need_alpha):
-// a no-op launch unless the reduction asked for the direct value
+// The reduction after a folded-alpha update pass (k_reduce_iter with qa = 1), with
+// its own fallback: when the folded alpha is ill-conditioned (need_alpha, near a
+// breakdown) this one workgroup reduces W_j^H L W_j itself (alpha_tiles over every
+// tile of the slab: slow, but only near a breakdown) and redoes the coefficients
+// from the direct value -- no extra launches in the common case.
 template <class S, int DIM, bool ANI>
-__global__ __launch_bounds__(NTHREADS) void k_alpha_cond(const S *__restrict__ V, Geo g, cplx *__restrict__ part,
-                                                         const KState *__restrict__ st) {
-  if (st->need_alpha == 0) return;  // uniform
+__global__ __launch_bounds__(NTHREADS) void k_reduce_qa(KState *__restrict__ st, const cplx *__restrict__ partU,
+                                                        int nbU, int j, int do_sum,
+                                                        const cplx *__restrict__ partX, int nbX,
+                                                        const S *__restrict__ Wj, Geo ga) {
+  reduce_iter_body(st, nullptr, 0, partU, nbU, j, do_sum, 1, 0, 1, partX, nbX);
+  __syncthreads();
+  if (st->need_alpha == 0) return;  // uniform (thread 0's global write, after the barrier)
   double a = 0.0, n2 = 0.0;
-  alpha_tiles<S, DIM, RB_ALPHA, ANI>(V, g, a, n2);
-  cplx v[2] = {{a, 0.0}, {n2, 0.0}};
-  block_store<2>(v, part, gridDim.x, 0);
+  alpha_tiles<S, DIM, RB_ALPHA, ANI>(Wj, ga, a, n2);
+  __shared__ double ra[NTHREADS / 64], rn[NTHREADS / 64];
+  a = wave_sum(a);
+  n2 = wave_sum(n2);
+  if ((threadIdx.x & 63) == 0) {
+    ra[threadIdx.x >> 6] = a;
+    rn[threadIdx.x >> 6] = n2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sa = ra[0], sn = rn[0];
+    for (int w = 1; w < NTHREADS / 64; ++w) {
+      sa += ra[w];
+      sn += rn[w];
+    }
+    st->sums[0] = {sa, 0.0};
+    st->sums[1] = {sn, 0.0};
+  }
+  __syncthreads();
+  reduce_iter_body(st, nullptr, 0, nullptr, 0, j, 0, 1, 2, 0);
 }
 
 // W_{J+1} = a * L W_J - sum_{k<=J} b_k W_k ;  partials g_k = W_k^H W_{J+1}, ||W_{J+1}||^2

@@ -24,6 +24,16 @@ from conftest import rel_l2
 pytestmark = pytest.mark.gpu
 nls_amd = pytest.importorskip("nls_amd")
 
+
+@pytest.fixture(autouse=True, params=["default", "folded"])
+def _alpha_mode(request, monkeypatch):
+    """Every edge case twice: the default sequence, and with the folded alpha forced
+    on (NLS_FUSED_ALPHA=1), whose near-breakdown fallback (k_reduce_qa) these cases
+    reach; the variable is read when a handle is created."""
+    if request.param == "folded":
+        monkeypatch.setenv("NLS_FUSED_ALPHA", "1")
+    yield
+
 TOL = 1e-10
 
 
