@@ -35,12 +35,16 @@ __device__ __forceinline__ double qpair(const Geo &g, const S &a, const S &b, do
   else return 2.0 * g.s * to_c(cj_mul(a, b)).re;
 }
 
-// Edge buffer layout: E[side][q][y][t], side 0 = the first x of x-tile t (lane 0 of
+// Edge buffer layout: E[side][t][y][q], side 0 = the first x of x-tile t (lane 0 of
 // chunk 0), side 1 = its last x (lane 63 of the last chunk); y = row (3D) or 0 (2D).
+// A wave stages its seam values for the planes of a tile in LDS and writes them at
+// the end of the tile as runs along q (single-lane 16-B stores per plane went to
+// HBM as partial-line writes: +2.5 ms per 512^3 step).
 __host__ __device__ inline int64_t xedge_index(const Geo &g, int64_t ntx, int side, int64_t q, int64_t y,
                                                int64_t t) {
-  return ((side * g.nzl + q) * g.nyp + y) * ntx + t;
+  return ((side * ntx + t) * g.nyp + y) * g.nzl + q;
 }
+constexpr int SEAM_KZ = 64;  // planes per tile the LDS seam staging holds (else direct stores)
 
 template <class S, int DIM, int RB, bool ANI, class Fn>
 __device__ __forceinline__ void march_q(const S *__restrict__ V, const Geo &g, double &qacc,
@@ -86,7 +90,14 @@ __device__ __forceinline__ void march_q(const S *__restrict__ V, const Geo &g, d
           ccur[r] = ld ? C[q0 * P + off[r]] : 0.0;
         }
       }
-      // halo row: the flat row after the last valid row (y-wrap: row 0 of plane q+1)
+      // halo row: the flat row after the last valid row (y-wrap: row 0 of plane q+1).
+      // In tiles whose 4*RB rows are all valid, waves 0..2 take L V of their halo row
+      // (the next wave's first row) from LDS; only wave 3 marches its own halo row.
+      const bool shy = (jt + 1) * (4 * RB) <= nyp;  // workgroup-uniform
+      const bool own_halo = !shy || w == 3;         // wave-uniform
+      __shared__ S hls[2][4][64];
+      __shared__ S seam[4][2][RB][SEAM_KZ];  // per wave: [side][row][plane - q0]
+      const bool stage = q1 - q0 <= SEAM_KZ;
       const int yl = yb + rlast;
       const int hw = yl + 1 >= nyp ? 1 : 0;
       const int hy = hw ? 0 : yl + 1;
@@ -95,11 +106,12 @@ __device__ __forceinline__ void march_q(const S *__restrict__ V, const Geo &g, d
       double chprv = 0.0, chcur = 0.0;
       {
         const int hq = q0 + hw;
-        hprv = (xin && z0 + hq - 1 >= 0 && z0 + hq - 1 < npl) ? V[(hq - 1) * P + hoff] : zero<S>();
-        hcur = (xin && z0 + hq < npl) ? V[hq * P + hoff] : zero<S>();
+        const bool hl = own_halo && xin;
+        hprv = (hl && z0 + hq - 1 >= 0 && z0 + hq - 1 < npl) ? V[(hq - 1) * P + hoff] : zero<S>();
+        hcur = (hl && z0 + hq < npl) ? V[hq * P + hoff] : zero<S>();
         if constexpr (ANI) {
-          chprv = (xin && z0 + hq - 1 >= 0 && z0 + hq - 1 < npl) ? C[(hq - 1) * P + hoff] : 0.0;
-          chcur = (xin && z0 + hq < npl) ? C[hq * P + hoff] : 0.0;
+          chprv = (hl && z0 + hq - 1 >= 0 && z0 + hq - 1 < npl) ? C[(hq - 1) * P + hoff] : 0.0;
+          chcur = (hl && z0 + hq < npl) ? C[hq * P + hoff] : 0.0;
         }
       }
       const bool bx = (x == 0) || (x == nx - 1);
@@ -177,48 +189,52 @@ __device__ __forceinline__ void march_q(const S *__restrict__ V, const Geo &g, d
         if (!peek) {
           fn(pv, cur, lapv, okv);
           // L V on the halo row (its y-1 neighbour is the last row; flat p + nx wraps)
-#ifdef NLS_QA_NOHALO  // timing experiment only: q is wrong
-          const int hq = -1000000;
-#else
-          const int hq = q + hw;  // local plane of the halo cell
-#endif
-          const int ghq = z0 + hq;
-          const bool hexists = ghq < npl;
-          const bool hnext_ok = ghq + 1 < npl;
-          S hnext = (xin && hnext_ok) ? V[(hq + 1) * P + hoff] : zero<S>();
-          double chnext = 0.0;
-          if constexpr (ANI) chnext = (xin && hnext_ok) ? C[(hq + 1) * P + hoff] : 0.0;
-          const int ph = hq * P + hoff;
-          const bool heyp = ghq < npl - 1 || hy < nyp - 1;
-          const S hyp = (xin && hexists && heyp) ? V[ph + nx] : zero<S>();
-          S hxm = shfl_up1(hcur), hxp = shfl_dn1(hcur);
-          const bool hedge = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin && hexists;
-          const S hxe = hedge ? V[ph + (lane == 0 ? -1 : 1)] : zero<S>();
-          if (lane == 0) hxm = hxe;
-          if (lane == 63) hxp = hxe;
-          if (!(x > 0)) hxm = zero<S>();
-          if (!(x + 1 < nx)) hxp = zero<S>();
-          S hlap;
+          S hlap = zero<S>();
           double wyl = 0.0;  // ani weight of the (last row, halo) pair
-          if constexpr (ANI) {
-            const double cc = chcur;
-            const double cym = ccur[rlast];
-            const double cyp = (xin && hexists && heyp) ? C[ph + nx] : 0.0;
-            double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
-            const double cxe = hedge ? C[ph + (lane == 0 ? -1 : 1)] : 0.0;
-            if (lane == 0) cxm = cxe;
-            if (lane == 63) cxp = cxe;
-            const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
-            const double wym = face_w(true, cc, cym), wyp = face_w(heyp, cc, cyp);
-            const double wzm = face_w(ghq > 0, cc, chprv), wzp = face_w(hnext_ok, cc, chnext);
-            hlap = g.s * ((((wzm * hprv + wzp * hnext) + (wxm * hxm + wxp * hxp)) +
-                           (wym * cur[rlast] + wyp * hyp)) -
-                          (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * hcur);
-            wyl = wypv[rlast];
-          } else {
-            const bool hbnd = bx || ghq == 0 || ghq == npl - 1 || hy == 0 || hy == nyp - 1;
-            hlap = g.s * (((hprv + hnext) + (hxm + hxp)) + (cur[rlast] + hyp)) +
-                   (hbnd ? g.sd_bd : g.sd_in) * hcur;
+          if constexpr (ANI) wyl = wypv[rlast];
+          S hnext = zero<S>();
+          double chnext = 0.0;
+          if (shy) {  // publish this wave's first row, take the next wave's
+            hls[q & 1][w][lane] = lapv[0];
+            __syncthreads();
+            if (w < 3) hlap = hls[q & 1][w + 1][lane];
+          }
+          if (own_halo) {
+            const int hq = q + hw;  // local plane of the halo cell
+            const int ghq = z0 + hq;
+            const bool hexists = ghq < npl;
+            const bool hnext_ok = ghq + 1 < npl;
+            hnext = (xin && hnext_ok) ? V[(hq + 1) * P + hoff] : zero<S>();
+            if constexpr (ANI) chnext = (xin && hnext_ok) ? C[(hq + 1) * P + hoff] : 0.0;
+            const int ph = hq * P + hoff;
+            const bool heyp = ghq < npl - 1 || hy < nyp - 1;
+            const S hyp = (xin && hexists && heyp) ? V[ph + nx] : zero<S>();
+            S hxm = shfl_up1(hcur), hxp = shfl_dn1(hcur);
+            const bool hedge = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin && hexists;
+            const S hxe = hedge ? V[ph + (lane == 0 ? -1 : 1)] : zero<S>();
+            if (lane == 0) hxm = hxe;
+            if (lane == 63) hxp = hxe;
+            if (!(x > 0)) hxm = zero<S>();
+            if (!(x + 1 < nx)) hxp = zero<S>();
+            if constexpr (ANI) {
+              const double cc = chcur;
+              const double cym = ccur[rlast];
+              const double cyp = (xin && hexists && heyp) ? C[ph + nx] : 0.0;
+              double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
+              const double cxe = hedge ? C[ph + (lane == 0 ? -1 : 1)] : 0.0;
+              if (lane == 0) cxm = cxe;
+              if (lane == 63) cxp = cxe;
+              const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
+              const double wym = face_w(true, cc, cym), wyp = face_w(heyp, cc, cyp);
+              const double wzm = face_w(ghq > 0, cc, chprv), wzp = face_w(hnext_ok, cc, chnext);
+              hlap = g.s * ((((wzm * hprv + wzp * hnext) + (wxm * hxm + wxp * hxp)) +
+                             (wym * cur[rlast] + wyp * hyp)) -
+                            (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * hcur);
+            } else {
+              const bool hbnd = bx || ghq == 0 || ghq == npl - 1 || hy == 0 || hy == nyp - 1;
+              hlap = g.s * (((hprv + hnext) + (hxm + hxp)) + (cur[rlast] + hyp)) +
+                     (hbnd ? g.sd_bd : g.sd_in) * hcur;
+            }
           }
           // forward pairs of plane q: x+1 (inside the tile) and y+1
 #pragma unroll
@@ -233,8 +249,11 @@ __device__ __forceinline__ void march_q(const S *__restrict__ V, const Geo &g, d
             }
             if (x + 1 < nx && lane != 63) acc += qpair<S, ANI>(g, yv, yx, wxpv[r]);
             // x-tile seam: the pair (lane 63, next tile's lane 0) is added by k_xpairs
-            if (lane == 0) E[xedge_index(g, ntx, 0, q, yb + r, it)] = yv;
-            if (lane == 63) E[xedge_index(g, ntx, 1, q, yb + r, it)] = yv;
+            if (lane == 0 || lane == 63) {
+              const int side = lane == 0 ? 0 : 1;
+              if (stage) seam[w][side][r][q - q0] = yv;
+              else E[xedge_index(g, ntx, side, q, yb + r, it)] = yv;
+            }
             if (r < rlast) acc += qpair<S, ANI>(g, yv, lapv[r + 1 < RB ? r + 1 : r], wypv[r]);
             else if (exv[r]) acc += qpair<S, ANI>(g, yv, hlap, wyl);
             qacc += acc;
@@ -263,10 +282,24 @@ __device__ __forceinline__ void march_q(const S *__restrict__ V, const Geo &g, d
           }
         }
       }
+      if (stage) {  // the tile's seam values, one run along q per side and row
+        __builtin_amdgcn_wave_barrier();
+        for (int i = lane; i < q1 - q0; i += 64) {
+#pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            if (!rv[r]) continue;
+            E[xedge_index(g, ntx, 0, q0 + i, yb + r, it)] = seam[w][0][r][i];
+            if (it * 64 + 63 < nx) E[xedge_index(g, ntx, 1, q0 + i, yb + r, it)] = seam[w][1][r][i];
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
     } else {
       const int q0 = qa + (kt * 4 + w) * kz;
       if (q0 >= qb) continue;  // wave-uniform
       const int q1 = q0 + kz < qb ? q0 + kz : qb;
+      __shared__ S seam2[4][2][SEAM_KZ];  // per wave: [side][row - q0]
+      const bool stage = q1 - q0 <= SEAM_KZ;
       int xr[RB];
       S prev[RB], cur[RB], lprev[RB];
       double cprv[RB], ccur[RB];
@@ -354,8 +387,11 @@ __device__ __forceinline__ void march_q(const S *__restrict__ V, const Geo &g, d
             if (x + 1 < nx && !(lane == 63 && r + 1 == RB))
               acc += qpair<S, ANI>(g, yv, lane == 63 ? ys : yx, wxpv[r]);
             // x-tile seam: the pair (last chunk's lane 63, next tile's lane 0) -> k_xpairs
-            if (lane == 0 && r == 0) E[xedge_index(g, ntx, 0, q, 0, it)] = yv;
-            if (lane == 63 && r + 1 == RB) E[xedge_index(g, ntx, 1, q, 0, it)] = yv;
+            if ((lane == 0 && r == 0) || (lane == 63 && r + 1 == RB)) {
+              const int side = lane == 0 ? 0 : 1;
+              if (stage) seam2[w][side][q - q0] = yv;
+              else E[xedge_index(g, ntx, side, q, 0, it)] = yv;
+            }
             qacc += acc;
           }
         }
@@ -376,6 +412,15 @@ __device__ __forceinline__ void march_q(const S *__restrict__ V, const Geo &g, d
           }
         }
       }
+      if (stage) {  // the tile's seam values as runs along q
+        __builtin_amdgcn_wave_barrier();
+        const bool rgt = it * 64 * RB + 64 * RB - 1 < nx;
+        for (int i = lane; i < q1 - q0; i += 64) {
+          E[xedge_index(g, ntx, 0, q0 + i, 0, it)] = seam2[w][0][i];
+          if (rgt) E[xedge_index(g, ntx, 1, q0 + i, 0, it)] = seam2[w][1][i];
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
     }
   }
 }
@@ -388,12 +433,11 @@ template <class S, int DIM, bool ANI>
 __global__ __launch_bounds__(NTHREADS) void k_xpairs(const S *__restrict__ E, Geo g, int ntx, int tw,
                                                      cplx *__restrict__ part) {
   const double *__restrict__ C = g.cf;
-  const int64_t nrow = g.nzl * g.nyp;  // (plane, row) lines
-  const int64_t npair = nrow * (ntx - 1);
+  const int64_t npair = g.nzl * g.nyp * (ntx - 1);
   double acc = 0.0;
   for (int64_t e = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; e < npair; e += (int64_t)gridDim.x * NTHREADS) {
-    const int64_t t = e % (ntx - 1), line = e / (ntx - 1);
-    const int64_t q = line / g.nyp, y = line % g.nyp;
+    const int64_t q = e % g.nzl, rest = e / g.nzl;  // q fastest: runs of the E layout
+    const int64_t y = rest % g.nyp, t = rest / g.nyp;
     const S a = E[xedge_index(g, ntx, 1, q, y, t)];
     const S b = E[xedge_index(g, ntx, 0, q, y, t + 1)];
     double w = 0.0;
