@@ -137,18 +137,13 @@ __device__ cplx eval_f(int func, double lam, double t_re, double t_im) {
   }
 }
 
-__device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf, int f0, int f1,
-                                         double t_re, double t_im);
-#ifndef NLS_EIGEN_JACOBI
-#define NLS_EIGEN_JACOBI 1
-#endif
 __device__ __noinline__ void eigen_phase_jacobi(KState *__restrict__ st, int m, int nf, int f0,
                                                 int f1, double t_re, double t_im);
 
 // After the last k_update<m-2>: sums[0..m-1] = g_0..g_{m-2}, nn (tail = 1: no
 // last update, s_{m-1} already set by the last k_reduce_iter).  Completes
 // T (T(m-1,m-1) = 0, eigen_krylov_complex.hpp:21), diagonalises it with
-// implicit-shift QL on wave 0 (lane r owns row r of Q) and writes
+// parallel cyclic Jacobi on the whole workgroup (eigen_phase_jacobi) and writes
 //   fin[f][k] = s_0 * (Q f(Lambda) Q^T e_1)_k / s_k
 // so that  f(L) W_0 = sum_k fin[f][k] W_k  (= beta V f(T) e1).
 __global__ __launch_bounds__(NTHREADS) void k_reduce_final(KState *__restrict__ st,
@@ -179,31 +174,66 @@ __global__ __launch_bounds__(NTHREADS) void k_reduce_final(KState *__restrict__ 
   }
   if (threadIdx.x == 0) st->Td[m - 1] = 0.0;
   __syncthreads();
-#if NLS_EIGEN_JACOBI
   eigen_phase_jacobi(st, m, nf, f0, f1, t_re, t_im);
-#else
-  if (threadIdx.x < 64) eigen_phase(st, m, nf, f0, f1, t_re, t_im);
-#endif
 }
 
-// Parallel cyclic Jacobi on the whole workgroup (the algorithm of the oracle,
-// oracle/nls_oracle.cpp jacobi_eig, with a round-robin ordering so that the
-// m/2 rotations of a round are disjoint and applied at once).  Per round: one
-// thread per pair computes (c, s); then all threads rotate the column pairs of
-// A and Q, then the row pairs of A.  Sweeps until off(A)^2 <= 1e-34 |A|^2.
+// Cyclic Jacobi (the algorithm of the oracle, oracle/nls_oracle.cpp jacobi_eig:
+// same rotation, same stopping rule off(A)^2 <= 1e-34 |A|^2, T pre-scaled to
+// max|entry| = 1 like Eigen's solver) with a round-robin (circle method)
+// ordering, so that the m/2 rotations of a round are disjoint and applied at
+// once.  The matrices are distributed one entry per thread: thread e owns A[i][j]
+// and Q[i][j] (e = i*m + j + k*NTHREADS, k < JENT) in registers.  A round is
+// two phases: thread i < m computes the rotation (c_i, z_i) acting on index i
+// (both members of a pair compute the same c, s: same inputs, same code), then
+// every entry is rotated with plain FMAs,
+//   A'[i][j] = c_i (c_j A[i][j] + z_j A[i][p_j]) + z_i (c_j A[p_i][j] + z_j A[p_i][p_j])
+//   Q'[i][j] = c_j Q[i][j] + z_j Q[i][p_j]
+// (p = partner index of the round, z = -s on the lower index of a pair, +s on
+// the upper), reading buffer cur and writing buffer cur^1.  Partners come from
+// a table built once.  The rotation is the oracle's (tan of the smaller angle,
+// t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)), theta = (a_qq - a_pp) / 2a_pq)
+// written with one sqrt, one division and one rsqrt (its latency is the round's):
+//   t = sgn(theta) |2 a_pq| / (|d| + sqrt(d^2 + 4 a_pq^2)),  d = a_qq - a_pp.
+__device__ __forceinline__ void jacobi_rot(const double (*A)[MMAX + 1], int i, int pi, double &c,
+                                           double &z) {
+  c = 1.0;
+  z = 0.0;
+  if (pi == i) return;
+  const int p = i < pi ? i : pi, q = i < pi ? pi : i;
+  const double apq = A[p][q];
+  if (apq == 0.0) return;
+  const double d = A[q][q] - A[p][p], a2 = 2.0 * apq;
+  const double h = sqrt(d * d + a2 * a2);
+  double tt;
+  if (h > 0.0 && h < 1e300) {
+    const bool pos = d == 0.0 || ((d > 0.0) == (apq > 0.0));  // theta >= 0
+    tt = (pos ? fabs(a2) : -fabs(a2)) / (fabs(d) + h);
+  } else {  // squares under/overflowed: the direct form
+    const double theta = d / a2;
+    tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+  }
+  c = rsqrt(tt * tt + 1.0);
+  z = i == p ? -(tt * c) : tt * c;
+}
+
 __device__ __noinline__ void eigen_phase_jacobi(KState *__restrict__ st, int m, int nf, int f0,
                                                 int f1, double t_re, double t_im) {
-  __shared__ double A[MMAX][MMAX + 1];
-  __shared__ double Q[MMAX][MMAX + 1];
-  __shared__ double rc[MMAX / 2], rs[MMAX / 2];
-  __shared__ int rp[MMAX / 2], rq[MMAX / 2];
-  __shared__ double red[2][NTHREADS / 64];
+  constexpr int JENT = MMAX * MMAX / NTHREADS;
+  __shared__ double A[2][MMAX][MMAX + 1];
+  __shared__ double Q[2][MMAX][MMAX + 1];
+  __shared__ unsigned char part[MMAX - 1][MMAX];
+  __shared__ double rc[MMAX], rz[MMAX];
+  __shared__ cplx fl[2][MMAX];
+  __shared__ double red[2][2][NTHREADS / 64];
   __shared__ double s_scl;
   const int t = threadIdx.x;
+#ifdef NLS_EIG_DEBUG
+  const long long tc0 = wall_clock64();
+  int nsw = 0;
+#endif
   const int mp = (m + 1) & ~1;  // even number of round-robin slots (slot m is a dummy if m is odd)
   const int npair = mp / 2;
-  // T scaled to max |entry| = 1 (as the QL path and Eigen's solver)
-  if (t < 64) {
+  if (t < 64) {  // T scaled to max |entry| = 1
     double v = 0.0;
     if (t < m) v = fabs(st->Td[t]);
     if (t < m - 1) v = fmax(v, fabs(st->To[t]));
@@ -211,217 +241,135 @@ __device__ __noinline__ void eigen_phase_jacobi(KState *__restrict__ st, int m, 
     for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
     if (t == 0) s_scl = v > 0.0 ? v : 1.0;
   }
-  __syncthreads();
-  const double iscl = 1.0 / s_scl;
-  for (int e = t; e < m * m; e += NTHREADS) {
-    const int i = e / m, j = e % m;
-    double a = 0.0;
-    if (i == j) a = st->Td[i] * iscl;
-    else if (i == j + 1) a = st->To[j] * iscl;
-    else if (j == i + 1) a = st->To[i] * iscl;
-    A[i][j] = a;
-    Q[i][j] = i == j ? 1.0 : 0.0;
+  // partner table (circle method: slot 0 fixed, the others rotate); an index
+  // paired with the dummy slot is its own partner (identity rotation)
+  for (int e = t; e < (mp - 1) * npair; e += NTHREADS) {
+    const int r = e / npair, k = e % npair;
+    const int a = k == 0 ? 0 : 1 + (k - 1 + r) % (mp - 1);
+    const int b = 1 + (mp - 2 - k + r) % (mp - 1);
+    const bool both = a < m && b < m;
+    part[r][a] = (unsigned char)(both ? b : a);
+    part[r][b] = (unsigned char)(both ? a : b);
   }
   __syncthreads();
-  int sweep = 0;
-  for (; sweep < 100; ++sweep) {
+  const double iscl = 1.0 / s_scl;
+  int ei[JENT], ej[JENT];
+  double av[JENT], qv[JENT];
+#pragma unroll
+  for (int k = 0; k < JENT; ++k) {
+    const int e = t + k * NTHREADS;
+    ei[k] = -1;
+    ej[k] = 0;
+    av[k] = qv[k] = 0.0;
+    if (e < m * m) {
+      const int i = e / m, j = e % m;
+      double a = 0.0;
+      if (i == j) a = st->Td[i] * iscl;
+      else if (i == j + 1) a = st->To[j] * iscl;
+      else if (j == i + 1) a = st->To[i] * iscl;
+      ei[k] = i;
+      ej[k] = j;
+      av[k] = a;
+      qv[k] = i == j ? 1.0 : 0.0;
+      A[0][i][j] = a;
+      Q[0][i][j] = qv[k];
+    }
+  }
+  __syncthreads();
+#ifdef NLS_EIG_DEBUG
+  const long long tc1 = wall_clock64();
+#endif
+  int cur = 0;
+  for (int sweep = 0; sweep < 100; ++sweep) {
+#ifdef NLS_EIG_DEBUG
+    nsw = sweep;
+#endif
     // convergence test on the whole matrix (oracle: off <= 1e-34 tot || off == 0)
     double off = 0.0, tot = 0.0;
-    for (int e = t; e < m * m; e += NTHREADS) {
-      const int i = e / m, j = e % m;
-      const double a2 = A[i][j] * A[i][j];
+#pragma unroll
+    for (int k = 0; k < JENT; ++k) {
+      const double a2 = av[k] * av[k];
       tot += a2;
-      if (i != j) off += a2;
+      if (ei[k] >= 0 && ei[k] != ej[k]) off += a2;
     }
     off = wave_sum(off);
     tot = wave_sum(tot);
     if ((t & 63) == 0) {
-      red[0][t >> 6] = off;
-      red[1][t >> 6] = tot;
+      red[sweep & 1][0][t >> 6] = off;
+      red[sweep & 1][1][t >> 6] = tot;
     }
     __syncthreads();
     double so = 0.0, sa = 0.0;
 #pragma unroll
     for (int w = 0; w < NTHREADS / 64; ++w) {
-      so += red[0][w];
-      sa += red[1][w];
+      so += red[sweep & 1][0][w];
+      sa += red[sweep & 1][1][w];
     }
-    __syncthreads();
     if (so <= 1e-34 * sa || so == 0.0) break;  // uniform across the workgroup
     for (int r = 0; r < mp - 1; ++r) {
-      if (t < npair) {  // circle method: slot 0 fixed, the others rotate
-        const int a = t == 0 ? 0 : 1 + (t - 1 + r) % (mp - 1);
-        const int b = 1 + (mp - 2 - t + r) % (mp - 1);
-        const int p = a < b ? a : b, q = a < b ? b : a;
-        double c = 1.0, sn = 0.0;
-        if (q < m) {
-          const double apq = A[p][q];
-          if (apq != 0.0) {
-            const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
-            const double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-            c = 1.0 / sqrt(tt * tt + 1.0);
-            sn = tt * c;
-          }
-        }
-        rp[t] = p;
-        rq[t] = q < m ? q : p;  // dummy pair: identity rotation on p
+      const double(*Ac)[MMAX + 1] = A[cur];
+      const double(*Qc)[MMAX + 1] = Q[cur];
+#if NLS_JAC_ONEPHASE
+#pragma unroll
+      for (int k = 0; k < JENT; ++k) {
+        if (ei[k] < 0) continue;
+        const int i = ei[k], j = ej[k];
+        const int pi = part[r][i], pj = part[r][j];
+        double ci, zi, cj, zj;
+        jacobi_rot(Ac, i, pi, ci, zi);
+        jacobi_rot(Ac, j, pj, cj, zj);
+#else
+      if (t < m) {
+        double c, z;
+        jacobi_rot(Ac, t, part[r][t], c, z);
         rc[t] = c;
-        rs[t] = q < m ? sn : 0.0;
+        rz[t] = z;
       }
       __syncthreads();
-      // A <- J^T A J and Q <- Q J in one phase: the pairs are disjoint, so each
-      // 2x2 block A[{pa,qa}][{pb,qb}] (and each Q row segment) has one owner.
-      // The annihilated entry of a diagonal block is set to exactly zero (else
-      // rounding keeps off(A) above the stopping threshold for ever).
-      for (int e = t; e < npair * npair + m * npair; e += NTHREADS) {
-        if (e < npair * npair) {
-          const int a = e / npair, b = e % npair;
-          const int pa = rp[a], qa = rq[a], pb = rp[b], qb = rq[b];
-          const double ca = rc[a], sa = rs[a], cb = rc[b], sb = rs[b];
-          const bool va = pa != qa, vb = pb != qb;
-          const double b00 = A[pa][pb], b01 = vb ? A[pa][qb] : 0.0;
-          const double b10 = va ? A[qa][pb] : 0.0, b11 = (va && vb) ? A[qa][qb] : 0.0;
-          // rows: [[ca, -sa], [sa, ca]] * B
-          const double r00 = ca * b00 - sa * b10, r01 = ca * b01 - sa * b11;
-          const double r10 = sa * b00 + ca * b10, r11 = sa * b01 + ca * b11;
-          // columns: * [[cb, sb], [-sb, cb]]
-          double n00 = r00 * cb - r01 * sb, n01 = r00 * sb + r01 * cb;
-          double n10 = r10 * cb - r11 * sb, n11 = r10 * sb + r11 * cb;
-          if (a == b && va) n01 = n10 = 0.0;
-          A[pa][pb] = n00;
-          if (vb) A[pa][qb] = n01;
-          if (va) A[qa][pb] = n10;
-          if (va && vb) A[qa][qb] = n11;
-        } else {
-          const int e2 = e - npair * npair;
-          const int k = e2 / npair, b = e2 % npair;
-          const int p = rp[b], q = rq[b];
-          if (p == q) continue;
-          const double c = rc[b], sn = rs[b];
-          const double qkp = Q[k][p], qkq = Q[k][q];
-          Q[k][p] = c * qkp - sn * qkq;
-          Q[k][q] = sn * qkp + c * qkq;
-        }
+#pragma unroll
+      for (int k = 0; k < JENT; ++k) {
+        if (ei[k] < 0) continue;
+        const int i = ei[k], j = ej[k];
+        const int pi = part[r][i], pj = part[r][j];
+        const double ci = rc[i], zi = rz[i], cj = rc[j], zj = rz[j];
+#endif
+        double na = ci * (cj * av[k] + zj * Ac[i][pj]) + zi * (cj * Ac[pi][j] + zj * Ac[pi][pj]);
+        if (pi == j && pi != i) na = 0.0;  // the annihilated pivot (else off(A) stalls on rounding)
+        const double nq = cj * qv[k] + zj * Qc[i][pj];
+        av[k] = na;
+        qv[k] = nq;
+        A[cur ^ 1][i][j] = na;
+        Q[cur ^ 1][i][j] = nq;
       }
       __syncthreads();
+      cur ^= 1;
     }
   }
 #ifdef NLS_EIG_DEBUG
-  if (t == 0) printf("[jacobi] m=%d sweeps=%d\n", m, sweep);
+  const long long tc2 = wall_clock64();
 #endif
-  // fin[f][r] = s0 / s_r * sum_k Q[r][k] Q[0][k] f(lambda_k)
+  // fin[f][r] = s0 / s_r * sum_k Q[r][k] Q[0][k] f(lambda_k); f(lambda_k) once per k
   if (t < m) {
-    st->lam[t] = A[t][t] * s_scl;
+    const double lam = A[cur][t][t] * s_scl;
+    st->lam[t] = lam;
+    for (int fi = 0; fi < nf; ++fi) fl[fi][t] = eval_f(fi == 0 ? f0 : f1, lam, t_re, t_im);
+  }
+  __syncthreads();
+  if (t < m) {
     const double s0 = st->s[0];
     const double isr = inv_or_zero(st->s[t]);
     for (int fi = 0; fi < nf; ++fi) {
-      const int func = fi == 0 ? f0 : f1;
       cplx c = {0.0, 0.0};
-      for (int k = 0; k < m; ++k) c += (Q[t][k] * Q[0][k]) * eval_f(func, A[k][k] * s_scl, t_re, t_im);
+      for (int k = 0; k < m; ++k) c += (Q[cur][t][k] * Q[cur][0][k]) * fl[fi][k];
       st->fin[fi][t] = (s0 * isr) * c;
     }
   }
-}
-
-// Wave-0 part of k_reduce_final.  Lane k holds d[k] and e[k] in registers; the
-// implicit-shift QL recurrence (uniform across lanes) reads them with
-// v_readlane and writes them back with a lane-select, so its dependency chain
-// never waits on LDS.  Lane r applies every Givens rotation to row r of Q (LDS).
-__device__ __forceinline__ double rdlane(double v, int i) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), i);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), i);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __noinline__ void eigen_phase(KState *__restrict__ st, int m, int nf, int f0, int f1,
-                                         double t_re, double t_im) {
-  __shared__ double Q[MMAX][MMAX + 1];
-  const int lane = threadIdx.x;
-  // scale T to max|entry| = 1 (as Eigen's SelfAdjointEigenSolver does)
-  double dl = lane < m ? st->Td[lane] : 0.0;
-  double el = lane < m - 1 ? st->To[lane] : 0.0;
-  double scl = fmax(fabs(dl), fabs(el));
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) scl = fmax(scl, __shfl_xor(scl, off, 64));
-  const double iscl = scl > 0.0 ? 1.0 / scl : 1.0;
-  if (scl == 0.0) scl = 1.0;
-  dl *= iscl;
-  el *= iscl;
-  if (lane < m)
-    for (int c = 0; c < m; ++c) Q[lane][c] = lane == c ? 1.0 : 0.0;
-  auto setd = [&](int i, double v) { if (lane == i) dl = v; };
-  auto sete = [&](int i, double v) { if (lane == i) el = v; };
 #ifdef NLS_EIG_DEBUG
-  int tot_iter = 0, tot_rot = 0;
+  __syncthreads();
+  if (t == 0)
+    printf("[jacobi] m=%d sweeps=%d init %.1f us, sweeps %.1f us, fin %.1f us\n", m, nsw,
+           (tc1 - tc0) * 0.01, (tc2 - tc1) * 0.01, (wall_clock64() - tc2) * 0.01);
 #endif
-  for (int l = 0; l < m; ++l) {
-    int iter = 0;
-    for (;;) {
-      int mm;
-      for (mm = l; mm < m - 1; ++mm) {
-        const double dd = fabs(rdlane(dl, mm)) + fabs(rdlane(dl, mm + 1));
-        if (fabs(rdlane(el, mm)) <= 2.220446049250313e-16 * dd) break;
-      }
-      if (mm == l) break;
-      if (++iter > 64) break;
-#ifdef NLS_EIG_DEBUG
-      ++tot_iter;
-      tot_rot += mm - l;
-#endif
-      const double dlv = rdlane(dl, l), el_l = rdlane(el, l);
-      double gg = (rdlane(dl, l + 1) - dlv) / (2.0 * el_l);
-      double rr = hypot(gg, 1.0);
-      gg = rdlane(dl, mm) - dlv + el_l / (gg + (gg >= 0.0 ? fabs(rr) : -fabs(rr)));
-      double ss = 1.0, cc = 1.0, pp = 0.0;
-      bool early = false;
-      for (int i = mm - 1; i >= l; --i) {
-        const double ei = rdlane(el, i);
-        const double ff = ss * ei, bb = cc * ei;
-        rr = sqrt(ff * ff + gg * gg);
-        sete(i + 1, rr);
-        if (rr == 0.0) {
-          setd(i + 1, rdlane(dl, i + 1) - pp);
-          sete(mm, 0.0);
-          early = true;
-          break;
-        }
-        const double irr = 1.0 / rr;
-        ss = ff * irr;
-        cc = gg * irr;
-        gg = rdlane(dl, i + 1) - pp;
-        rr = (rdlane(dl, i) - gg) * ss + 2.0 * cc * bb;
-        pp = ss * rr;
-        setd(i + 1, gg + pp);
-        gg = cc * rr - bb;
-        if (lane < m) {
-          const double fq = Q[lane][i + 1];
-          Q[lane][i + 1] = ss * Q[lane][i] + cc * fq;
-          Q[lane][i] = cc * Q[lane][i] - ss * fq;
-        }
-      }
-      if (early) continue;
-      setd(l, rdlane(dl, l) - pp);
-      sete(l, gg);
-      sete(mm, 0.0);
-    }
-  }
-#ifdef NLS_EIG_DEBUG
-  if (lane == 0) printf("[ql] m=%d iters=%d rotations=%d\n", m, tot_iter, tot_rot);
-#endif
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  const double lam_l = dl * scl;
-  if (lane < m) {
-    st->lam[lane] = lam_l;
-    const double s0 = st->s[0];
-    const double isr = inv_or_zero(st->s[lane]);
-    for (int fi = 0; fi < nf; ++fi) {
-      const int func = fi == 0 ? f0 : f1;
-      cplx c = {0.0, 0.0};
-      for (int k = 0; k < m; ++k) c += (Q[lane][k] * Q[0][k]) * eval_f(func, rdlane(lam_l, k), t_re, t_im);
-      st->fin[fi][lane] = (s0 * isr) * c;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
