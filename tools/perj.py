@@ -10,8 +10,12 @@ n, dim, m = w["n"], w["dim"], w["m"]
 dx = 2 * w["L"] / (n - 1)
 s = nls_amd.Solver(dim, n, n, n if dim == 3 else 1, dx, dx, equation=w["eq"], m=m)
 u = bench.synthetic_ic(w, s.z0, s.nzl)
-u /= np.sqrt(bench.global_mass(u, dx ** dim))
-s.set_field(u)
+if w["eq"] == 3:  # G2: m(x), c(x) as in bench.py
+    s.set_field(u)
+    s.set_coefficients(*bench.g2_coefficients(n, w["L"], s.z0, s.nzl))
+else:
+    u /= np.sqrt(bench.global_mass(u, dx ** dim))
+    s.set_field(u)
 s.step(w["dt"], 2)
 s.sync()
 s.reset_timing(); s.set_timing(True)
