@@ -138,6 +138,7 @@ struct nls_handle {
   hipStream_t cstream = nullptr;
   hipEvent_t ev_bnd = nullptr, ev_halo = nullptr;
   bool halo_pending = false;
+  bool bnd_side = true;  // boundary-plane launches on cstream (NLS_BND_SIDE=0: in order on the compute stream)
   // asynchronous snapshots: staging copy on the compute stream, D2H on xstream
   hipStream_t xstream = nullptr;
   hipEvent_t ev_snap = nullptr, ev_snap_done = nullptr;
@@ -226,19 +227,21 @@ void harvest_timing(nls_handle *h) {
   h->recs.clear();
 }
 
-void launch(nls_handle *h, int cls, int j, const void *fn, int grid, void **args) {
+void launch(nls_handle *h, int cls, int j, const void *fn, int grid, void **args,
+            hipStream_t stream = nullptr) {
   if (!fn) fail(h, NLS_ERR_ARG, "kernel variant not instantiated");
+  if (!stream) stream = h->stream;
   TimingRec rec{cls, j, nullptr, nullptr};
   if (h->timing) {
     if (h->recs.size() >= 4096) harvest_timing(h);
     rec.a = get_event(h);
     rec.b = get_event(h);
-    hip_check(h, hipEventRecord(rec.a, h->stream), "hipEventRecord");
+    hip_check(h, hipEventRecord(rec.a, stream), "hipEventRecord");
   }
-  hip_check(h, hipLaunchKernel(fn, dim3(grid), dim3(NTHREADS), args, 0, h->stream),
+  hip_check(h, hipLaunchKernel(fn, dim3(grid), dim3(NTHREADS), args, 0, stream),
             "hipLaunchKernel");
   if (h->timing) {
-    hip_check(h, hipEventRecord(rec.b, h->stream), "hipEventRecord");
+    hip_check(h, hipEventRecord(rec.b, stream), "hipEventRecord");
     h->recs.push_back(rec);
   }
 }
@@ -565,6 +568,15 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
     const void *fu = kernel_update(h->cplx_, (int)h->cfg.dim, j, h->ani);
     const UpdPlan &pl = h->plan[j];
     const bool need_halo = j + 1 <= m - 2 && h->collective;
+    // With a halo to send, the boundary-plane launches run on the halo stream,
+    // followed there by the exchange, concurrently with the interior launch on
+    // the compute stream (disjoint output planes and partial columns); the next
+    // pass waits on the halo event.
+    const bool side = need_halo && pl.nbnd > 0 && h->bnd_side;
+    if (side) {
+      hip_check(h, hipEventRecord(h->ev_bnd, h->stream), "hipEventRecord");
+      hip_check(h, hipStreamWaitEvent(h->cstream, h->ev_bnd, 0), "hipStreamWaitEvent");
+    }
     for (int i = 0; i < pl.n; ++i) {
       Geo gi = g;
       gi.qa = pl.qa[i];
@@ -572,8 +584,17 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
       int ps = pl.total, po = pl.off[i];
       void *nul = nullptr;
       void *args[] = {&W, &out, &vs, &gi, &st, &h->partU, &ps, &po, &nul};
-      launch(h, 1, j, fu, pl.grid[i], args);
-      if (need_halo && i + 1 == pl.nbnd) halo_begin(h, b, j + 1);
+      const bool bnd = i < pl.nbnd;
+      launch(h, 1, j, fu, pl.grid[i], args, side && bnd ? h->cstream : nullptr);
+      if (need_halo && i + 1 == pl.nbnd) {
+        if (side) {
+          halo_planes(h, vec_ptr(h, b, j + 1), (int64_t)h->esize, h->cstream);
+          hip_check(h, hipEventRecord(h->ev_halo, h->cstream), "hipEventRecord");
+          h->halo_pending = true;
+        } else {
+          halo_begin(h, b, j + 1);
+        }
+      }
     }
     if (need_halo && pl.nbnd == 0) halo(h, b, j + 1);
   }
@@ -923,7 +944,9 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
       rccl_check(h, ncclCommInitRank(&h->comm, 1, id, 0), "ncclCommInitRank");
     }
     h->collective = h->nranks > 1 || h->comm != nullptr;
+    if (const char *e = std::getenv("NLS_BND_SIDE")) h->bnd_side = std::atoi(e) != 0;
     if (h->collective) {
+      // (a high-priority stream here measured every kernel of the process 2x slower)
       hip_check(h, hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking), "hipStreamCreate");
       hip_check(h, hipEventCreateWithFlags(&h->ev_bnd, hipEventDisableTiming), "hipEventCreate");
       hip_check(h, hipEventCreateWithFlags(&h->ev_halo, hipEventDisableTiming), "hipEventCreate");
