@@ -1,0 +1,69 @@
+"""The two-vectors-per-pass Lanczos model (tests/sstep_model.py) against the MGS
+oracle (oracle/np_ref.py lanczos, eigen_krylov_complex.hpp:10-53): same T, same
+f(L)u, orthonormal implicit basis; the shift is what keeps the Gram-derived norms
+accurate.  CPU only, small grids."""
+import numpy as np
+import pytest
+
+from oracle import np_ref
+import sstep_model as sm
+
+
+def _field(dim, n, seed=0):
+    rng = np.random.default_rng(seed)
+    L = 10.0
+    dx = 2 * L / (n - 1)
+    x = np.linspace(-L, L, n)
+    g = np.meshgrid(*([x] * dim), indexing="ij")
+    r2 = sum(a * a for a in g)
+    shape = (n,) * dim
+    u = np.exp(-r2 / 4.0) * (1 + 0.1j) + 1e-3 * (rng.standard_normal(shape) + 1j * rng.standard_normal(shape))
+    u = u.ravel()
+    return u / np.sqrt(np.sum(np.abs(u) ** 2) * dx ** dim), dx
+
+
+@pytest.mark.parametrize("dim,n,m", [(3, 12, 16), (2, 32, 16), (3, 10, 25), (2, 24, 10), (3, 10, 15)])
+def test_tridiagonal_matches_mgs(dim, n, m):
+    u, dx = _field(dim, n)
+    nz = n if dim == 3 else 1
+    ap = lambda v: np_ref.laplacian_apply(dim, n, n, nz, dx, dx, v)
+    T, S, C, beta, G = sm.lanczos2(ap, u, m)
+    _, Tr, br = np_ref.lanczos(ap, u, m)
+    assert abs(beta - br) <= 1e-15 * br
+    assert np.abs(T - np.real(Tr)).max() <= 1e-12 * np.abs(Tr).max()
+    assert np.abs(C.conj().T @ G @ C - np.eye(m)).max() <= 1e-12
+
+
+def test_shift_is_needed():
+    u, dx = _field(3, 12)
+    ap = lambda v: np_ref.laplacian_apply(3, 12, 12, 12, dx, dx, v)
+    _, Tr, _ = np_ref.lanczos(ap, u, 16)
+    err = {}
+    for shift in (True, False):
+        T, *_ = sm.lanczos2(ap, u, 16, shift=shift)
+        err[shift] = np.abs(T - np.real(Tr)).max() / np.abs(Tr).max()
+    assert err[True] < 1e-12 < err[False]
+
+
+def test_nlse_trajectory_matches_oracle():
+    u, dx = _field(3, 12)
+    ref = np_ref.nlse_steps(3, 12, 12, 12, dx, dx, u, 1e-3, 8, 16)
+    got, worst = sm.nlse_steps2(3, 12, dx, u, 1e-3, 8, 16)
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) <= 1e-12
+    assert worst <= 1e-12
+
+
+def test_g2_anisotropic_operator():
+    n, m = 10, 25
+    u, dx = _field(3, n, seed=3)
+    x = np.linspace(-1, 1, n)
+    g = np.meshgrid(x, x, x, indexing="ij")
+    c = (1.0 + 0.3 * np.sin(2 * g[0]) * np.cos(g[1]) * np.cos(g[2])).ravel()
+    A = np_ref.aniso_laplacian(3, n, n, n, dx, dx, c)
+    ap = lambda v: A @ v
+    T, S, C, beta, G = sm.lanczos2(ap, u, m)
+    _, Tr, _ = np_ref.lanczos(ap, u, m)
+    assert np.abs(T - np.real(Tr)).max() <= 1e-12 * np.abs(Tr).max()
+    b2, _, _ = sm.krylov2(ap, u, 1j * 1e-3, m, np_ref.F_EXP)
+    b1 = np_ref.krylov(ap, u, 1j * 1e-3, m, np_ref.F_EXP)
+    assert np.linalg.norm(b2 - b1) / np.linalg.norm(b1) <= 1e-12
