@@ -107,6 +107,11 @@ struct nls_handle {
   // fused tail (m >= 3): the last update pass of a basis and the combination
   // that ends the step are one pass, k_tail (NLS_FUSED_TAIL=0 disables)
   bool fused_tail = false;
+  // two new Lanczos vectors per basis pass (nls_pass2.hpp; NLS_PASS2=1, 3D isotropic NLSE, one rank)
+  bool pass2 = false;
+  void *p2 = nullptr;          // P2State
+  cplx *partP2 = nullptr;      // per-workgroup partials of k_pass2
+  int p2grid = 0, p2kz = 32;
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
@@ -602,6 +607,49 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   reduce_final(h, b, nf, f0, f1, tr, ti);
 }
 
+// Two new vectors per pass (nls_pass2.hpp): the alpha pass + reduction of W_0
+// give beta and alpha_0 (the first shift); then passes at J = 0, 2, 4, ... each
+// followed by its column sums and k_p2coef; the eigensolve on the resulting T;
+// k_p2fin maps fin to the stored vectors for the caller's final pass.
+void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
+  const int m = h->m;
+  Geo ga = h->geo;
+  ga.kz = h->kz_alpha;
+  alpha_pass(h, 0, 0, ga);
+  reduce_iter(h, 0, 0);
+  KState *st = h->B[0].st;
+  void *ps = h->p2;
+  {
+    int J = 0, mm = m, mode = 0;
+    void *args[] = {&ps, &st, &J, &mm, &mode};
+    launch(h, 2, 0, kernel_p2coef(), 1, args);
+  }
+  void *W = vec_ptr(h, 0, 0);
+  int64_t vs = h->vs;
+  Geo g = h->geo;
+  g.kz = h->p2kz;
+  cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(h->p2) + p2state_sums_offset());
+  int J = 0;
+  while (J + 1 < m) {
+    const bool hz = J + 2 < m;
+    int nb = h->p2grid;
+    void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb};
+    launch(h, 1, J, kernel_pass2(J, hz), h->p2grid, args);
+    const cplx *pA = nullptr;
+    int nbA = 0, ncA = 0, ncU = hz ? 2 * J + 5 : J + 2;
+    void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
+    launch(h, 2, J, kernel_colsum(), ncU, cargs);
+    int mm = m, mode = 1, jj = J;
+    void *a2[] = {&ps, &st, &jj, &mm, &mode};
+    launch(h, 2, J, kernel_p2coef(), 1, a2);
+    J += hz ? 2 : 1;
+  }
+  reduce_final(h, 0, nf, f0, f1, tr, ti, 1);
+  int mm = m, nff = nf;
+  void *fa[] = {&ps, &st, &mm, &nff};
+  launch(h, 2, m, kernel_p2fin(), 1, fa);
+}
+
 int occupancy_grid(nls_handle *h, const void *fn, int64_t work_items) {
   int per_cu = 0;
   hip_check(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHREADS, 0),
@@ -684,8 +732,22 @@ void alloc_all(nls_handle *h) {
   const bool c = h->cplx_;
   const int dim = h->cfg.dim;
   const bool ani = h->ani;
+  // two-vectors-per-pass Lanczos (opt-in): stores all m vectors, no fused tail / folded alpha
+  h->pass2 = false;
+  if (const char *e = std::getenv("NLS_PASS2"); e && std::atoi(e) != 0)
+    h->pass2 = c && !ani && dim == 3 && !h->collective && h->nbasis == 1 && g.nx % 64 == 0 &&
+               g.nyp % P2_TILE_Y == 0 && h->m >= 3 && h->m <= MMAX;
+  if (h->pass2) {
+    if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
+    const int64_t nzc = (g.npl + h->p2kz - 1) / h->p2kz;
+    h->p2grid = (int)((g.nx / 64) * (g.nyp / P2_TILE_Y) * nzc);
+    hip_check(h, hipMalloc(&h->p2, p2state_bytes()), "hipMalloc(p2)");
+    hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes(), h->stream), "hipMemset");
+    hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (2 * MMAX + 8) * sizeof(cplx)),
+              "hipMalloc(partP2)");
+  }
   // fused tails first: a basis that always ends in one never stores W_{m-1}
-  h->fused_tail = h->m >= 3;
+  h->fused_tail = h->m >= 3 && !h->pass2;
   if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && std::atoi(e) != 0;
   if (h->fused_tail) {
     Geo g2 = g;
@@ -761,6 +823,7 @@ void alloc_all(nls_handle *h) {
   h->fused_alpha = !h->collective &&
                    (g.nloc > (int64_t(1) << 25) || (dim == 2 && g.nloc >= (int64_t(1) << 24)));
   if (const char *e = std::getenv("NLS_FUSED_ALPHA")) h->fused_alpha = !h->collective && std::atoi(e) != 0;
+  if (h->pass2) h->fused_alpha = false;
   if (h->fused_alpha) {  // seam buffer for the narrowest x tiles (64 wide)
     const size_t xe = 2 * (size_t)g.nzl * (size_t)g.nyp * (size_t)xtiles(g, dim, 1) * h->esize;
     hip_check(h, hipMalloc(&h->xedge, xe), "hipMalloc(xedge)");
@@ -812,7 +875,7 @@ void free_all(nls_handle *h) {
   }
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
-                  (void *)h->vel, h->xedge, (void *)h->partX,
+                  (void *)h->vel, h->xedge, (void *)h->partX, h->p2, (void *)h->partP2,
                   (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
   h->u = h->scratch = h->snap = h->uprev = nullptr;
@@ -1147,7 +1210,8 @@ void ss2_step(nls_handle *h, double dt) {
     halo(h, 0, 0);
   }
   const bool tail = use_tail(h, TAIL_NLSE);
-  if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt, tail);
+  if (h->pass2) run_lanczos2(h, 1, NLS_F_EXP_ABS, 0, -0.0, -dt);
+  else if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt, tail);
   else run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt, tail);
   void *W = vec_ptr(h, 0, 0);
   KState *st = h->B[0].st;

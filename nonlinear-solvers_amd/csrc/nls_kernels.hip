@@ -25,6 +25,7 @@
 #include "nls_kernels.hpp"
 #include "nls_reduce.hpp"
 #include "nls_stencil.hpp"
+#include "nls_pass2.hpp"
 
 namespace nls {
 
@@ -816,5 +817,20 @@ const void *kernel_sg_end(int M) {
   }
 }
 
-}  // namespace nls
+// two-vectors-per-pass Lanczos (nls_pass2.hpp): even J only
+const void *kernel_pass2(int J, bool hz) {
+  switch (J) {
+#define X(J) \
+  case J: return hz ? reinterpret_cast<const void *>(&k_pass2<J, true>) \
+                    : reinterpret_cast<const void *>(&k_pass2<J, false>);
+    X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30)
+#undef X
+    default: return nullptr;
+  }
+}
+const void *kernel_p2coef() { return reinterpret_cast<const void *>(&k_p2coef); }
+const void *kernel_p2fin() { return reinterpret_cast<const void *>(&k_p2fin); }
+size_t p2state_bytes() { return sizeof(P2State); }
+size_t p2state_sums_offset() { return offsetof(P2State, sums); }
 
+}  // namespace nls

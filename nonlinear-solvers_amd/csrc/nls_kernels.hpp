@@ -58,6 +58,13 @@ const void *kernel_reduce_final();
 //   colsum       : (const cplx* partA, int nbA, int ncA, const cplx* partU, int nbU, cplx* dst)
 //                  grid = ncA + ncU columns; dst = KState::sums (the do_sum phase, parallel)
 const void *kernel_colsum();
+// two-vectors-per-pass Lanczos (nls_pass2.hpp; 3D isotropic complex, single rank)
+const void *kernel_pass2(int J, bool hz);  // hz: also the second vector Z
+const void *kernel_p2coef();
+const void *kernel_p2fin();
+size_t p2state_bytes();
+size_t p2state_sums_offset();
+constexpr int P2_TILE_Y = 16;  // == P2_TY
 
 // pointwise (grid-stride):
 //   nl_init   : (const cplx* u, cplx* w0, const double* mf, int64_t n, double dt, int nonlin,

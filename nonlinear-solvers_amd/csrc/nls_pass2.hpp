@@ -1,0 +1,345 @@
+// nls_pass2.hpp -- two new Lanczos vectors per basis pass (3D isotropic NLSE,
+// single-rank handles; NLS_PASS2=1).  The scheme and its numerics are in
+// DESIGN.md §3 "two new vectors per basis pass" and tests/sstep_model.py.
+//
+// Stored raw vectors S_0..S_J (S_0 = the start vector), orthonormal basis
+// W = S C (C upper triangular), D = C^{-1} (S_l = sum_{i<=l} W_i D[i][l]),
+// Arnoldi matrix H[k][i] = W_k^H L W_i.  One pass k_pass2<J> reads S_0..S_J once
+// and the stencils L S_J, L^2 S_J of the last one (radius-2 tile march through
+// LDS), and writes
+//   X = bX1 L S_J + sum_l aX[l] S_l               (-> S_{J+1})
+//   Z = bZ2 L^2 S_J + bZ1 L S_J + sum_l aZ[l] S_l  (-> S_{J+2}, unless the last pass)
+// with X = L W_J - sigma W_J - sum_{k<J} conj(H[J][k]) W_k and Z = (L - sigma) X,
+// reducing S_l^H X, S_l^H Z, X^H X, X^H Z, Z^H Z.  k_p2coef turns those into the
+// new columns of C, D, H and the coefficients of the next pass.
+#pragma once
+#include "nls_common.hpp"
+
+namespace nls {
+
+constexpr int P2M = MMAX + 2;
+struct P2State {
+  cplx C[P2M][P2M];  // C[l][i]: W_i = sum_l S_l C[l][i]
+  cplx D[P2M][P2M];  // D[i][l]: S_l = sum_i W_i D[i][l]
+  cplx H[P2M][P2M];  // H[k][i] = W_k^H L W_i
+  cplx aX[P2M], aZ[P2M];
+  cplx bX1, bZ1, bZ2;
+  double sigma, beta;
+  cplx sums[2 * P2M + 8];
+};
+
+constexpr int P2_TY = 16;            // rows per tile (4 waves x 4 rows)
+constexpr int P2_HY = P2_TY + 4;     // S ring rows  (rows -2 .. TY+1)
+constexpr int P2_HX = 64 + 4;        // S ring cols  (x -2 .. 65)
+constexpr int P2_LY = P2_TY + 2;     // L1 ring rows (rows -1 .. TY)
+constexpr int P2_LX = 64 + 2;        // L1 ring cols (x -1 .. 64)
+
+__device__ __forceinline__ int p2slot(int k) { return ((k % 3) + 3) % 3; }
+
+// Tiles: 64 x-cells x 16 rows of one plane, marched over kz planes.  Flat
+// indexing throughout (rows past ny continue in the next plane: the reference's
+// 3D y-wrap, laplacians.hpp:57-105), so halo rows need no special case.
+template <int J, bool HZ>
+__global__ __launch_bounds__(NTHREADS) void k_pass2(cplx *__restrict__ W, int64_t vs, Geo g,
+                                                    const P2State *__restrict__ ps,
+                                                    cplx *__restrict__ part, int nb) {
+  __shared__ cplx Sr[3][P2_HY][P2_HX];
+  __shared__ cplx Lr[3][P2_LY][P2_LX];
+  __shared__ cplx cX[J + 1], cZ[J + 1];
+  constexpr int NC = HZ ? 2 * (J + 1) + 3 : J + 2;  // HZ: gX, gZ, xx, xz, zz; else gX, xx
+  __shared__ cplx red[NTHREADS / 64][NC];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t nx = g.nx, ny = g.nyp, P = g.P, nz = g.npl, nloc = g.nloc;
+  const int ntx = (int)(nx / 64), nty = (int)(ny / P2_TY);
+  const int nzc = (int)((nz + g.kz - 1) / g.kz);
+  const int tile = blockIdx.x;
+  if (tile >= ntx * nty * nzc) return;  // uniform per workgroup
+  const int xt = tile % ntx, yt = (tile / ntx) % nty, zc = tile / (ntx * nty);
+  const int64_t x0 = (int64_t)xt * 64, y0 = (int64_t)yt * P2_TY;
+  const int k0 = zc * g.kz, k1 = (int)min((int64_t)k0 + g.kz, nz);
+  for (int l = t; l <= J; l += NTHREADS) {
+    cX[l] = ps->aX[l];
+    cZ[l] = ps->aZ[l];
+  }
+  const cplx bX1 = ps->bX1, bZ1 = ps->bZ1, bZ2 = ps->bZ2;
+  const double s = g.s, sdi = g.sd_in, sdb = g.sd_bd;
+  const cplx *__restrict__ SJ = W + (int64_t)J * vs;
+  cplx *__restrict__ Xo = W + (int64_t)(J + 1) * vs;
+  cplx *__restrict__ Zo = W + (int64_t)(J + 2) * vs;
+
+  auto diag = [&](int64_t flat, int64_t x) {
+    const int64_t j = (flat / nx) % ny, k = flat / P;
+    const bool bd = x == 0 || x == nx - 1 || j == 0 || j == ny - 1 || k == 0 || k == nz - 1;
+    return bd ? sdb : sdi;
+  };
+  auto loadS = [&](int k) {
+    const int sl = p2slot(k);
+    for (int e = t; e < P2_HY * P2_HX; e += NTHREADS) {
+      const int r = e / P2_HX, c = e % P2_HX;
+      const int64_t x = x0 - 2 + c;
+      const int64_t flat = (int64_t)k * P + (y0 - 2 + r) * nx + x;
+      cplx v = {0.0, 0.0};
+      if (x >= 0 && x < nx && flat >= 0 && flat < nloc) v = SJ[flat];
+      Sr[sl][r][c] = v;
+    }
+  };
+  auto compL1 = [&](int k) {  // L S_J at plane k, rows -1..TY, x -1..64
+    const int sp = p2slot(k - 1), sc = p2slot(k), sn = p2slot(k + 1);
+    for (int e = t; e < P2_LY * P2_LX; e += NTHREADS) {
+      const int r = e / P2_LX, c = e % P2_LX;
+      const int64_t x = x0 - 1 + c;
+      const int64_t flat = (int64_t)k * P + (y0 - 1 + r) * nx + x;
+      cplx v = {0.0, 0.0};
+      if (x >= 0 && x < nx && flat >= 0 && flat < nloc) {
+        const cplx nbs = Sr[sc][r + 1][c] + Sr[sc][r + 1][c + 2] + Sr[sc][r][c + 1] +
+                         Sr[sc][r + 2][c + 1] + Sr[sp][r + 1][c + 1] + Sr[sn][r + 1][c + 1];
+        v = diag(flat, x) * Sr[sc][r + 1][c + 1] + s * nbs;
+      }
+      Lr[p2slot(k)][r][c] = v;
+    }
+  };
+
+  cplx acc[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) acc[i] = {0.0, 0.0};
+
+  loadS(k0 - 2);
+  loadS(k0 - 1);
+  loadS(k0);
+  __syncthreads();
+  compL1(k0 - 1);
+  __syncthreads();
+  loadS(k0 + 1);  // overwrites the slot of k0 - 2
+  __syncthreads();
+  compL1(k0);
+  for (int k = k0; k < k1; ++k) {
+    loadS(k + 2);  // slot of k - 1 (last read by compL1(k))
+    __syncthreads();
+    compL1(k + 1);
+    __syncthreads();
+    const int lp = p2slot(k - 1), lc = p2slot(k), ln = p2slot(k + 1);
+#pragma unroll 1
+    for (int i = 0; i < P2_TY / 4; ++i) {
+      const int r = w * (P2_TY / 4) + i;
+      const int64_t x = x0 + lane;
+      const int64_t flat = (int64_t)k * P + (y0 + r) * nx + x;
+      const cplx l1 = Lr[lc][r + 1][lane + 1];
+      cplx sv[J + 1];
+#pragma unroll
+      for (int l = 0; l < J; ++l) sv[l] = ld_nt(W + (int64_t)l * vs + flat);
+      sv[J] = Sr[lc][r + 2][lane + 2];
+      cplx X = cmul(bX1, l1);
+#pragma unroll
+      for (int l = 0; l <= J; ++l) X += cmul(cX[l], sv[l]);
+#pragma unroll
+      for (int l = 0; l <= J; ++l) acc[l] += cj_mul(sv[l], X);
+      st_nt(Xo + flat, X);
+      if constexpr (HZ) {
+        const cplx nbs = Lr[lc][r + 1][lane] + Lr[lc][r + 1][lane + 2] + Lr[lc][r][lane + 1] +
+                         Lr[lc][r + 2][lane + 1] + Lr[lp][r + 1][lane + 1] + Lr[ln][r + 1][lane + 1];
+        const cplx l2 = diag(flat, x) * l1 + s * nbs;
+        cplx Z = cmul(bZ2, l2) + cmul(bZ1, l1);
+#pragma unroll
+        for (int l = 0; l <= J; ++l) Z += cmul(cZ[l], sv[l]);
+#pragma unroll
+        for (int l = 0; l <= J; ++l) acc[J + 1 + l] += cj_mul(sv[l], Z);
+        acc[2 * J + 2].re += abs2(X);
+        acc[2 * J + 3] += cj_mul(X, Z);
+        acc[2 * J + 4].re += abs2(Z);
+        st_nt(Zo + flat, Z);
+      } else {
+        acc[J + 1].re += abs2(X);
+      }
+    }
+  }
+  // workgroup reduction, fixed order
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const double a = wave_sum(acc[i].re), b = wave_sum(acc[i].im);
+    if (lane == 0) red[w][i] = {a, b};
+  }
+  __syncthreads();
+  for (int i = t; i < NC; i += NTHREADS) {
+    cplx v = red[0][i];
+    for (int q = 1; q < NTHREADS / 64; ++q) v += red[q][i];
+    part[(int64_t)i * nb + blockIdx.x] = v;
+  }
+}
+
+// Coefficient kernel (one workgroup).  mode 0: start (after the alpha pass and
+// reduction of W_0: s[0] = beta, H[0][0] = alpha_0); mode 1: after the pass at
+// J (sums = the pass's columns, summed).  Computes the new columns of C, D, H
+// and, if another pass follows (J' + 1 < m), its coefficients; otherwise T into
+// the KState for k_reduce_final (s[] = 1, so fin is in the W basis; k_p2fin
+// converts it).
+__global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, KState *__restrict__ st,
+                                                     int J, int m, int mode) {
+  __shared__ cplx p[P2M], q[P2M], lw[P2M], xw[P2M], zw[P2M];
+  __shared__ double nu[2];
+  const int t = threadIdx.x;
+  int Jn;  // J of the next pass
+  if (mode == 0) {
+    for (int e = t; e < P2M * P2M; e += NTHREADS) {
+      const int i = e / P2M, k = e % P2M;
+      ps->C[i][k] = {0.0, 0.0};
+      ps->D[i][k] = {0.0, 0.0};
+      ps->H[i][k] = {0.0, 0.0};
+    }
+    __syncthreads();
+    if (t == 0) {
+      const double b = st->s[0];
+      ps->beta = b;
+      ps->C[0][0] = {b > 0.0 ? 1.0 / b : 0.0, 0.0};
+      ps->D[0][0] = {b, 0.0};
+      ps->sigma = st->H[0][0].re;
+    }
+    __syncthreads();
+    Jn = 0;
+  } else {
+    const int hz = J + 2 < m;  // the pass also produced Z
+    const cplx *sm = ps->sums;
+    // sums: hz: gX[0..J], gZ[0..J], xx, xz, zz; else gX[0..J], xx
+    const cplx xx = hz ? sm[2 * J + 2] : sm[J + 1];
+    const cplx xz = hz ? sm[2 * J + 3] : cplx{0.0, 0.0}, zz = hz ? sm[2 * J + 4] : cplx{0.0, 0.0};
+    // p_k = W_k^H X = sum_l conj(C[l][k]) (S_l^H X)
+    for (int k = t; k <= J; k += NTHREADS) {
+      cplx v = {0.0, 0.0};
+      for (int l = 0; l <= k; ++l) v += cj_mul(ps->C[l][k], sm[l]);
+      p[k] = v;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double n2 = xx.re;
+      for (int k = 0; k <= J; ++k) n2 -= abs2(p[k]);
+      nu[0] = n2 > 0.0 ? sqrt(n2) : 0.0;
+    }
+    __syncthreads();
+    const double nu1 = nu[0], inu1 = nu1 > 0.0 ? 1.0 / nu1 : 0.0;
+    const double sig = ps->sigma;
+    for (int i = t; i <= J + 1; i += NTHREADS) {
+      // C[:, J+1] = (e_{J+1} - C p) / nu1 ; D[:, J+1] = (p, nu1)
+      cplx v = {i == J + 1 ? 1.0 : 0.0, 0.0};
+      for (int k = i; k <= J; ++k) v = v - cmul(ps->C[i][k], p[k]);
+      ps->C[i][J + 1] = inu1 * v;
+      ps->D[i][J + 1] = i <= J ? p[i] : cplx{nu1, 0.0};
+      // H column J: p_k + sigma delta_kJ + conj(H[J][k]) (k < J); H[J+1][J] = nu1
+      cplx h = i <= J ? p[i] : cplx{nu1, 0.0};
+      if (i == J) h.re += sig;
+      if (i < J) h += cconj(ps->H[J][i]);
+      ps->H[i][J] = h;
+    }
+    __syncthreads();
+    if (hz) {
+      // q_k = W_k^H Z (k <= J+1): S-dots gZ (l <= J) and S_{J+1}^H Z = xz
+      for (int k = t; k <= J + 1; k += NTHREADS) {
+        cplx v = {0.0, 0.0};
+        for (int l = 0; l <= k && l <= J; ++l) v += cj_mul(ps->C[l][k], sm[J + 1 + l]);
+        if (k == J + 1) v += cj_mul(ps->C[J + 1][J + 1], xz);
+        q[k] = v;
+      }
+      __syncthreads();
+      if (t == 0) {
+        double n2 = zz.re;
+        for (int k = 0; k <= J + 1; ++k) n2 -= abs2(q[k]);
+        nu[1] = n2 > 0.0 ? sqrt(n2) : 0.0;
+      }
+      __syncthreads();
+      const double nu2 = nu[1], inu2 = nu2 > 0.0 ? 1.0 / nu2 : 0.0;
+      for (int i = t; i <= J + 2; i += NTHREADS) {
+        cplx v = {i == J + 2 ? 1.0 : 0.0, 0.0};
+        for (int k = i; k <= J + 1; ++k) v = v - cmul(ps->C[i][k], q[k]);
+        ps->C[i][J + 2] = inu2 * v;
+        ps->D[i][J + 2] = i <= J + 1 ? q[i] : cplx{nu2, 0.0};
+      }
+      // H column J+1 = (wz + sigma wx - p_J (wx + sigma e_J + conj(H[J][:J])) - sum_{k<J} p_k H[:,k]) / nu1
+      //   wx = (p, nu1, 0), wz = (q, nu2)
+      for (int i = t; i <= J + 2; i += NTHREADS) {
+        const cplx wxi = i <= J ? p[i] : (i == J + 1 ? cplx{nu1, 0.0} : cplx{0.0, 0.0});
+        const cplx wzi = i <= J + 1 ? q[i] : cplx{nu2, 0.0};
+        cplx lwj = wxi;
+        if (i == J) lwj.re += sig;
+        if (i < J) lwj += cconj(ps->H[J][i]);
+        cplx v = wzi + sig * wxi - cmul(p[J], lwj);
+        if (i <= J)
+          for (int k = (i > 0 ? i - 1 : 0); k < J; ++k) v = v - cmul(p[k], ps->H[i][k]);
+        ps->H[i][J + 1] = inu1 * v;
+      }
+      __syncthreads();
+      if (t == 0) ps->sigma = ps->H[J + 1][J + 1].re;
+      Jn = J + 2;
+    } else {
+      Jn = J + 1;  // W_{m-1} done
+    }
+    __syncthreads();
+  }
+  if (Jn + 1 < m) {
+    // coefficients of the pass at Jn
+    const int j = Jn;
+    const double sig = ps->sigma;
+    const cplx cjj = ps->C[j][j];
+    // lw = -C[j][j] H[:, :j] D[:j, j]   (the W part of L W_j besides C[j][j] L S_j)
+    for (int k = t; k <= j; k += NTHREADS) {
+      cplx v = {0.0, 0.0};
+      for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) v += cmul(ps->H[k][i], ps->D[i][j]);
+      v = cmul(cjj, v);
+      lw[k] = {-v.re, -v.im};
+    }
+    __syncthreads();
+    for (int k = t; k <= j; k += NTHREADS) {
+      cplx v = lw[k];
+      if (k == j) v.re -= sig;
+      if (k < j) v = v - cconj(ps->H[j][k]);
+      xw[k] = v;
+    }
+    __syncthreads();
+    // zw = H[:, :j] xw[:j] + xw[j] lw - sigma xw
+    for (int k = t; k <= j; k += NTHREADS) {
+      cplx v = {0.0, 0.0};
+      for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) v += cmul(ps->H[k][i], xw[i]);
+      v += cmul(xw[j], lw[k]);
+      v = v - sig * xw[k];
+      zw[k] = v;
+    }
+    __syncthreads();
+    // S-basis coefficients a = C w
+    for (int l = t; l <= j; l += NTHREADS) {
+      cplx ax = {0.0, 0.0}, az = {0.0, 0.0};
+      for (int k = l; k <= j; ++k) {
+        ax += cmul(ps->C[l][k], xw[k]);
+        az += cmul(ps->C[l][k], zw[k]);
+      }
+      ps->aX[l] = ax;
+      ps->aZ[l] = az;
+    }
+    if (t == 0) {
+      ps->bX1 = cjj;
+      ps->bZ1 = cmul(xw[j], cjj) - sig * cjj;
+      ps->bZ2 = cjj;
+    }
+  } else if (t < MMAX) {
+    // T as the reference builds it (alpha_j, j < m-1; norms; T[m-1][m-1] = 0 set by
+    // k_reduce_final), s[] = 1 so that k_reduce_final's fin is c = Q f(Lambda) Q^T e_1
+    if (t < m - 1) {
+      st->Td[t] = ps->H[t][t].re;
+      st->To[t] = ps->H[t + 1][t].re;
+    }
+    st->s[t] = 1.0;
+  }
+}
+
+// fin (W basis, from k_reduce_final) -> S basis: fin_S = beta C fin_W
+__global__ __launch_bounds__(NTHREADS) void k_p2fin(const P2State *__restrict__ ps,
+                                                    KState *__restrict__ st, int m, int nf) {
+  __shared__ cplx fw[2][MMAX];
+  const int t = threadIdx.x;
+  for (int e = t; e < nf * m; e += NTHREADS) fw[e / m][e % m] = st->fin[e / m][e % m];
+  __syncthreads();
+  for (int e = t; e < nf * m; e += NTHREADS) {
+    const int f = e / m, l = e % m;
+    cplx v = {0.0, 0.0};
+    for (int i = l; i < m; ++i) v += cmul(ps->C[l][i], fw[f][i]);
+    st->fin[f][l] = ps->beta * v;
+  }
+}
+
+}  // namespace nls

@@ -1,0 +1,65 @@
+"""GPU parity of the two-vectors-per-pass Lanczos (NLS_PASS2=1, nls_pass2.hpp):
+3D isotropic NLSE trajectories and single Krylov actions against the CPU oracle,
+with the same tolerances as tests/test_gpu_parity.py.  The pass runs on tiles
+of 64 x 16 cells, so the grids have nx % 64 == 0 and ny % 16 == 0."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import rel_l2
+from test_gpu_parity import soliton_field, spacing
+
+pytestmark = pytest.mark.gpu
+
+nls_amd = pytest.importorskip("nls_amd")
+
+TOL_KRYLOV, TOL_TRAJ = 1e-12, 1e-10
+
+
+@pytest.fixture(autouse=True)
+def _pass2(monkeypatch):
+    monkeypatch.setenv("NLS_PASS2", "1")
+    monkeypatch.setenv("NLS_P2_KZ", "8")  # several z chunks per column of tiles
+
+
+def _ran_pass2(s, m):
+    """k_pass2 launches are timed at even J only; the plain path times every j."""
+    t = s.timing()
+    cnt = t["update_count"]
+    return cnt[0] > 0 and all(cnt[j] == 0 for j in range(1, m - 1, 2))
+
+
+@pytest.mark.parametrize("nx,ny,nz,m", [(64, 16, 12, 16), (64, 32, 20, 10), (128, 16, 9, 15),
+                                        (64, 16, 16, 25), (64, 16, 10, 3), (64, 48, 8, 4)])
+@pytest.mark.parametrize("eq", [0, 1])
+def test_pass2_trajectory_matches_oracle(nx, ny, nz, m, eq):
+    L = 10.0
+    dx = spacing(nx, L)
+    u0 = soliton_field(3, nx, ny, nz, L, seed=11)
+    u0 = u0 / np.sqrt(np.sum(np.abs(u0) ** 2) * dx ** 3)
+    g = O.grid(3, nx, ny, nz, dx, dx)
+    dt, nsteps = 1e-3, 10
+    ref = O.nlse_steps(g, u0, dt, nsteps, m, nonlin=eq)
+    with nls_amd.Solver(3, nx, ny, nz, dx, dx, equation=eq, m=m) as s:
+        s.set_field(u0)
+        s.set_timing(True)
+        s.step(dt, nsteps)
+        u = s.get_field()
+        assert _ran_pass2(s, m)
+    assert np.all(np.isfinite(u))
+    assert rel_l2(u, ref) <= TOL_TRAJ
+
+
+def test_pass2_one_step_matches_plain_path(monkeypatch):
+    nx, ny, nz, m = 64, 32, 16, 16
+    L = 10.0
+    dx = spacing(nx, L)
+    u0 = soliton_field(3, nx, ny, nz, L, seed=5)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("NLS_PASS2", mode)
+        with nls_amd.Solver(3, nx, ny, nz, dx, dx, m=m) as s:
+            s.set_field(u0)
+            s.step(1e-3, 1)
+            out[mode] = s.get_field()
+    assert rel_l2(out["1"], out["0"]) <= 1e-12
