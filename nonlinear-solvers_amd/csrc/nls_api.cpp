@@ -233,7 +233,7 @@ void harvest_timing(nls_handle *h) {
 }
 
 void launch(nls_handle *h, int cls, int j, const void *fn, int grid, void **args,
-            hipStream_t stream = nullptr) {
+            hipStream_t stream = nullptr, int block = NTHREADS) {
   if (!fn) fail(h, NLS_ERR_ARG, "kernel variant not instantiated");
   if (!stream) stream = h->stream;
   TimingRec rec{cls, j, nullptr, nullptr};
@@ -243,7 +243,7 @@ void launch(nls_handle *h, int cls, int j, const void *fn, int grid, void **args
     rec.b = get_event(h);
     hip_check(h, hipEventRecord(rec.a, stream), "hipEventRecord");
   }
-  hip_check(h, hipLaunchKernel(fn, dim3(grid), dim3(NTHREADS), args, 0, stream),
+  hip_check(h, hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, stream),
             "hipLaunchKernel");
   if (h->timing) {
     hip_check(h, hipEventRecord(rec.b, stream), "hipEventRecord");
@@ -634,7 +634,7 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
     const bool hz = J + 2 < m;
     int nb = h->p2grid;
     void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb};
-    launch(h, 1, J, kernel_pass2(J, hz), h->p2grid, args);
+    launch(h, 1, J, kernel_pass2(J, hz), h->p2grid, args, nullptr, P2_THREADS);
     const cplx *pA = nullptr;
     int nbA = 0, ncA = 0, ncU = hz ? 2 * J + 5 : J + 2;
     void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
@@ -736,7 +736,8 @@ void alloc_all(nls_handle *h) {
   h->pass2 = false;
   if (const char *e = std::getenv("NLS_PASS2"); e && std::atoi(e) != 0)
     h->pass2 = c && !ani && dim == 3 && !h->collective && h->nbasis == 1 && g.nx % 64 == 0 &&
-               g.nyp % P2_TILE_Y == 0 && h->m >= 3 && h->m <= MMAX;
+               g.nyp % P2_TILE_Y == 0 && h->m >= 3 && h->m <= MMAX &&
+               g.nloc + 2 * g.P < (int64_t(1) << 31);  // k_pass2's 32-bit cell indices
   if (h->pass2) {
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
     const int64_t nzc = (g.npl + h->p2kz - 1) / h->p2kz;

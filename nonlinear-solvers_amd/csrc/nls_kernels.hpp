@@ -65,6 +65,10 @@ const void *kernel_p2fin();
 size_t p2state_bytes();
 size_t p2state_sums_offset();
 constexpr int P2_TILE_Y = 16;  // == P2_TY
+#ifndef NLS_P2_NT
+#define NLS_P2_NT 256
+#endif
+constexpr int P2_THREADS = NLS_P2_NT;  // == P2_NT (k_pass2's workgroup)
 
 // pointwise (grid-stride):
 //   nl_init   : (const cplx* u, cplx* w0, const double* mf, int64_t n, double dt, int nonlin,

@@ -1,0 +1,11 @@
+#!/bin/bash
+# pass2 vs default at 512^3: parity tests, bench lines, per-J pass times
+set -e
+O=gpurun_out/p2
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_pass2.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 4 --warmup 1 > $O/base.json 2>&1
+NLS_PASS2=1 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 4 --warmup 1 > $O/p2.json 2>&1
+NLS_PASS2=1 timeout -k 10 200 python tools/perj.py nlse3d_512 > $O/perj_p2.json
+NLS_PASS2=1 NLS_P2_KZ=64 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 4 --warmup 1 > $O/p2kz64.json 2>&1
