@@ -111,7 +111,8 @@ struct nls_handle {
   bool pass2 = false;
   void *p2 = nullptr;          // P2State
   cplx *partP2 = nullptr;      // per-workgroup partials of k_pass2
-  int p2grid = 0, p2kz = 32;
+  int p2grid = 0, p2kz = 64;
+  bool p2reg = true;           // register-march k_pass2r (NLS_P2_IMPL=0: the LDS form)
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
@@ -607,6 +608,14 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   reduce_final(h, b, nf, f0, f1, tr, ti);
 }
 
+// k_pass2r grid: one wave per 60 x rb output column of kz planes, 4 waves per workgroup
+int p2r_grid(const nls_handle *h, int rb) {
+  const Geo &g = h->geo;
+  const int64_t nzc = (g.npl + h->p2kz - 1) / h->p2kz;
+  const int64_t waves = ((g.nx + P2R_WAVE_XO - 1) / P2R_WAVE_XO) * (g.nyp / rb) * nzc;
+  return (int)((waves + NTHREADS / 64 - 1) / (NTHREADS / 64));
+}
+
 // Two new vectors per pass (nls_pass2.hpp): the alpha pass + reduction of W_0
 // give beta and alpha_0 (the first shift); then passes at J = 0, 2, 4, ... each
 // followed by its column sums and k_p2coef; the eigensolve on the resulting T;
@@ -632,9 +641,10 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
   int J = 0;
   while (J + 1 < m) {
     const bool hz = J + 2 < m;
-    int nb = h->p2grid;
+    int nb = h->p2reg ? p2r_grid(h, P2R_ROWS(J)) : h->p2grid;
     void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb};
-    launch(h, 1, J, kernel_pass2(J, hz), h->p2grid, args, nullptr, P2_THREADS);
+    launch(h, 1, J, kernel_pass2(J, hz, h->p2reg), nb, args, nullptr,
+           h->p2reg ? NTHREADS : P2_THREADS);
     const cplx *pA = nullptr;
     int nbA = 0, ncA = 0, ncU = hz ? 2 * J + 5 : J + 2;
     void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
@@ -740,8 +750,13 @@ void alloc_all(nls_handle *h) {
                g.nloc + 2 * g.P < (int64_t(1) << 31);  // k_pass2's 32-bit cell indices
   if (h->pass2) {
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("NLS_P2_IMPL")) h->p2reg = std::atoi(e) != 0;
     const int64_t nzc = (g.npl + h->p2kz - 1) / h->p2kz;
-    h->p2grid = (int)((g.nx / 64) * (g.nyp / P2_TILE_Y) * nzc);
+    if (h->p2reg) {  // one wave per 60 x RB output column, 4 waves per workgroup (grid at RB = 1)
+      h->p2grid = p2r_grid(h, 1);
+    } else {
+      h->p2grid = (int)((g.nx / 64) * (g.nyp / P2_TILE_Y) * nzc);
+    }
     hip_check(h, hipMalloc(&h->p2, p2state_bytes()), "hipMalloc(p2)");
     hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes(), h->stream), "hipMemset");
     hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (2 * MMAX + 8) * sizeof(cplx)),

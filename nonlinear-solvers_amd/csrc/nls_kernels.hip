@@ -818,11 +818,13 @@ const void *kernel_sg_end(int M) {
 }
 
 // two-vectors-per-pass Lanczos (nls_pass2.hpp): even J only
-const void *kernel_pass2(int J, bool hz) {
+const void *kernel_pass2(int J, bool hz, bool reg) {
   switch (J) {
 #define X(J) \
-  case J: return hz ? reinterpret_cast<const void *>(&k_pass2<J, true>) \
-                    : reinterpret_cast<const void *>(&k_pass2<J, false>);
+  case J: return reg ? (hz ? reinterpret_cast<const void *>(&k_pass2r<J, true>) \
+                           : reinterpret_cast<const void *>(&k_pass2r<J, false>)) \
+                     : (hz ? reinterpret_cast<const void *>(&k_pass2<J, true>) \
+                           : reinterpret_cast<const void *>(&k_pass2<J, false>));
     X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30)
 #undef X
     default: return nullptr;

@@ -59,7 +59,12 @@ const void *kernel_reduce_final();
 //                  grid = ncA + ncU columns; dst = KState::sums (the do_sum phase, parallel)
 const void *kernel_colsum();
 // two-vectors-per-pass Lanczos (nls_pass2.hpp; 3D isotropic complex, single rank)
-const void *kernel_pass2(int J, bool hz);  // hz: also the second vector Z
+const void *kernel_pass2(int J, bool hz, bool reg);  // hz: also Z; reg: register-march form
+constexpr int P2R_WAVE_XO = 60;  // == P2R_XO
+#ifndef NLS_P2R_RB1
+#define NLS_P2R_RB1 12  // k_pass2r: one row per wave from this J (registers)
+#endif
+#define P2R_ROWS(J) ((J) >= NLS_P2R_RB1 ? 1 : 2)  // == p2r_rb(J)
 const void *kernel_p2coef();
 const void *kernel_p2fin();
 size_t p2state_bytes();

@@ -1,7 +1,8 @@
 """GPU parity of the two-vectors-per-pass Lanczos (NLS_PASS2=1, nls_pass2.hpp):
 3D isotropic NLSE trajectories and single Krylov actions against the CPU oracle,
-with the same tolerances as tests/test_gpu_parity.py.  The pass runs on tiles
-of 64 x 16 cells, so the grids have nx % 64 == 0 and ny % 16 == 0."""
+with the same tolerances as tests/test_gpu_parity.py, for both forms of the
+pass (register march k_pass2r, LDS tiles k_pass2).  The LDS form runs on tiles of
+64 x 16 cells, so the grids have nx % 64 == 0 and ny % 16 == 0."""
 import numpy as np
 import pytest
 
@@ -16,10 +17,11 @@ nls_amd = pytest.importorskip("nls_amd")
 TOL_KRYLOV, TOL_TRAJ = 1e-12, 1e-10
 
 
-@pytest.fixture(autouse=True)
-def _pass2(monkeypatch):
+@pytest.fixture(autouse=True, params=["reg", "lds"])
+def _pass2(monkeypatch, request):
     monkeypatch.setenv("NLS_PASS2", "1")
     monkeypatch.setenv("NLS_P2_KZ", "8")  # several z chunks per column of tiles
+    monkeypatch.setenv("NLS_P2_IMPL", "1" if request.param == "reg" else "0")
 
 
 def _ran_pass2(s, m):
