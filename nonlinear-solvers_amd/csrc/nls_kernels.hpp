@@ -64,7 +64,7 @@ constexpr int P2R_WAVE_XO = 60;  // == P2R_XO
 #ifndef NLS_P2R_RB1
 #define NLS_P2R_RB1 12  // k_pass2r: one row per wave from this J (registers)
 #endif
-#define P2R_ROWS(J) ((J) >= NLS_P2R_RB1 ? 1 : 2)  // == p2r_rb(J)
+#define P2R_ROWS(J) (((J) == 4 || (J) >= NLS_P2R_RB1) ? 1 : 2)  // 512^3: J=4 3.92 vs 4.90 ms with one row
 const void *kernel_p2coef();
 const void *kernel_p2fin();
 size_t p2state_bytes();

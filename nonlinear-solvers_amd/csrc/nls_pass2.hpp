@@ -227,7 +227,7 @@ __global__ __launch_bounds__(P2_NT) void k_pass2(cplx *__restrict__ W, int64_t v
 // planes k-1..k+1, L S_J on rows -1..RB for planes k-2..k.  Step k loads
 // S_J(k+1) and the J other streams of plane k-1, forms L S_J(k), then
 // L^2 S_J(k-1) and the outputs of plane k-1.
-constexpr int p2r_rb(int J) { return J >= NLS_P2R_RB1 ? 1 : 2; }  // rows per wave (registers)
+constexpr int p2r_rb(int J) { return P2R_ROWS(J); }  // rows per wave (registers; measured per J)
 constexpr int P2R_XO = 60;  // output x per wave
 template <int J, bool HZ>
 __global__ __launch_bounds__(NTHREADS) void k_pass2r(cplx *__restrict__ W, int64_t vs, Geo g,

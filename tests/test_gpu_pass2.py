@@ -52,9 +52,9 @@ def test_pass2_trajectory_matches_oracle(nx, ny, nz, m, eq):
     assert rel_l2(u, ref) <= TOL_TRAJ
 
 
-def test_pass2_one_step_matches_plain_path(monkeypatch):
+@pytest.mark.parametrize("L", [10.0, 0.6])  # ||L|| ~ 1e2 and ~ 3e4 (the 512^3 bench's dx is 0.039)
+def test_pass2_one_step_matches_plain_path(monkeypatch, L):
     nx, ny, nz, m = 64, 32, 16, 16
-    L = 10.0
     dx = spacing(nx, L)
     u0 = soliton_field(3, nx, ny, nz, L, seed=5)
     out = {}

@@ -1,10 +1,10 @@
 #!/bin/bash
-# pass2 vs default at 512^3, alternating on one box (bench lines) + per-J pass times
+# Round-end check: full GPU suite, then default vs two-vector pass (J=4 one-row waves) at 512^3
 set -e
-O=gpurun_out/p2b
+O=gpurun_out/p2c
 mkdir -p $O
 rm -f $O/*.json
-timeout -k 10 300 python -u -m pytest tests/test_gpu_pass2.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for i in 1 2; do
 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 4 --warmup 1 > $O/base$i.json 2>&1
