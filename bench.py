@@ -9,10 +9,13 @@ HBM before the timed region.  With --gpus N (launched by torch.distributed.run)
 the 512^3 grid is z-slab decomposed over N ranks (strong scaling) with RCCL halo
 exchange + all-reduce of the Lanczos dot products.
 
-roofline: the dominant kernel is k_update<J=m-2> (the Lanczos update pass that
-streams J+1 basis vectors and writes one): algorithmic bytes per launch =
-(J+2) * 16 B * cells, timed with HIP events on the
-solver's own stream over the timed region.
+roofline: the dominant kernel is the fused tail k_tail<NLSE, m> (the last
+Lanczos vector + combination + both nonlinear half-steps; m-1 basis vectors
+read, u and the next start vector written): algorithmic bytes per launch =
+(m+1) * 16 B * cells, timed with HIP events on the
+solver's own stream in a separate pass of --prof-steps steps right after the
+timed region (the timed region itself carries no per-launch events).
+--gpus N without torch.distributed.run: bench.py starts the N ranks itself.
 cpu_baseline: the oracle (single-threaded C++ restatement of the reference's
 Eigen path, oracle/) on a bounded 128^3 sample of the same workload.
 """
@@ -269,6 +272,39 @@ def _claim_stdout():
     return os.fdopen(saved, "w")
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def rank_launch_cmd(n: int, argv, port: int):
+    """The command `python bench.py --gpus N ...` runs when started without
+    torch.distributed.run: the same launcher line the driver uses, one rank per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n: int, argv):
+    """Run the N ranks as children; return (exit code, rank 0's JSON line or None).
+    Children's stderr passes through; their stdout (only rank 0 prints, one line)
+    is scanned for the result line."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    p = subprocess.run(rank_launch_cmd(n, argv, free_port()), stdout=subprocess.PIPE, env=env, text=True)
+    line = None
+    for ln in p.stdout.splitlines():
+        ln = ln.strip()
+        if ln.startswith("{") and '"metric"' in ln:
+            line = ln
+        elif ln:
+            print(ln, file=sys.stderr)
+    return p.returncode, line
+
+
 def main():
     out = _claim_stdout()
     ap = argparse.ArgumentParser()
@@ -279,15 +315,23 @@ def main():
     ap.add_argument("--n", type=int, default=None, help="override grid side (testing only)")
     ap.add_argument("--m", type=int, default=None, help="override Krylov dim (testing only)")
     ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--prof-steps", type=int, default=5,
+                    help="steps of the separate per-kernel timing pass (after the timed region)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # not started by torch.distributed.run: start the N ranks ourselves (before
+        # anything touches the GPU) and forward rank 0's JSON line
+        rc, line = launch_ranks(args.gpus, sys.argv[1:])
+        if line:
+            print(line, file=out, flush=True)
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
@@ -343,20 +387,24 @@ def main():
     if args.warmup:
         run(args.warmup)
     s.sync()
-    s.reset_timing()
-    s.set_timing(True)
     if dist is not None:
         dist.barrier()
     s.sync()
     t0 = time.perf_counter()
-    run(args.steps)
+    run(args.steps)   # the timed region: no per-launch events
     s.sync()
     if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t0
+    el = max_over_ranks(el, dist)
+    # per-kernel times (roofline) from a separate, untimed pass with HIP events
+    # around every launch on the solver's own streams
+    s.reset_timing()
+    s.set_timing(True)
+    run(max(1, args.prof_steps))
+    s.sync()
     tm = s.timing()
     s.set_timing(False)
-    el = max_over_ranks(el, dist)
     cells_total = n ** dim
     value = cells_total * args.steps / el / 1e6
     n_local = s.n_local
@@ -402,7 +450,9 @@ def main():
         "config": {"workload": w["desc"], "grid": [n] * dim, "krylov_m": m, "dt": dt,
                    "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi", "nlse_g2", "kg_gautschi"][w["eq"]]
                    + ("_sewi" if w.get("sewi") else ""),
-                   "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
+                   "parallelism": f"z-slab x{world}" if world > 1 else "single GPU",
+                   "ranks": {"world": world, "transport": "rccl" if world > 1 else "none",
+                             "slab_planes_rank0": int(s.nzl)}},
         "roofline": {
             "bound": "hbm",
             "kernel": kname,
@@ -413,6 +463,7 @@ def main():
             "traffic": traffic,
             "bytes_per_launch": bytes_launch,
             "avg_launch_ms": avg_ms,
+            "timed_in": f"separate {max(1, args.prof_steps)}-step pass with HIP events (not the timed region)",
         },
         "step_roofline": {
             "algorithmic_bytes_per_cell_step": algorithmic_bytes_per_cell_step(m, w["eq"], w.get("sewi", False)),

@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define NLS_ABI_VERSION 3
+#define NLS_ABI_VERSION 4
 #define NLS_MAX_KRYLOV 32
 
 enum nls_status {
@@ -77,10 +77,22 @@ enum nls_equation {
                            div(c grad): SS2 with exp(+tau/2 m|u|^2) and exp(tau*lambda)
                            (nlsolvers/device/include/nlse_dev.hpp:187-203,
                            nlsolvers/device/drivers/nlse_cubic_driver_{2d,3d}.cpp) */
-  NLS_KG_GAUTSCHI = 4   /* G2 Klein-Gordon u_tt = div(c grad u) - m u^3, Gautschi with
+  NLS_KG_GAUTSCHI = 4,  /* G2 Klein-Gordon u_tt = div(c grad u) - m u^3, Gautschi with
                            cos / sinc^2 of t sqrt|lambda| (nlsolvers/device/include/kg_single.cuh:49-86,
                            kg_driver_dev_{2d,3d}.cpp); real field; m, c via
                            nls_set_coefficients, u / u_past via nls_set_sg_state */
+  /* G2 device Gautschi family (nlsolvers/device/include/{sg_single,sg_double,
+     sg_hyperbolic,phi4_single}.cuh, drivers {sg_single,sg_double,sg_hyperbolic,
+     phi4}_driver_dev.cpp): u_tt = Lap u - m F(u) on the isotropic operator
+     (laplacians.hpp:10-52 / :55-105), step
+       y = id(u), g = -m F(y), s = sinc^2(t sqrt|L|) g, c = cos(t sqrt|L|) u,
+       u+ = 2c - u- + tau^2 s      (id, cos, sinc^2 of t sqrt|lambda|, t = tau = dt)
+     with F per equation below; real field; u, u_past, m via nls_set_sg_state;
+     Neumann copy BC on u after each step via nls_apply_bc (the drivers' apply_bc). */
+  NLS_SG_G2 = 5,           /* F = sin u                sg_single.cuh:14-20 */
+  NLS_SG_DOUBLE = 6,       /* F = sin u + sin(u/2)     sg_double.cuh:14-21 */
+  NLS_SG_HYPERBOLIC = 7,   /* F = sinh u               sg_hyperbolic.cuh:14-20 */
+  NLS_PHI4 = 8             /* F = u + u^3              phi4_single.cuh:14-20 */
 };
 
 /* Krylov matrix functions f, applied as f(L) u (nls_krylov_apply) */

@@ -92,6 +92,7 @@ struct nls_handle {
   double *cfb = nullptr;    // G2 anisotropy c(x): (nzl + 2) planes, local plane 0 at +P
   bool ani = false;         // G2 operator div(c grad) (laplacians.hpp:54-218)
   bool kg = false;          // G2 Klein-Gordon Gautschi (real, ani)
+  int gfun = -1;            // G2 Gautschi family (NLS_SG_G2 .. NLS_PHI4): GautschiForce; -1 G1 sine-Gordon
   double *vel = nullptr;    // KG velocity v = (u - u_past)/dt of the last step
   bool vel_valid = false;   //   (set by every KG step, before the driver's BC)
   bool u_slot = false;      // u stored as slot nvec[0] of basis 0
@@ -789,7 +790,7 @@ void alloc_all(nls_handle *h) {
       if (ok) h->nvec[0] = h->m - 1;
     } else if (h->kg) {
       if (has(TAIL_KG_END)) h->nvec[0] = h->m - 1;  // the sinc^2 basis is stored in full
-    } else if (has(TAIL_SG_MID) && has(TAIL_SG_END) && has(TAIL_COMBINE)) {
+    } else if (has(h->gfun >= 0 ? TAIL_GG_MID : TAIL_SG_MID) && has(TAIL_SG_END) && has(TAIL_COMBINE)) {
       h->nvec[0] = h->nvec[1] = h->m - 1;
     }
   }
@@ -917,6 +918,18 @@ void pw_launch(nls_handle *h, int cls, const void *fn, void **args) {
   launch(h, cls, -1, fn, h->grid_pw, args);
 }
 
+// The stencil kernels index a stored vector with 32-bit ints (nls_stencil.hpp
+// march: p = q * P + off over the ghost planes -P .. (nzl + 1) * P, tile counts);
+// the largest slab (rank 0, nls_slab_planes) must stay below 2^31 elements incl.
+// the ghost planes and the stride pad.  Checked before any allocation.
+bool slab_index_limit_exceeded(const nls_config &c) {
+  const uint64_t npl = c.dim == 3 ? c.nz : c.ny;
+  const uint64_t P = c.dim == 3 ? (uint64_t)c.nx * c.ny : (uint64_t)c.nx;
+  uint32_t z0 = 0, nzl = 0;
+  if (nls_slab_planes((uint32_t)npl, c.nranks, 0, &z0, &nzl) != NLS_OK) return true;
+  return ((uint64_t)nzl + 2) * P + 4096 >= (uint64_t(1) << 31);
+}
+
 }  // namespace
 
 // ============================================================================
@@ -950,7 +963,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   const nls_config &c = *cfg;
   std::string why;
   if (c.dim != 2 && c.dim != 3) why = "dim must be 2 or 3";
-  else if (c.equation < 0 || c.equation > 4) why = "unknown equation";
+  else if (c.equation < 0 || c.equation > NLS_PHI4) why = "unknown equation";
   else if (c.equation == NLS_SG_GAUTSCHI && c.dim != 2 && c.dim != 3) why = "bad dim";
   else if (c.nx < 2 || c.ny < 2 || (c.dim == 3 && c.nz < 2)) why = "grid too small (need >= 2 per dimension)";
   else if (!(c.dx > 0.0) || !(c.dy > 0.0)) why = "dx, dy must be > 0";
@@ -966,6 +979,9 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   else if ((c.equation == NLS_NLSE_G2 || c.equation == NLS_KG_GAUTSCHI) &&
            (uint32_t)(2 * c.nranks) > (c.dim == 3 ? c.nz : c.ny))
     why = "G2 NLSE / KG need >= 2 planes per rank";
+  else if (slab_index_limit_exceeded(c))
+    why = "slab too large for 32-bit cell indices: (planes per rank + 2) * plane size + 4096 must be "
+          "< 2^31 (use more ranks)";
   if (!why.empty()) {
     g_create_error = why;
     return NLS_ERR_ARG;
@@ -976,7 +992,8 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
     return NLS_ERR_OOM;
   }
   h->cfg = c;
-  h->cplx_ = c.equation != NLS_SG_GAUTSCHI && c.equation != NLS_KG_GAUTSCHI;
+  h->gfun = (c.equation >= NLS_SG_G2 && c.equation <= NLS_PHI4) ? c.equation - NLS_SG_G2 : -1;
+  h->cplx_ = c.equation != NLS_SG_GAUTSCHI && c.equation != NLS_KG_GAUTSCHI && h->gfun < 0;
   h->esize = h->cplx_ ? 16 : 8;
   h->m = (int)c.krylov_m;
   h->nbasis = h->cplx_ ? 1 : 2;
@@ -1151,14 +1168,16 @@ int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfie
 
 int nls_apply_bc(nls_handle *h) {
   return guarded(h, [&] {
-    if (!h->cplx_ && !h->kg) fail(h, NLS_ERR_STATE, "nls_apply_bc on a G1 sine-Gordon handle");
+    if (!h->cplx_ && !h->kg && h->gfun < 0) fail(h, NLS_ERR_STATE, "nls_apply_bc on a G1 sine-Gordon handle");
     if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
     const Geo &g = h->geo;
     if (g.nx < 3 || g.npl < 3 || (h->cfg.dim == 3 && g.nyp < 3))
       fail(h, NLS_ERR_ARG, "Neumann copy boundary needs >= 3 cells per dimension");
     if ((g.z0 == 0 || g.z0 + g.nzl == g.npl) && g.nzl < 2)
       fail(h, NLS_ERR_ARG, "Neumann copy boundary needs >= 2 planes on the boundary slabs");
-    if (h->kg) {  // KGESolverDevice::apply_bc: u only (nlsolvers/device/include/kg_dev.hpp)
+    // KGESolverDevice::apply_bc (nlsolvers/device/include/kg_dev.hpp) and the G2
+    // Gautschi family's apply_bc (e.g. phi4_dev.hpp:92): u only
+    if (!h->cplx_) {
       void *u = vec_ptr(h, 0, 0);
       Geo gg = g;
       const int64_t cells = neumann_bc_cells(g);
@@ -1355,24 +1374,29 @@ void issue_step(nls_handle *h, double dt) {
     halo(h, 0, 0);
     h->vel_valid = true;
   } else {
-    // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u
-    bool tail = use_tail(h, TAIL_SG_MID);
+    // SGESolver::step (sg_solver.hpp:53-74): id and cos share the basis of u.
+    // G2 Gautschi family (e.g. phi4_single.cuh:33-47): the same sequence with
+    // g = -m F(id u) and sinc^2(t sqrt|lambda|) instead of the G1 half argument.
+    const int mid = h->gfun >= 0 ? TAIL_GG_MID : TAIL_SG_MID;
+    bool tail = use_tail(h, mid);
     run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0, tail);
     if (tail) {
       TailArgs ta = tail_args(h, 0);
       ta.out = vec_ptr(h, 1, 0);
       ta.up = h->up;
-      tail_launch(h, TAIL_SG_MID, ta);
+      ta.nonlin = h->gfun;
+      tail_launch(h, mid, ta);
     } else {
       void *W = vec_ptr(h, 0, 0);
       void *g0 = vec_ptr(h, 1, 0);
       KState *st = h->B[0].st;
-      void *args[] = {&W, &vs, (void *)&n, &st, &h->mf, &h->up, &g0};
+      int gf = h->gfun;
+      void *args[] = {&W, &vs, (void *)&n, &st, &h->mf, &h->up, &g0, &gf};
       pw_launch(h, 3, kernel_sg_mid(m), args);
     }
     halo(h, 1, 0);
     tail = use_tail(h, TAIL_SG_END);
-    run_lanczos(h, 1, 1, NLS_F_SINC2_HALF, 0, dt, 0.0, tail);
+    run_lanczos(h, 1, 1, h->gfun >= 0 ? NLS_F_SINC2_SQRT : NLS_F_SINC2_HALF, 0, dt, 0.0, tail);
     if (tail) {
       TailArgs ta = tail_args(h, 1);
       ta.u = vec_ptr(h, 0, 0);

@@ -115,6 +115,33 @@ __device__ __forceinline__ void nl_sincos(double x, double &sn, double &cs) {
   cs = q == 0 ? c : q == 1 ? -s : q == 2 ? -c : s;
 }
 
+// g = -m F(y) of the G2 Gautschi family (GautschiForce, nls_device.hpp):
+// sg_single.cuh:18, sg_double.cuh:19, sg_hyperbolic.cuh:18, phi4_single.cuh:18.
+// sin via the register-light nl_sincos; sinh from one exp (|y| >= 2^-5) or its
+// Taylor series (below, where exp(y) - exp(-y) would cancel).
+__device__ __forceinline__ double gg_force(double y, int kind) {
+  double sn, cs;
+  switch (kind) {
+    case 1: {
+      double s2, c2;
+      nl_sincos(y, sn, cs);
+      nl_sincos(0.5 * y, s2, c2);
+      return sn + s2;
+    }
+    case 2: {
+      const double a = fabs(y);
+      if (a < 0.03125) {
+        const double z = y * y;
+        return y + y * z * (1.0 / 6.0 + z * (1.0 / 120.0 + z * (1.0 / 5040.0 + z * (1.0 / 362880.0))));
+      }
+      const double e = exp(a);
+      return copysign(0.5 * (e - 1.0 / e), y);
+    }
+    case 3: return y + y * y * y;
+    default: nl_sincos(y, sn, cs); return sn;
+  }
+}
+
 __device__ __forceinline__ cplx nl_half(cplx u, double mval, double dt, int nonlin, cplx s1, cplx s2) {
   if (nonlin == 0 || nonlin == 2) {
     const double x = u.re * u.re + u.im * u.im;

@@ -93,8 +93,15 @@ enum TailMode {
   TAIL_COMBINE_W0 = 4,  // W_0 <- y                                  (k_combine_w0; sEWI)
   TAIL_COMBINE = 5,     // out <- y                                  (k_combine; sEWI)
   TAIL_SEWI_END = 6,    // u <- y - 2 tau e; up <- old u             (k_sewi_end; nlse_dev.hpp:52-63)
+  TAIL_GG_MID = 7,      // g_0 = -m F(y_id) (F by TailArgs::nonlin, gg_force); up <- 2 y_cos - up
+                        //   (G2 Gautschi family, e.g. phi4_single.cuh:33-47)
 };
-constexpr int tail_nf(int mode) { return mode == TAIL_SG_MID ? 2 : 1; }
+constexpr int tail_nf(int mode) { return (mode == TAIL_SG_MID || mode == TAIL_GG_MID) ? 2 : 1; }
+
+// Nonlinearity F of the G2 Gautschi family (g = -m F(id u)):
+//   0 sin u (sg_single.cuh:18), 1 sin u + sin(u/2) (sg_double.cuh:19),
+//   2 sinh u (sg_hyperbolic.cuh:18), 3 u + u^3 (phi4_single.cuh:18)
+enum GautschiForce { GG_SIN = 0, GG_SIN_DOUBLE = 1, GG_SINH = 2, GG_PHI4 = 3 };
 
 struct TailArgs {
   void *W;              // the tail basis (local plane 0 of W_0)

@@ -654,7 +654,7 @@ __global__ __launch_bounds__(NTHREADS) void k_sg_mid(const double *__restrict__ 
                                                      const KState *__restrict__ st,
                                                      const double *__restrict__ mf,
                                                      double *__restrict__ up,
-                                                     double *__restrict__ g0) {
+                                                     double *__restrict__ g0, int gfun) {
   double ci[M], cc[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) {
@@ -670,7 +670,8 @@ __global__ __launch_bounds__(NTHREADS) void k_sg_mid(const double *__restrict__ 
       yi += ci[k] * w;
       yc += cc[k] * w;
     }
-    st_nt(g0 + p, mf[p] * (-sin(yi)));
+    // G1 (gfun < 0): m (-sin y) (sg_solver.hpp:65-69); G2 family: -m F(y) (gg_force)
+    st_nt(g0 + p, gfun < 0 ? mf[p] * (-sin(yi)) : -mf[p] * gg_force(yi, gfun));
     st_nt(up + p, 2 * yc - up[p]);
   }
 }

@@ -84,7 +84,7 @@ constexpr int P2_THREADS = NLS_P2_NT;  // == P2_NT (k_pass2's workgroup)
 //                cplx s1, cplx s2)   -- boundary cells only (grid over neumann_bc_cells())
 //   combine   : (const S* W, int64_t vs, int64_t n, const KState*, S* out)
 //   sg_mid    : (const double* W, int64_t vs, int64_t n, const KState*, const double* mf,
-//                double* up, double* g0)
+//                double* up, double* g0, int gfun)   (gfun < 0: G1 m(-sin y); else -m F(y), GautschiForce)
 //   sg_end    : (const double* W2, int64_t vs, int64_t n, const KState*, double* u, double* up,
 //                double dt)
 //   sg_velocity: (const double* u, const double* up, double* v, int64_t n, double dt)

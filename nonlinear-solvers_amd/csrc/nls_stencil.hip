@@ -35,8 +35,9 @@ template <class S> const void *update_fn(int code) {
     default: return nullptr;
   }
 }
-// tail kernels: J encodes mode * 64 + M.  G1 (iso) tables hold the NLSE and
-// sine-Gordon tails, G2 (ani) tables the NLSE, Klein-Gordon and sEWI tails.
+// tail kernels: J encodes mode * 64 + M.  G1 (iso) tables hold the NLSE,
+// sine-Gordon and G2 Gautschi-family tails, G2 (ani) tables the NLSE,
+// Klein-Gordon and sEWI tails.
 template <class S, int MODE> const void *tail_m(int M) {
   switch (M) {
 #define X(M) case M: return reinterpret_cast<const void *>(&k_tail<S, NLS_DIM, M, (NLS_ANI != 0), MODE>);
@@ -64,6 +65,7 @@ const void *tail_fn(bool complex_, int code) {
     case TAIL_KG_END: return tail_m<double, TAIL_KG_END>(M);
 #else
     case TAIL_SG_MID: return tail_m<double, TAIL_SG_MID>(M);
+    case TAIL_GG_MID: return tail_m<double, TAIL_GG_MID>(M);
     case TAIL_SG_END: return tail_m<double, TAIL_SG_END>(M);
 #endif
     default: return nullptr;

@@ -703,6 +703,10 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
         double *__restrict__ up = static_cast<double *>(ta.up);
         st_nt(static_cast<double *>(ta.out) + q, ta.mf[q] * (-sin_rl(to_c(y[0]).re)));
         st_nt(up + q, 2 * to_c(y[1]).re - up[q]);
+      } else if constexpr (MODE == TAIL_GG_MID) {  // e.g. phi4_single.cuh:38-45
+        double *__restrict__ up = static_cast<double *>(ta.up);
+        st_nt(static_cast<double *>(ta.out) + q, -ta.mf[q] * gg_force(to_c(y[0]).re, ta.nonlin));
+        st_nt(up + q, 2 * to_c(y[1]).re - up[q]);
       } else if constexpr (MODE == TAIL_SG_END) {
         double *__restrict__ u = static_cast<double *>(ta.u);
         double *__restrict__ up = static_cast<double *>(ta.up);

@@ -5,7 +5,7 @@
 //
 //   3D: prog nx ny nz Lx Ly Lz u0.npy v0.npy traj_u.npy traj_v.npy T nt num_snapshots m.npy c.npy
 //   2D: prog nx ny Lx Ly u0.npy v0.npy traj_u.npy traj_v.npy T nt num_snapshots m.npy c.npy
-//       [--m=K] [--device=D]   (optional extension flags)
+//       [--m=K] [--device=D] [--true-shape]   (optional extension flags)
 //
 // Semantics kept: float64 inputs; dx = 2 Lx/(nx-1) (scale 1/dx^2 in 3D,
 // 1/(dx*dy) in 2D) on -div(c grad) (the drivers negate the anisotropic
@@ -13,9 +13,11 @@
 // (u0, v0), then for i = 1 .. nt-1: step, apply_bc (u only), and snapshot
 // i / freq when i % freq == 0 (u after the BC, v as the step computed it);
 // the reference's shape checks and messages (2D checks u0 as [nx, ny], m as
-// [ny, nx], c as [nx, ny]).  Differences: the 3D outputs carry the shape
-// [ns, nz, ny, nx] of the data (the reference writes the header [ns, ny, nx]
-// for ns*nz*ny*nx values, kg_driver_dev_3d.cpp:161-163); num_snapshots > nt
+// [ny, nx], c as [nx, ny]); the 3D outputs carry the reference's header
+// [ns, ny, nx] over ns*nz*ny*nx values (kg_driver_dev_3d.cpp:161-163: numpy
+// reads the first ns*ny*nx of them unless the consumer reshapes the raw
+// payload); --true-shape writes the header [ns, nz, ny, nx] of the data
+// instead.  Differences: num_snapshots > nt
 // exits 1 (the reference takes i % 0); failed m / c loads exit 1 after the
 // reference's messages (the reference rethrows into std::terminate).
 #include <iostream>
@@ -129,7 +131,9 @@ int main(int argc, char **argv) {
   }
 #if KG_DIM == 3
   const std::vector<uint64_t> fshape = {nz, ny, nx}, mshape = fshape, cshape = fshape;
-  const std::vector<uint64_t> out_shape = {ns, nz, ny, nx};
+  const bool true_shape = a.flags.count("true-shape") > 0;
+  const std::vector<uint64_t> out_shape =
+      true_shape ? std::vector<uint64_t>{ns, nz, ny, nx} : std::vector<uint64_t>{ns, ny, nx};
 #else
   // kg_driver_dev_2d.cpp:63,77,92 -- consistent only on the square grids the
   // builder asserts (laplacians.hpp:63)
@@ -147,8 +151,9 @@ int main(int argc, char **argv) {
   if (!load_field(c_file, cshape, "c", cfield)) return 1;
 
   try {
-    npy::Writer wu = npy::Writer::open<double>(out_u, out_shape);
-    npy::Writer wv = npy::Writer::open<double>(out_v, out_shape);
+    const uint64_t payload = (uint64_t)ns * nz * ny * nx;
+    npy::Writer wu = npy::Writer::open<double>(out_u, out_shape, payload);
+    npy::Writer wv = npy::Writer::open<double>(out_v, out_shape, payload);
     nls::Grid g;
     g.dim = KG_DIM;
 #if KG_DIM == 3

@@ -323,6 +323,42 @@ class KGESolverDevice {
   std::vector<double> u_, v_;
 };
 
+// G2 device Gautschi family -- SGESolverDevice / SGEDoubleSolverDevice /
+// SGEHyperbolicSolverDevice / Phi4SolverDevice of nlsolvers/device/include/
+// {sg_single,sg_double,sg_hyperbolic,phi4}_dev.hpp as their drivers use them
+// (phi4_driver_dev.cpp:103-118): the ctor stores snapshot 0 = u0 (phi4_dev.hpp:65)
+// and sets u_past = u0 - dt v0 (:43-46); per step i = 1 .. nt-1 the driver calls
+// step(), apply_bc() (u only, :92) and store_snapshot(i / freq) when i % freq == 0.
+// equation: NLS_SG_G2, NLS_SG_DOUBLE, NLS_SG_HYPERBOLIC or NLS_PHI4.
+class GautschiSolverDevice {
+ public:
+  using SnapshotFn = std::function<void(uint32_t index, const double *u, uint64_t n)>;
+  GautschiSolverDevice(const Grid &g, int equation, const double *u0, const double *v0,
+                       const double *mfield, double dt, uint32_t num_snapshots, uint32_t krylov_m,
+                       SnapshotFn cb, int device = -1)
+      : h_(g, equation, krylov_m, device), ns_(num_snapshots), dt_(dt), cb_(std::move(cb)), u_(h_.n()) {
+    std::vector<double> up(h_.n());
+    for (uint64_t i = 0; i < h_.n(); ++i) up[i] = u0[i] - dt * v0[i];
+    check(nls_set_sg_state(h_.get(), u0, up.data(), mfield, h_.n()), h_.get());
+    if (cb_ && ns_ > 0) cb_(0, u0, h_.n());
+  }
+  void step() { check(nls_step(h_.get(), dt_, 1), h_.get()); }
+  void apply_bc() { check(nls_apply_bc(h_.get()), h_.get()); }
+  void store_snapshot(uint32_t idx) {
+    if (idx >= ns_) return;
+    check(nls_get_field(h_.get(), u_.data(), h_.n()), h_.get());
+    if (cb_) cb_(idx, u_.data(), h_.n());
+  }
+  uint64_t n() const { return h_.n(); }
+
+ private:
+  Handle h_;
+  uint32_t ns_;
+  double dt_;
+  SnapshotFn cb_;
+  std::vector<double> u_;
+};
+
 namespace g2 {
 
 // G2 cubic NLSE stepper (nlsolvers/device/include/nlse_dev.hpp:66-361) as the

@@ -49,13 +49,21 @@ class Writer {
  public:
   template <class T>
   static Writer open(const std::string &path, const std::vector<uint64_t> &shape) {
+    uint64_t n = 1;
+    for (auto d : shape) n *= d;
+    return open<T>(path, shape, n);
+  }
+  // header `shape`, payload of `elems` values: the reference's 3D Klein-Gordon
+  // driver writes the header [ns, ny, nx] for ns*nz*ny*nx values
+  // (kg_driver_dev_3d.cpp:161-163; libnpy writes the whole vector)
+  template <class T>
+  static Writer open(const std::string &path, const std::vector<uint64_t> &shape, uint64_t elems) {
     Writer w;
     w.f_ = std::fopen(path.c_str(), "wb");
     if (!w.f_) throw std::runtime_error("cannot open " + path + " for writing");
     const std::string h = make_header(descr<T>(), shape);
     if (std::fwrite(h.data(), 1, h.size(), w.f_) != h.size()) throw std::runtime_error("write failed");
-    w.expect_ = sizeof(T);
-    for (auto d : shape) w.expect_ *= d;
+    w.expect_ = sizeof(T) * elems;
     return w;
   }
   Writer() = default;

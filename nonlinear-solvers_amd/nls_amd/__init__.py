@@ -14,12 +14,16 @@ import os
 import numpy as np
 
 __all__ = [
-    "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "NLSE_G2", "KG_GAUTSCHI", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
+    "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "NLSE_G2", "KG_GAUTSCHI", "SG_G2", "SG_DOUBLE", "SG_HYPERBOLIC",
+    "PHI4", "REAL_EQUATIONS", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
     "F_SINC2_SQRT", "F_ID_SQRT", "F_SINC2_HALF", "F_SINC", "MAX_KRYLOV", "NlsError", "Config", "Solver",
     "lib", "lib_path", "rccl_unique_id", "slab_planes", "EXPORTED_SYMBOLS",
 ]
 
 NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI, NLSE_G2, KG_GAUTSCHI = 0, 1, 2, 3, 4
+# G2 device Gautschi family (nlsolvers/device/include/{sg_single,sg_double,sg_hyperbolic,phi4_single}.cuh)
+SG_G2, SG_DOUBLE, SG_HYPERBOLIC, PHI4 = 5, 6, 7, 8
+REAL_EQUATIONS = (SG_GAUTSCHI, KG_GAUTSCHI, SG_G2, SG_DOUBLE, SG_HYPERBOLIC, PHI4)
 F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF, F_SINC = range(8)
 MAX_KRYLOV = 32
 
@@ -113,7 +117,7 @@ def lib():
     L.nls_set_timing.argtypes = [H, C.c_int32]
     L.nls_get_timing.argtypes = [H, C.POINTER(Timing)]
     L.nls_reset_timing.argtypes = [H]
-    if L.nls_abi_version() != 3:
+    if L.nls_abi_version() != 4:
         raise RuntimeError("libnls_amd ABI mismatch")
     _LIB = L
     return L
@@ -168,7 +172,8 @@ def _dptr(a: np.ndarray):
 class Solver:
     """One device handle (nls_handle).
 
-    equation: NLSE_CUBIC / NLSE_CQ / NLSE_G2 (complex128 fields) or SG_GAUTSCHI (float64).
+    equation: NLSE_CUBIC / NLSE_CQ / NLSE_G2 (complex128 fields) or SG_GAUTSCHI, KG_GAUTSCHI,
+    SG_G2, SG_DOUBLE, SG_HYPERBOLIC, PHI4 (float64).
     NLSE_G2 (nlsolvers/device/include/nlse_dev.hpp) also needs set_coefficients(m, c).
     Grid: dim 2 -> (ny, nx), dim 3 -> (nz, ny, nx); dx, dy as the reference
     drivers compute them (dx = 2 Lx / (nx - 1)).
@@ -193,7 +198,7 @@ class Solver:
         self._group = group
         cfg.local_group = group._g if group is not None else None
         self.cfg = cfg
-        self.complex = equation not in (SG_GAUTSCHI, KG_GAUTSCHI)
+        self.complex = equation not in REAL_EQUATIONS
         self.dtype = np.complex128 if self.complex else np.float64
         h = C.c_void_p()
         rc = L.nls_create(C.byref(cfg), C.byref(h))

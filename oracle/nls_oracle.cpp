@@ -675,4 +675,47 @@ int oracle_sg_steps(const oracle_grid *g, double *u, double *u_past,
   return 0;
 }
 
+// G2 device Gautschi family, Phi4Solver / SGESolver / SGEDoubleSolver /
+// SGEHyperbolicSolver ::step (nlsolvers/device/include/phi4_single.cuh:33-47,
+// sg_single.cuh:33-47, sg_double.cuh:34-48, sg_hyperbolic.cuh:33-47) on the
+// isotropic no-flux operator the drivers build (phi4_driver_dev.cpp:84-85):
+//   buf = u ; buf2 = id_sqrt(u) ; buf2 = -m F(buf2) ; buf3 = sinc2_sqrt(buf2) ;
+//   buf2 = cos_sqrt(u) ; u = 2 buf2 - u_past + tau^2 buf3 ; u_past = buf
+// (t = tau = dt; matfunc_real.hpp:212-238: f(t sqrt|lambda|)), then (bc != 0)
+// the drivers' apply_bc() on u only (phi4_driver_dev.cpp:108-111, phi4_dev.hpp:92).
+// kind: 0 sin u (sg_single.cuh:18), 1 sin u + sin(u/2) (sg_double.cuh:19),
+//       2 sinh u (sg_hyperbolic.cuh:18), 3 u + u^3 (phi4_single.cuh:18).
+int oracle_gautschi_g2_steps(const oracle_grid *g, int kind, double *u, double *u_past,
+                             const double *mfield, double dt, uint32_t nsteps, uint32_t m,
+                             int bc) {
+  Grid G;
+  if (!make_grid(g, G) || !u || !u_past || !mfield || m < 1 || kind < 0 || kind > 3) return -1;
+  if (bc && (G.nx < 3 || G.ny < 3 || (G.dim == 3 && G.nz < 3))) return -1;
+  StencilOp op{G};
+  const uint64_t n = G.N;
+  std::vector<double> buf(n), buf2(n), buf3(n);
+  const cd t(dt, 0.0);
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    std::memcpy(buf.data(), u, n * sizeof(double));
+    krylov_apply(op, u, t, m, ORACLE_F_ID_SQRT, buf2.data());
+    for (uint64_t p = 0; p < n; ++p) {
+      const double y = buf2[p];
+      double f;
+      switch (kind) {
+        case 0: f = std::sin(y); break;
+        case 1: f = std::sin(y) + std::sin(0.5 * y); break;
+        case 2: f = std::sinh(y); break;
+        default: f = y + y * y * y; break;
+      }
+      buf2[p] = -(mfield[p] * f);
+    }
+    krylov_apply(op, buf2.data(), t, m, ORACLE_F_SINC2_SQRT, buf3.data());
+    krylov_apply(op, u, t, m, ORACLE_F_COS_SQRT, buf2.data());
+    for (uint64_t p = 0; p < n; ++p) u[p] = 2.0 * buf2[p] - u_past[p] + dt * dt * buf3[p];
+    std::memcpy(u_past, buf.data(), n * sizeof(double));
+    if (bc) neumann_bc(G, u);
+  }
+  return 0;
+}
+
 }  // extern "C"

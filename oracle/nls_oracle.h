@@ -15,6 +15,8 @@
  *   nlsolvers/device/include/boundaries.cuh:10-81            (Neumann copy BC)
  *   nlsolvers/device/include/nlse_dev.hpp:205-238            (sEWI)
  *   nlsolvers/device/include/kg_single.cuh:49-86             (Klein-Gordon Gautschi)
+ *   nlsolvers/device/include/{sg_single,sg_double,sg_hyperbolic,phi4_single}.cuh
+ *                                                            (G2 Gautschi family)
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
  * load this library.  The product path (libnls_amd.so) never links it.
@@ -113,6 +115,15 @@ int oracle_kg_steps(const oracle_grid *g, const double *c, const double *mfield,
                     double *u, double *u_past, double *v, double dt,
                     uint32_t nsteps, uint32_t m, int bc);
 int oracle_neumann_bc_r(const oracle_grid *g, double *u);
+
+/* G2 device Gautschi family (nlsolvers/device/include/{sg_single,sg_double,
+ * sg_hyperbolic,phi4_single}.cuh): kind 0 sin, 1 sin + sin(u/2), 2 sinh,
+ * 3 u + u^3; g = -m F(id(u)), sinc^2 / cos / id of t sqrt|lambda| (t = dt) on the
+ * isotropic operator; bc != 0: Neumann copy BC on u after every step.  u, u_past
+ * updated in place. */
+int oracle_gautschi_g2_steps(const oracle_grid *g, int kind, double *u, double *u_past,
+                             const double *mfield, double dt, uint32_t nsteps, uint32_t m,
+                             int bc);
 
 /* sine-Gordon Gautschi (sg_solver.hpp:53-74); u, u_past updated in place. */
 int oracle_sg_steps(const oracle_grid *g, double *u, double *u_past,

@@ -14,6 +14,7 @@ Reference lines followed:
   eigen_krylov_real.hpp:5-201             real Lanczos + cos/sinc^2/id filters
   nlse_solver.hpp:53-77                   Strang SS2 step
   sg_solver.hpp:53-74                     Gautschi step
+  nlsolvers/device/include/{sg_single,sg_double,sg_hyperbolic,phi4_single}.cuh   G2 Gautschi family
   nlsolvers/common/include/util.hpp:95-125  create_centered_gaussian_3d
 """
 from __future__ import annotations
@@ -309,6 +310,36 @@ def sg_steps(dim, nx, ny, nz, dx, dy, u, u_past, mfield, dt, nsteps, m):
         s2 = krylov(ap, g, dt, m, F_SINC2_HALF)
         cs = krylov(ap, u, dt, m, F_COS_SQRT)
         u, up = 2 * cs - up + dt * dt * s2, u
+    return u, up
+
+
+def gg_force(y, kind):
+    """F of the G2 Gautschi family: sg_single.cuh:18, sg_double.cuh:19, sg_hyperbolic.cuh:18,
+    phi4_single.cuh:18 (g = -m F(y))."""
+    if kind == 0:
+        return np.sin(y)
+    if kind == 1:
+        return np.sin(y) + np.sin(0.5 * y)
+    if kind == 2:
+        return np.sinh(y)
+    return y + y ** 3
+
+
+def gautschi_g2_steps(dim, nx, ny, nz, dx, dy, kind, u, u_past, mfield, dt, nsteps, m, bc=True):
+    """Phi4Solver / SGE{,Double,Hyperbolic}Solver::step (nlsolvers/device/include/phi4_single.cuh:33-47)
+    on the isotropic operator, then the drivers' apply_bc on u."""
+    ap = lambda v: laplacian_apply(dim, nx, ny, nz, dx, dy, v)
+    u = np.asarray(u, dtype=np.float64).ravel().copy()
+    up = np.asarray(u_past, dtype=np.float64).ravel().copy()
+    mf = np.asarray(mfield, dtype=np.float64).ravel()
+    for _ in range(nsteps):
+        y = krylov(ap, u, dt, m, F_ID_SQRT)
+        g = -(mf * gg_force(y, kind))
+        s2 = krylov(ap, g, dt, m, F_SINC2_SQRT)
+        cs = krylov(ap, u, dt, m, F_COS_SQRT)
+        u, up = 2.0 * cs - up + dt * dt * s2, u
+        if bc:
+            u = neumann_bc(dim, nx, ny, nz, u)
     return u, up
 
 

@@ -60,6 +60,8 @@ def lib():
                                            C.c_int]
         L.oracle_kg_steps.argtypes = [g, dp, dp, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32, C.c_int]
         L.oracle_neumann_bc_r.argtypes = [g, dp]
+        L.oracle_gautschi_g2_steps.argtypes = [g, C.c_int, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
+                                               C.c_int]
         L.oracle_nlse_sewi_steps.argtypes = [g, dp, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
                                              C.c_uint32, C.c_int]
     return _LIB
@@ -197,3 +199,15 @@ def neumann_bc_r(g, u):
     ui = _r(u).copy()
     _check(lib().oracle_neumann_bc_r(C.byref(g), ui))
     return ui
+
+
+GG_KINDS = {"sg": 0, "sg_double": 1, "sg_hyperbolic": 2, "phi4": 3}
+
+
+def gautschi_g2_steps(g, kind, u, u_past, mfield, dt, nsteps, m, bc=True):
+    """G2 Gautschi family (phi4_single.cuh:33-47 & siblings); returns (u, u_past)."""
+    u = _r(u).copy()
+    up = _r(u_past).copy()
+    _check(lib().oracle_gautschi_g2_steps(C.byref(g), int(kind), u, up, _r(mfield), dt, nsteps, m,
+                                          1 if bc else 0))
+    return u, up

@@ -26,3 +26,19 @@ def rel_l2(a, b):
 @pytest.fixture
 def rel():
     return rel_l2
+
+
+# The reference algorithm's own rounding sensitivity (DESIGN.md section 6,
+# "parity floor"): on smooth data over fine grids, or at ||L|| dt >> m, the
+# Lanczos basis amplifies rounding noise in the high modes by roughly
+# prod_j ||L|| / beta_j per action, and the SS2 map carries that growth from
+# step to step.  Two faithful CPU restatements of the reference (the C oracle,
+# MGS + cyclic Jacobi, and the numpy twin, MGS + LAPACK eigh) then drift apart
+# exponentially although each is "exact".  A GPU trajectory is held to the
+# north_star tolerance where that floor is below it, and to FLOOR_FACTOR times
+# the floor where the reference algorithm itself cannot resolve 1e-10.
+FLOOR_FACTOR = 10.0
+
+
+def parity_bound(tol, floor):
+    return max(tol, FLOOR_FACTOR * floor)

@@ -137,9 +137,30 @@ def main():
     assert np.linalg.norm(ku - tu) / np.linalg.norm(tu) < 1e-12
     cases["kg_3d"] = dict(dim=3, n=n, dx=dx, dt=kdt, steps=steps, m=m, u0=ku0, v0=kv0, c=cf, mfield=mf,
                           u=ku, u_past=kup, v=kv)
+    # --- G2 Gautschi family (phi4_dev / sg_{single,double,hyperbolic}_dev: m=10), BC per step
+    n, m, steps, L, gdt = 24, 10, 8, 4.0, 1e-2
+    dx = 2 * L / (n - 1)
+    x = np.linspace(-L, L, n)
+    Y, X = np.meshgrid(x, x, indexing="ij")
+    rng = np.random.default_rng(41)
+    gu0 = (1.5 * np.exp(-(X ** 2 + Y ** 2) / 2) + 1e-3 * rng.standard_normal(X.shape)).ravel()
+    gv0 = (0.2 * np.sin(X) * np.exp(-Y ** 2)).ravel()
+    gmf = (1.0 + 0.2 * np.cos(X + Y)).ravel()
+    g = O.grid(2, n, n, 1, dx, dx)
+    gg = dict(dim=2, n=n, dx=dx, dt=gdt, steps=steps, m=m, u0=gu0, v0=gv0, mfield=gmf)
+    for kname, kind in O.GG_KINDS.items():
+        ku, kup = O.gautschi_g2_steps(g, kind, gu0, gu0 - gdt * gv0, gmf, gdt, steps, m, bc=True)
+        tu, _ = np_ref.gautschi_g2_steps(2, n, n, 1, dx, dx, kind, gu0, gu0 - gdt * gv0, gmf, gdt, steps, m)
+        assert np.linalg.norm(ku - tu) / np.linalg.norm(tu) < 1e-12, kname
+        gg[f"u_{kname}"], gg[f"u_past_{kname}"] = ku, kup
+    cases["gautschi_g2"] = gg
+    only = sys.argv[1:]  # optional: regenerate only the named fixtures
     for name, d in cases.items():
+        if only and name not in only:
+            continue
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **{k: np.asarray(v) for k, v in d.items()})
-    total = sum(os.path.getsize(os.path.join(HERE, f"{k}.npz")) for k in cases)
+    total = sum(os.path.getsize(os.path.join(HERE, f"{k}.npz")) for k in cases
+                if os.path.exists(os.path.join(HERE, f"{k}.npz")))
     print(f"wrote {len(cases)} fixtures, {total / 1024:.1f} KiB")
 
 

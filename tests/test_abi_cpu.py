@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert sorted(nls_amd.EXPORTED_SYMBOLS) == syms
-    assert L.nls_abi_version() == 3
+    assert L.nls_abi_version() == 4
     out = subprocess.run(["nm", "-D", "--defined-only", nls_amd.lib_path()], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (nls_\w+)", out))
     assert set(syms) <= exported
@@ -48,8 +48,12 @@ def test_config_default_matches_reference_defaults():
 @pytest.mark.parametrize("kw,msg", [
     (dict(m=0), "krylov_m"), (dict(m=33), "krylov_m"), (dict(dim=4), "dim"),
     (dict(nx=1), "grid too small"), (dict(dx=0.0), "dx"), (dict(nranks=2), "rccl_id"),
-    (dict(equation=5), "unknown equation"), (dict(equation=3, nx=2), "need >= 3 cells"), (dict(equation=4, ny=2), "need >= 3 cells"),
+    (dict(equation=9), "unknown equation"), (dict(equation=3, nx=2), "need >= 3 cells"), (dict(equation=4, ny=2), "need >= 3 cells"),
     (dict(equation=3, dim=3, nz=3, nranks=2, group=True), "2 planes per rank"),
+    # 32-bit cell indices of the stencil march: (planes + 2) * plane + pad < 2^31
+    (dict(dim=2, nx=50000, ny=50000, equation=2), "32-bit cell indices"),
+    (dict(dim=3, nx=1300, ny=1300, nz=1300), "32-bit cell indices"),
+    (dict(dim=3, nx=2048, ny=2048, nz=2048, nranks=4, group=True), "32-bit cell indices"),
 ])
 def test_invalid_config_rejected_before_device(kw, msg):
     base = dict(dim=2, nx=16, ny=16, nz=1, dx=0.5)
@@ -68,12 +72,37 @@ def run(args, **kw):
     return subprocess.run(args, capture_output=True, text=True, timeout=60, **kw)
 
 
-@pytest.mark.parametrize("prog", ["nlse_call", "nlse_cq_call", "to_nlse_call"])
+def test_index_limit_boundary_not_rejected_early():
+    """Just below the limit the config passes validation (it then needs a device:
+    on this CPU-only host creation fails with a HIP error, not NLS_ERR_ARG)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("would allocate ~ 2^31 cells on a GPU")
+    with pytest.raises(nls_amd.NlsError) as e:
+        nls_amd.Solver(3, 1024, 1024, 2045, 0.1, m=3)
+    assert "32-bit" not in str(e.value)
+
+
+@pytest.mark.parametrize("prog", ["nlse_call", "nlse_cq_call", "to_nlse_call", "to_nlse_cq_call"])
 def test_driver_usage_exit_code(prog):
     r = run([os.path.join(BIN, prog)])
     assert r.returncode == 1 and "Usage:" in r.stderr
     r = run([os.path.join(BIN, prog)] + ["8"] * 8)
     assert r.returncode == 1 and "Usage:" in r.stderr
+
+
+@pytest.mark.parametrize("prog", ["sg_single_dev", "sg_double_dev", "sg_hyperbolic_dev", "phi4_dev"])
+def test_gautschi_g2_driver_usage(prog, tmp_path):
+    """phi4_driver_dev.cpp:17-28: 11 or 12 argv, else usage + exit 1; u0 of the wrong
+    shape -> "Error: Input array dimensions mismatch" + exit 1 (before any device call)."""
+    for n in (0, 9, 12):
+        r = run([os.path.join(BIN, prog)] + ["8"] * n)
+        assert r.returncode == 1 and "Usage:" in r.stderr
+    np.save(tmp_path / "u0.npy", np.zeros((8, 9)))
+    np.save(tmp_path / "v0.npy", np.zeros((8, 9)))
+    r = run([os.path.join(BIN, prog), "8", "8", "1", "1", str(tmp_path / "u0.npy"), str(tmp_path / "v0.npy"),
+             str(tmp_path / "o.npy"), "1", "10", "2"])
+    assert r.returncode == 1 and "Input array dimensions mismatch" in r.stderr
 
 
 def test_driver_shape_mismatch(tmp_path):

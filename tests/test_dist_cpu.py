@@ -104,3 +104,44 @@ def test_bench_orchestration_over_gloo(world):
     assert r["ic_equal"]
     assert r["mass"] < 1e-14
     assert abs(r["max"] - 0.1 * world) < 1e-12
+
+
+def test_bench_launcher_command_line():
+    """`python bench.py --gpus N` without torch.distributed.run re-launches itself
+    as N ranks with the driver's own launcher line (127.0.0.1 rendezvous)."""
+    import bench
+    cmd = bench.rank_launch_cmd(4, ["--gpus", "4", "--steps", "3"], 29555)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert "--master-port=29555" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+def test_bench_launcher_forwards_rank0_line(tmp_path, monkeypatch):
+    """launch_ranks runs a real torch.distributed.run with 2 gloo ranks (a stand-in
+    script for bench.py: no GPU here) and forwards only rank 0's JSON line; the
+    children see WORLD_SIZE / RANK / MASTER_ADDR from the launcher."""
+    import sys
+    import bench
+    script = tmp_path / "fake_bench.py"
+    script.write_text(
+        "import json, os\n"
+        "import torch.distributed as dist\n"
+        "dist.init_process_group('gloo')\n"
+        "r, w = dist.get_rank(), dist.get_world_size()\n"
+        "assert os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+        "dist.barrier()\n"
+        "if r == 0:\n"
+        "    print('banner line on stdout')\n"
+        "    print(json.dumps({'metric': 'x', 'value': 1.0, 'n_gpus': w}))\n"
+        "dist.destroy_process_group()\n")
+    real = bench.rank_launch_cmd
+
+    def fake_cmd(n, argv, port):
+        cmd = real(n, argv, port)
+        i = cmd.index(os.path.abspath(bench.__file__))
+        return cmd[:i] + [str(script)]
+    monkeypatch.setattr(bench, "rank_launch_cmd", fake_cmd)
+    rc, line = bench.launch_ranks(2, [])
+    assert rc == 0
+    assert json.loads(line) == {"metric": "x", "value": 1.0, "n_gpus": 2}

@@ -135,10 +135,24 @@ def test_kg_driver_matches_oracle(tmp_path, dim):
         args = [os.path.join(BIN, "kg_gautschi_3d_dev"), str(n), str(n), str(n), str(L), str(L), str(L)]
     else:
         args = [os.path.join(BIN, "kg_gautschi_2d_dev"), str(n), str(n), str(L), str(L)]
-    args += [p["u0"], p["v0"], p["tu"], p["tv"], str(T), str(nt), str(ns), p["m"], p["c"]]
-    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    tail = [str(T), str(nt), str(ns), p["m"], p["c"]]
+    r = subprocess.run(args + [p["u0"], p["v0"], p["tu"], p["tv"]] + tail + (["--true-shape"] if dim == 3 else []),
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     tu, tv = np.load(p["tu"]), np.load(p["tv"])
+    if dim == 3:
+        # default: the reference's header [ns, ny, nx] over the full ns*nz*ny*nx payload
+        # (kg_driver_dev_3d.cpp:161-163), byte-identical data to the --true-shape file
+        ref_u = str(tmp_path / "ref_u.npy")
+        r = subprocess.run(args + [p["u0"], p["v0"], ref_u, str(tmp_path / "ref_v.npy")] + tail,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        with open(ref_u, "rb") as f:
+            ver = np.lib.format.read_magic(f)
+            hdr_shape, _, dtype = np.lib.format._read_array_header(f, ver)
+            payload = np.fromfile(f, dtype=dtype)
+        assert hdr_shape == (ns, n, n)
+        assert np.array_equal(payload, tu.ravel())
     assert tu.shape == (ns,) + shp and tv.shape == (ns,) + shp
     g = O.grid(dim, n, n, n, dx, dx)
     u, up = u0.copy(), u0 - dt * v0

@@ -1,0 +1,221 @@
+"""GPU parity at the headline's stiffness (VERDICT r01 "next round" item 1).
+
+The BASELINE workloads run on fine grids: 3D 512^3 with dx = 20/511
+(||L|| dt ~ 12/dx^2 * 1e-3 ~ 7.9), 2D 4096^2 with dx = 20/4095 (||L|| dt ~ 335)
+and sine-Gordon 8192^2 with dx = 6/8191 (t sqrt||L|| ~ 39).  The oracle cannot
+run those grids, so these tests keep the SPACING of each workload on a
+sub-grid the oracle finishes in seconds (3D 128^3, 2D 1024^2) -- the Krylov
+problem has the same stiffness -- and force the code paths that the library
+otherwise enables only on large slabs (> 32 M cells):
+
+  NLS_FUSED_ALPHA=1   folded alpha (nls_march_q.hpp; O(||L||^3) cancellation)
+  NLS_GRID_MULT=16    one tile per workgroup grids
+  NLS_KZ=1            shallow update tiles -> > 2048 per-workgroup partials,
+                      so k_colsum sums them (reduce_iter / reduce_qa / reduce_final)
+  NLS_KZ_ALPHA=4      the large-slab alpha tile depth
+
+plus the fused tail (s_{m-1}^2 = ||L v||^2 - sum |H|^2, O(eps ||L||^2 / s^2)).
+Reference algorithm: eigen_krylov_complex.hpp:10-84 (MGS Lanczos, exp(t|lambda|)),
+nlse_solver.hpp:53-77 (SS2), eigen_krylov_real.hpp:53-201 + sg_solver.hpp:53-74
+(Gautschi).  Tolerance: north_star's 1e-10 relative L2 on the field after 1 and
+5 steps, and after 20 steps wherever the reference algorithm itself resolves it.
+The 3D case does (two CPU restatements agree to ~5e-14 after 20 steps).  The 2D
+NLSE at dx = 20/4095 (||L|| dt ~ 335 against m = 16) does not: the C oracle and
+the numpy twin -- both exact restatements, differing only in rounding order and
+eigensolver -- drift from 1e-13 (step 1) to ~4e-7 (step 20), about 2.2x per
+step.  There the GPU is held to FLOOR_FACTOR x that measured floor
+(conftest.parity_bound).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import np_ref as R
+import oracle_py as O
+from conftest import parity_bound, rel_l2
+
+pytestmark = pytest.mark.gpu
+nls_amd = pytest.importorskip("nls_amd")
+
+TOL = 1e-10
+
+LARGE = {"NLS_FUSED_ALPHA": "1", "NLS_GRID_MULT": "16", "NLS_KZ": "1", "NLS_KZ_ALPHA": "4",
+         "NLS_FUSED_TAIL": "1"}
+PLAIN = {"NLS_FUSED_ALPHA": "0", "NLS_FUSED_TAIL": "1"}
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _ic(dim, n, dx, seed):
+    """A few Gaussian bumps with phases on [-L, L]^dim (L = (n-1) dx / 2) plus
+    1e-3 complex white noise (the noise populates the top of the spectrum,
+    where the stiffness lives); unit mass as nlse_call.cpp:41-49."""
+    rng = np.random.default_rng(seed)
+    L = (n - 1) * dx / 2
+    x = np.linspace(-L, L, n)
+    if dim == 3:
+        Z, Y, X = np.meshgrid(x, x, x, indexing="ij", sparse=True)
+        u = np.zeros((n, n, n), np.complex128)
+        for _ in range(3):
+            c = rng.uniform(-L / 2, L / 2, 3)
+            k = rng.uniform(-2, 2, 3)
+            w = rng.uniform(0.2, 0.4) * L
+            u += np.exp(-((X - c[0]) ** 2 + (Y - c[1]) ** 2 + (Z - c[2]) ** 2) / w ** 2
+                        + 1j * (k[0] * X + k[1] * Y + k[2] * Z))
+    else:
+        Y, X = np.meshgrid(x, x, indexing="ij", sparse=True)
+        u = np.zeros((n, n), np.complex128)
+        for _ in range(3):
+            c = rng.uniform(-L / 2, L / 2, 2)
+            k = rng.uniform(-2, 2, 2)
+            w = rng.uniform(0.2, 0.4) * L
+            u += np.exp(-((X - c[0]) ** 2 + (Y - c[1]) ** 2) / w ** 2 + 1j * (k[0] * X + k[1] * Y))
+    u = u.ravel()
+    u += 1e-3 * (rng.standard_normal(u.size) + 1j * rng.standard_normal(u.size))
+    return u / np.sqrt(np.sum(np.abs(u) ** 2) * dx ** dim)
+
+
+CHECK = (1, 5, 20)  # checkpoints (steps)
+
+
+def _gpu_nlse(dim, n, dx, u0, dt, m, eq, env):
+    def run():
+        nz = n if dim == 3 else 1
+        out, done = {}, 0
+        with nls_amd.Solver(dim, n, n, nz, dx, dx, equation=eq, m=m) as s:
+            s.set_field(u0)
+            s.set_timing(True)
+            for k in CHECK:
+                s.step(dt, k - done)
+                done = k
+                out[k] = s.get_field()
+            return out, s.timing()
+    return _with_env(env, run)
+
+
+_CPU = {}
+
+
+def _cpu_nlse(dim, n, dx, u0, dt, m, eq):
+    """Oracle and numpy-twin fields at the checkpoints (cached per problem)."""
+    key = ("nlse", dim, n, dx, dt, m, eq)
+    if key not in _CPU:
+        g = O.grid(dim, n, n, n, dx, dx)
+        nz = n if dim == 3 else 1
+        a, b, done, ora, twin = u0, u0, 0, {}, {}
+        for k in CHECK:
+            a = O.nlse_steps(g, a, dt, k - done, m, nonlin=eq)
+            b = R.nlse_steps(dim, n, n, nz, dx, dx, b, dt, k - done, m, nonlin=eq)
+            done = k
+            ora[k], twin[k] = a, b
+        _CPU[key] = (ora, twin)
+    return _CPU[key]
+
+
+def _check(gpu, ora, twin, hard=(1, 5)):
+    """GPU vs oracle at every checkpoint: <= TOL at the `hard` checkpoints, else
+    <= parity_bound(TOL, floor) with floor = oracle vs twin."""
+    rows = []
+    for k in CHECK:
+        err, floor = rel_l2(gpu[k], ora[k]), rel_l2(twin[k], ora[k])
+        bound = TOL if k in hard else parity_bound(TOL, floor)
+        rows.append((k, err, floor, bound))
+    msg = "; ".join(f"step {k}: gpu {e:.2e} floor {f:.2e} bound {b:.1e}" for k, e, f, b in rows)
+    assert all(e <= b for _, e, _, b in rows), msg
+
+
+# (dim, n, dx): the sub-grid keeps the BASELINE workload's spacing
+STIFF = [(3, 128, 20.0 / 511), (2, 1024, 20.0 / 4095)]
+
+
+@pytest.mark.parametrize("dim,n,dx", STIFF, ids=["3d128_dx512", "2d1024_dx4096"])
+@pytest.mark.parametrize("eq", [0, 1], ids=["cubic", "cq"])
+@pytest.mark.parametrize("mode", ["large", "plain"])
+def test_nlse_stiff_matches_oracle(dim, n, dx, eq, mode):
+    m, dt = 16, 1e-3
+    u0 = _ic(dim, n, dx, 41 + eq)
+    env = LARGE if mode == "large" else PLAIN
+    gpu, tm = _gpu_nlse(dim, n, dx, u0, dt, m, eq, env)
+    steps = CHECK[-1]
+    assert all(np.all(np.isfinite(v)) for v in gpu.values())
+    # the fused tail ran every step; with the folded alpha only alpha_0 and the
+    # tail's k_alpha_l2 remain per step (2 alpha launches instead of m - 1)
+    assert tm["class_count"]["final"] == steps
+    if mode == "large":
+        assert tm["class_count"]["alpha"] == 2 * steps
+    else:
+        assert tm["class_count"]["alpha"] == (m - 1) * steps
+    ora, twin = _cpu_nlse(dim, n, dx, u0, dt, m, eq)
+    if dim == 3:  # resolved by the reference algorithm: 1e-10 at every checkpoint
+        assert rel_l2(twin[steps], ora[steps]) <= 1e-12
+        _check(gpu, ora, twin, hard=CHECK)
+    else:
+        _check(gpu, ora, twin)
+
+
+def test_large_slab_path_uses_colsum():
+    """With NLS_KZ=1 + 16x grids at 128^3 the per-workgroup partials exceed
+    COLSUM_MIN (2048), so every reduction goes through k_colsum first: more
+    launches of the reduce class than the plain configuration, same field."""
+    dim, n, dx, m, dt = 3, 128, 20.0 / 511, 16, 1e-3
+    u0 = _ic(dim, n, dx, 7)
+    a, ta = _gpu_nlse(dim, n, dx, u0, dt, m, 0, LARGE)
+    b, tb = _gpu_nlse(dim, n, dx, u0, dt, m, 0, {**LARGE, "NLS_GRID_MULT": "1", "NLS_KZ": "32"})
+    assert ta["class_count"]["reduce"] > tb["class_count"]["reduce"]
+    assert rel_l2(a[CHECK[-1]], b[CHECK[-1]]) <= 1e-12
+
+
+def _sg_ic(n, dx, seed):
+    """sg_driver_dev.cpp:34-36 kink ring 2 atan(exp(3 - 5 r)) on L = (n-1) dx / 2,
+    scaled to the sub-domain, plus 1e-3 white noise; v0 = 0."""
+    rng = np.random.default_rng(seed)
+    L = (n - 1) * dx / 2
+    x = np.linspace(-L, L, n)
+    Y, X = np.meshgrid(x, x, indexing="ij")
+    r = np.sqrt(X ** 2 + Y ** 2) * (3.0 / L)
+    u = 2.0 * np.arctan(np.exp(3.0 - 5.0 * r)).ravel()
+    return u + 1e-3 * rng.standard_normal(u.size)
+
+
+@pytest.mark.parametrize("mode", ["large", "plain"])
+def test_sg_stiff_matches_oracle(mode):
+    """Sine-Gordon Gautschi at C4's spacing dx = 6/8191 (t sqrt||L|| ~ 39) on 1024^2;
+    oracle vs twin: 3e-13 (step 1), 2.6e-12 (5), 1.5e-10 (20)."""
+    n, dx, m, dt = 1024, 6.0 / 8191, 10, 5.0 / 500
+    u0 = _sg_ic(n, dx, 3)
+    mf = -np.ones(n * n)
+    env = LARGE if mode == "large" else PLAIN
+
+    def run():
+        out, done = {}, 0
+        with nls_amd.Solver(2, n, n, 1, dx, dx, equation=nls_amd.SG_GAUTSCHI, m=m) as s:
+            s.set_sg_state(u0, u0.copy(), mf)
+            for k in CHECK:
+                s.step(dt, k - done)
+                done = k
+                out[k] = s.get_field()
+        return out
+    gpu = _with_env(env, run)
+    key = ("sg", n, dx, dt, m)
+    if key not in _CPU:
+        g = O.grid(2, n, n, 1, dx, dx)
+        a, ap, b, bp, done, ora, twin = u0, u0, u0, u0, 0, {}, {}
+        for k in CHECK:
+            a, ap = O.sg_steps(g, a, ap, mf, dt, k - done, m)
+            b, bp = R.sg_steps(2, n, n, 1, dx, dx, b, bp, mf, dt, k - done, m)
+            done = k
+            ora[k], twin[k] = a, b
+        _CPU[key] = (ora, twin)
+    _check(gpu, *_CPU[key])

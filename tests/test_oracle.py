@@ -344,3 +344,62 @@ def test_golden_kg():
     u, up, v = O.kg_steps(g, d["c"], d["mfield"], d["u0"], d["u0"] - dt * d["v0"], dt, int(d["steps"]),
                           int(d["m"]))
     assert rel_l2(u, d["u"]) < 1e-13 and rel_l2(up, d["u_past"]) < 1e-13 and rel_l2(v, d["v"]) < 1e-11
+
+
+# ---- G2 Gautschi family: sg_single / sg_double / sg_hyperbolic / phi4 -------------
+
+@pytest.mark.parametrize("kind", sorted(O.GG_KINDS.values()))
+@pytest.mark.parametrize("dim,n", [(2, 15), (3, 8)])
+def test_gautschi_g2_oracle_matches_numpy_twin(kind, dim, n):
+    """Phi4Solver / SGE{,Double,Hyperbolic}Solver::step (phi4_single.cuh:33-47,
+    sg_single.cuh:33-47, sg_double.cuh:34-48, sg_hyperbolic.cuh:33-47) + apply_bc,
+    two restatements (C: cyclic Jacobi, numpy: LAPACK eigh)."""
+    rng = np.random.default_rng(61 + kind + dim)
+    N = n ** dim
+    u = rng.standard_normal(N)
+    dt = 1e-2
+    up = u - dt * 0.1 * rng.standard_normal(N)
+    mf = rng.uniform(0.5, 1.5, N)
+    g = O.grid(dim, n, n, n, 0.5, 0.5)
+    a = O.gautschi_g2_steps(g, kind, u, up, mf, dt, 4, 10, bc=True)
+    b = np_ref.gautschi_g2_steps(dim, n, n, n, 0.5, 0.5, kind, u, up, mf, dt, 4, 10, bc=True)
+    assert rel_l2(a[0], b[0]) < 1e-12 and rel_l2(a[1], b[1]) < 1e-12
+
+
+def test_gautschi_g2_family_differs_only_in_force():
+    """At small amplitude all four forces are ~ u to first order (sin, sinh, u + u^3,
+    and the double sine ~ 1.5 u): the trajectories of sin / sinh / phi4 agree to
+    O(u^3) and differ in the expected direction of the cubic term."""
+    n = 16
+    rng = np.random.default_rng(3)
+    u = 1e-3 * rng.standard_normal(n * n)
+    mf = np.ones(n * n)
+    g = O.grid(2, n, n, 1, 0.4, 0.4)
+    outs = {k: O.gautschi_g2_steps(g, v, u, u, mf, 1e-2, 5, 10)[0] for k, v in O.GG_KINDS.items()}
+    assert rel_l2(outs["sg"], outs["phi4"]) < 1e-5
+    assert rel_l2(outs["sg"], outs["sg_hyperbolic"]) < 1e-5
+    assert rel_l2(outs["sg"], outs["sg_double"]) > 1e-8  # 1.5x the linear force
+
+
+def test_gautschi_g2_uses_full_sinc2_argument():
+    """The G2 device family filters g with sinc^2(t sqrt|lambda|) (matfunc_real.hpp:212-219),
+    not the G1 CPU path's sinc^2(t/2 sqrt|lambda|) (eigen_krylov_real.hpp:172-201): with the
+    sine force, m = -1 and no BC it must differ from oracle_sg_steps at O(dt^4 ||L||)."""
+    n = 16
+    x = np.linspace(-3, 3, n)
+    Y, X = np.meshgrid(x, x, indexing="ij")
+    u = (2.0 * np.arctan(np.exp(3.0 - 5.0 * np.sqrt(X * X + Y * Y)))).ravel()
+    g = O.grid(2, n, n, 1, 0.4, 0.4)
+    a, _ = O.gautschi_g2_steps(g, 0, u, u, np.ones(n * n), 1e-2, 3, 10, bc=False)
+    b, _ = O.sg_steps(g, u, u, -np.ones(n * n), 1e-2, 3, 10)
+    assert 1e-12 < rel_l2(a, b) < 1e-3
+
+
+def test_golden_gautschi_g2():
+    d = np.load(os.path.join(GOLD, "gautschi_g2.npz"))
+    n, dt = int(d["n"]), float(d["dt"])
+    g = O.grid(2, n, n, 1, float(d["dx"]), float(d["dx"]))
+    for kname, kind in O.GG_KINDS.items():
+        u, up = O.gautschi_g2_steps(g, kind, d["u0"], d["u0"] - dt * d["v0"], d["mfield"], dt,
+                                    int(d["steps"]), int(d["m"]))
+        assert rel_l2(u, d[f"u_{kname}"]) < 1e-13 and rel_l2(up, d[f"u_past_{kname}"]) < 1e-13
