@@ -108,12 +108,14 @@ struct nls_handle {
   // fused tail (m >= 3): the last update pass of a basis and the combination
   // that ends the step are one pass, k_tail (NLS_FUSED_TAIL=0 disables)
   bool fused_tail = false;
-  // two new Lanczos vectors per basis pass (nls_pass2.hpp; NLS_PASS2=1, 3D isotropic NLSE, one rank)
+  // two new Lanczos vectors per basis pass (nls_pass2.hpp, nls_pass2d.hpp; 3D isotropic
+  // NLSE, one rank), ending in the fused tail k_tail over the stored S vectors
   bool pass2 = false;
   void *p2 = nullptr;          // P2State
-  cplx *partP2 = nullptr;      // per-workgroup partials of k_pass2
-  int p2grid = 0, p2kz = 64;
-  bool p2reg = true;           // register-march k_pass2r (NLS_P2_IMPL=0: the LDS form)
+  cplx *partP2 = nullptr;      // per-workgroup partials of the pass
+  int p2grid = 0, p2kz = 32;
+  int p2impl = 2;              // 2: LDS-DMA k_p2d; 1: register-march k_pass2r (NLS_P2_IMPL)
+  cplx *zbuf = nullptr;        // 1 KiB of zeros: the DMA source of out-of-grid cells
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
@@ -609,20 +611,26 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   reduce_final(h, b, nf, f0, f1, tr, ti);
 }
 
-// k_pass2r grid: one wave per 60 x rb output column of kz planes, 4 waves per workgroup
-int p2r_grid(const nls_handle *h, int rb) {
+// grid of one two-vector pass: k_p2d one workgroup per 60 x 4-row tile of
+// p2kz planes; k_pass2r one wave per 60 x rb output column, 4 waves per workgroup
+int p2_grid(const nls_handle *h, int J) {
   const Geo &g = h->geo;
   const int64_t nzc = (g.npl + h->p2kz - 1) / h->p2kz;
+  if (h->p2impl == 2)
+    return (int)(((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * (g.nyp / P2D_ROWS) * nzc);
+  const int rb = P2R_ROWS(J);
   const int64_t waves = ((g.nx + P2R_WAVE_XO - 1) / P2R_WAVE_XO) * (g.nyp / rb) * nzc;
   return (int)((waves + NTHREADS / 64 - 1) / (NTHREADS / 64));
 }
 
 // Two new vectors per pass (nls_pass2.hpp): the alpha pass + reduction of W_0
 // give beta and alpha_0 (the first shift); then passes at J = 0, 2, 4, ... each
-// followed by its column sums and k_p2coef; the eigensolve on the resulting T;
-// k_p2fin maps fin to the stored vectors for the caller's final pass.
+// followed by its column sums and k_p2coef, until S_0..S_{m-2} are stored; the
+// last alpha pass (k_alpha_l2 over S_{m-2}) and k_p2tail complete T; the
+// eigensolve; k_p2tfin maps fin to the coefficients of the caller's k_tail
+// (S_0..S_{m-2} and L S_{m-2}: the last Lanczos vector is never stored).
 void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
-  const int m = h->m;
+  const int m = h->m, nstore = m - 1;
   Geo ga = h->geo;
   ga.kz = h->kz_alpha;
   alpha_pass(h, 0, 0, ga);
@@ -630,7 +638,7 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
   KState *st = h->B[0].st;
   void *ps = h->p2;
   {
-    int J = 0, mm = m, mode = 0;
+    int J = 0, mm = nstore, mode = 0;
     void *args[] = {&ps, &st, &J, &mm, &mode};
     launch(h, 2, 0, kernel_p2coef(), 1, args);
   }
@@ -640,25 +648,35 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
   g.kz = h->p2kz;
   cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(h->p2) + p2state_sums_offset());
   int J = 0;
-  while (J + 1 < m) {
-    const bool hz = J + 2 < m;
-    int nb = h->p2reg ? p2r_grid(h, P2R_ROWS(J)) : h->p2grid;
-    void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb};
-    launch(h, 1, J, kernel_pass2(J, hz, h->p2reg), nb, args, nullptr,
-           h->p2reg ? NTHREADS : P2_THREADS);
+  while (J + 1 < nstore) {
+    const bool hz = J + 2 < nstore;
+    int nb = p2_grid(h, J);
+    void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb, &h->zbuf};
+    launch(h, 1, J, kernel_pass2(J, hz, h->p2impl), nb, args);
     const cplx *pA = nullptr;
     int nbA = 0, ncA = 0, ncU = hz ? 2 * J + 5 : J + 2;
     void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
     launch(h, 2, J, kernel_colsum(), ncU, cargs);
-    int mm = m, mode = 1, jj = J;
+    int mm = nstore, mode = 1, jj = J;
     void *a2[] = {&ps, &st, &jj, &mm, &mode};
     launch(h, 2, J, kernel_p2coef(), 1, a2);
     J += hz ? 2 : 1;
   }
+  // the tail's alpha pass over S_{m-2}: a = S^H L S, ||S||^2, ||L S||^2
+  alpha_l2_pass(h, 0, m - 2);
+  {
+    const cplx *pU = nullptr;
+    int nbA = h->grid_alpha2, ncA = 3, nbU = 0;
+    void *cargs[] = {(void *)&h->partA, &nbA, &ncA, (void *)&pU, &nbU, &sums};
+    launch(h, 2, m - 2, kernel_colsum(), ncA, cargs);
+    int mm = m;
+    void *a2[] = {&ps, &st, &sums, &mm};
+    launch(h, 2, m - 2, kernel_p2tail(), 1, a2);
+  }
   reduce_final(h, 0, nf, f0, f1, tr, ti, 1);
   int mm = m, nff = nf;
   void *fa[] = {&ps, &st, &mm, &nff};
-  launch(h, 2, m, kernel_p2fin(), 1, fa);
+  launch(h, 2, m, kernel_p2tfin(), 1, fa);
 }
 
 int occupancy_grid(nls_handle *h, const void *fn, int64_t work_items) {
@@ -743,29 +761,31 @@ void alloc_all(nls_handle *h) {
   const bool c = h->cplx_;
   const int dim = h->cfg.dim;
   const bool ani = h->ani;
-  // two-vectors-per-pass Lanczos (opt-in): stores all m vectors, no fused tail / folded alpha
+  // two-vectors-per-pass Lanczos (NLS_PASS2=1): stores S_0..S_{m-2}, ends in the fused tail
   h->pass2 = false;
-  if (const char *e = std::getenv("NLS_PASS2"); e && std::atoi(e) != 0)
-    h->pass2 = c && !ani && dim == 3 && !h->collective && h->nbasis == 1 && g.nx % 64 == 0 &&
-               g.nyp % P2_TILE_Y == 0 && h->m >= 3 && h->m <= MMAX &&
-               g.nloc + 2 * g.P < (int64_t(1) << 31);  // k_pass2's 32-bit cell indices
+  if (const char *e = std::getenv("NLS_P2_IMPL")) h->p2impl = std::atoi(e) == 1 ? 1 : 2;
+  if (const char *e = std::getenv("NLS_PASS2"); e && std::atoi(e) != 0) {
+    const bool base = c && !ani && dim == 3 && !h->collective && h->nbasis == 1 && h->m >= 3 &&
+                      g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
+    // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS; k_pass2r: 64-aligned x
+    const bool dma = g.nyp % P2D_ROWS == 0 && g.nyp >= 4 && h->m - 4 <= P2D_MAXJ;
+    if (h->p2impl == 2 && !dma) h->p2impl = 1;
+    h->pass2 = base && (h->p2impl == 2 || (g.nx % 64 == 0 && g.nyp % 2 == 0));
+  }
   if (h->pass2) {
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("NLS_P2_IMPL")) h->p2reg = std::atoi(e) != 0;
-    const int64_t nzc = (g.npl + h->p2kz - 1) / h->p2kz;
-    if (h->p2reg) {  // one wave per 60 x RB output column, 4 waves per workgroup (grid at RB = 1)
-      h->p2grid = p2r_grid(h, 1);
-    } else {
-      h->p2grid = (int)((g.nx / 64) * (g.nyp / P2_TILE_Y) * nzc);
-    }
+    h->p2grid = 0;
+    for (int J = 0; J + 1 < h->m - 1; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
     hip_check(h, hipMalloc(&h->p2, p2state_bytes()), "hipMalloc(p2)");
     hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes(), h->stream), "hipMemset");
     hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (2 * MMAX + 8) * sizeof(cplx)),
               "hipMalloc(partP2)");
+    hip_check(h, hipMalloc(&h->zbuf, 64 * sizeof(cplx)), "hipMalloc(zbuf)");
+    hip_check(h, hipMemsetAsync(h->zbuf, 0, 64 * sizeof(cplx), h->stream), "hipMemset");
   }
   // fused tails first: a basis that always ends in one never stores W_{m-1}
-  h->fused_tail = h->m >= 3 && !h->pass2;
-  if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && std::atoi(e) != 0;
+  h->fused_tail = h->m >= 3;
+  if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && (std::atoi(e) != 0 || h->pass2);
   if (h->fused_tail) {
     Geo g2 = g;
     if (const char *e = std::getenv("NLS_KZ_ALPHA2")) h->kz_alpha2 = std::max(1, std::atoi(e));
@@ -893,8 +913,10 @@ void free_all(nls_handle *h) {
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
                   (void *)h->vel, h->xedge, (void *)h->partX, h->p2, (void *)h->partP2,
-                  (void *)h->partA, (void *)h->partU})
+                  (void *)h->zbuf, (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
+  h->p2 = nullptr;
+  h->partP2 = h->zbuf = nullptr;
   h->u = h->scratch = h->snap = h->uprev = nullptr;
   h->up = h->mf = h->cfb = h->vel = nullptr;
   h->xedge = nullptr;

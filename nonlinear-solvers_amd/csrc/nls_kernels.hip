@@ -26,6 +26,7 @@
 #include "nls_reduce.hpp"
 #include "nls_stencil.hpp"
 #include "nls_pass2.hpp"
+#include "nls_pass2d.hpp"
 
 namespace nls {
 
@@ -818,19 +819,28 @@ const void *kernel_sg_end(int M) {
   }
 }
 
-// two-vectors-per-pass Lanczos (nls_pass2.hpp): even J only
-const void *kernel_pass2(int J, bool hz, bool reg) {
+// two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp): even J only.
+// impl 2: LDS-DMA form k_p2d (J <= P2D_JMAX); 1: register-march k_pass2r
+const void *kernel_pass2(int J, bool hz, int impl) {
+  if (impl == 2) {
+    switch (J) {
+#define X(J) \
+  case J: return hz ? reinterpret_cast<const void *>(&k_p2d<J, true>) : reinterpret_cast<const void *>(&k_p2d<J, false>);
+      X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14)
+#undef X
+      default: return nullptr;
+    }
+  }
   switch (J) {
 #define X(J) \
-  case J: return reg ? (hz ? reinterpret_cast<const void *>(&k_pass2r<J, true>) \
-                           : reinterpret_cast<const void *>(&k_pass2r<J, false>)) \
-                     : (hz ? reinterpret_cast<const void *>(&k_pass2<J, true>) \
-                           : reinterpret_cast<const void *>(&k_pass2<J, false>));
+  case J: return hz ? reinterpret_cast<const void *>(&k_pass2r<J, true>) : reinterpret_cast<const void *>(&k_pass2r<J, false>);
     X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30)
 #undef X
     default: return nullptr;
   }
 }
+const void *kernel_p2tail() { return reinterpret_cast<const void *>(&k_p2tail); }
+const void *kernel_p2tfin() { return reinterpret_cast<const void *>(&k_p2tfin); }
 const void *kernel_p2coef() { return reinterpret_cast<const void *>(&k_p2coef); }
 const void *kernel_p2fin() { return reinterpret_cast<const void *>(&k_p2fin); }
 size_t p2state_bytes() { return sizeof(P2State); }

@@ -58,8 +58,13 @@ const void *kernel_reduce_final();
 //   colsum       : (const cplx* partA, int nbA, int ncA, const cplx* partU, int nbU, cplx* dst)
 //                  grid = ncA + ncU columns; dst = KState::sums (the do_sum phase, parallel)
 const void *kernel_colsum();
-// two-vectors-per-pass Lanczos (nls_pass2.hpp; 3D isotropic complex, single rank)
-const void *kernel_pass2(int J, bool hz, bool reg);  // hz: also Z; reg: register-march form
+// two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp; 3D isotropic complex, single rank)
+//   pass2 : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb[, const cplx* zbuf])
+const void *kernel_pass2(int J, bool hz, int impl);  // hz: also Z; impl 2: LDS-DMA k_p2d, 1: k_pass2r
+constexpr int P2D_WAVE_XO = 60, P2D_ROWS = 4, P2D_MAXJ = 14;  // == P2D_XO, P2D_TR, P2D_JMAX
+//   p2tail: (P2State*, KState*, const cplx* sums, int m);  p2tfin: (const P2State*, KState*, int m, int nf)
+const void *kernel_p2tail();
+const void *kernel_p2tfin();
 constexpr int P2R_WAVE_XO = 60;  // == P2R_XO
 #ifndef NLS_P2R_RB1
 #define NLS_P2R_RB1 12  // k_pass2r: one row per wave from this J (registers)
@@ -69,11 +74,6 @@ const void *kernel_p2coef();
 const void *kernel_p2fin();
 size_t p2state_bytes();
 size_t p2state_sums_offset();
-constexpr int P2_TILE_Y = 16;  // == P2_TY
-#ifndef NLS_P2_NT
-#define NLS_P2_NT 256
-#endif
-constexpr int P2_THREADS = NLS_P2_NT;  // == P2_NT (k_pass2's workgroup)
 
 // pointwise (grid-stride):
 //   nl_init   : (const cplx* u, cplx* w0, const double* mf, int64_t n, double dt, int nonlin,

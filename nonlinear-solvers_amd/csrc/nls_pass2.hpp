@@ -26,200 +26,11 @@ struct P2State {
   cplx bX1, bZ1, bZ2;
   double sigma, beta;
   cplx sums[2 * P2M + 8];
+  cplx tk[P2M];   // fused tail: t_k = W_k^H L S_{m-2} (k_p2tail)
+  double beta_t;  // fused tail: beta_{m-1}
 };
 
-constexpr int P2_TY = 16;            // rows per tile (4 waves x 4 rows)
-constexpr int P2_HY = P2_TY + 4;     // S ring rows  (rows -2 .. TY+1)
-constexpr int P2_HX = 64 + 4;        // S ring cols  (x -2 .. 65)
-constexpr int P2_LY = P2_TY + 2;     // L1 ring rows (rows -1 .. TY)
-constexpr int P2_LX = 64 + 2;        // L1 ring cols (x -1 .. 64)
-
-__device__ __forceinline__ int p2slot(int k) { return ((k % 3) + 3) % 3; }
-
-// Tiles: 64 x-cells x 16 rows of one plane, marched over kz planes by one
-// workgroup (4 waves x 4 rows; one workgroup per CU by its LDS, so up to 512
-// VGPR+AGPR per lane).  Flat indexing throughout (rows past
-// ny continue in the next plane: the reference's 3D y-wrap, laplacians.hpp:57-105),
-// so halo rows need no special case.  Per plane: the S_J ring plane two ahead is
-// stored from registers loaded one plane earlier (its HBM latency overlaps the
-// previous plane's work), L S_J of the next plane is computed into the L1 ring,
-// then each thread forms X, Z for its two cells from the J other streams.
-#ifndef NLS_P2_NT
-#define NLS_P2_NT 256
-#endif
-constexpr int P2_NT = NLS_P2_NT;
-template <int J, bool HZ>
-__global__ __launch_bounds__(P2_NT) void k_pass2(cplx *__restrict__ W, int64_t vs, Geo g,
-                                                 const P2State *__restrict__ ps,
-                                                 cplx *__restrict__ part, int nb) {
-  constexpr int NW = P2_NT / 64, RPW = P2_TY / NW;  // waves, rows per wave
-  constexpr int SE = P2_HY * P2_HX, SPT = (SE + P2_NT - 1) / P2_NT;
-  constexpr int LE = P2_LY * P2_LX;
-  constexpr int NC = HZ ? 2 * (J + 1) + 3 : J + 2;  // HZ: gX, gZ, xx, xz, zz; else gX, xx
-  // rows whose loads are issued together
-  constexpr int RU = P2_NT == 256 ? (J <= 6 ? 4 : (J <= 8 ? 2 : 1)) : (J <= 4 ? RPW : 1);
-  __shared__ cplx Sr[3][P2_HY][P2_HX];
-  __shared__ cplx Lr[3][P2_LY][P2_LX];
-  __shared__ cplx cX[J + 1], cZ[J + 1];
-  __shared__ cplx red[NW][NC];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  // 32-bit cell indices (a slab of < 2^31 cells; checked by the host)
-  const int nx = (int)g.nx, ny = (int)g.nyp, P = (int)g.P, nz = (int)g.npl;
-  const int ntx = (int)(nx / 64), nty = (int)(ny / P2_TY);
-  const int nzc = (int)((nz + g.kz - 1) / g.kz);
-  const int tile = blockIdx.x;
-  if (tile >= ntx * nty * nzc) return;  // uniform per workgroup
-  const int xt = tile % ntx, yt = (tile / ntx) % nty, zc = tile / (ntx * nty);
-  const int x0 = xt * 64, y0 = yt * P2_TY;
-  const int k0 = zc * g.kz, k1 = min(k0 + g.kz, nz);
-  for (int l = t; l <= J; l += P2_NT) {
-    cX[l] = ps->aX[l];
-    cZ[l] = ps->aZ[l];
-  }
-  const cplx bX1 = ps->bX1, bZ1 = ps->bZ1, bZ2 = ps->bZ2;
-  const double s = g.s, sdi = g.sd_in, sdb = g.sd_bd;
-  const cplx *__restrict__ SJ = W + (int64_t)J * vs;
-  cplx *__restrict__ Xo = W + (int64_t)(J + 1) * vs;
-  cplx *__restrict__ Zo = W + (int64_t)(J + 2) * vs;
-
-  // row yy of plane k (yy may be -2..ny+1): its true (row, plane); diagonal of a cell
-  auto cell_ok = [&](int k, int yy, int x, int &j, int &kk) {
-    j = yy;
-    kk = k;
-    if (yy < 0) { j += ny; kk -= 1; }
-    if (yy >= ny) { j -= ny; kk += 1; }
-    return x >= 0 && x < nx && kk >= 0 && kk < nz;
-  };
-  auto diag = [&](int x, int j, int kk) {
-    const bool bd = x == 0 || x == nx - 1 || j == 0 || j == ny - 1 || kk == 0 || kk == nz - 1;
-    return bd ? sdb : sdi;
-  };
-  cplx pre[SPT];
-  auto fetchS = [&](int k) {
-#pragma unroll
-    for (int i = 0; i < SPT; ++i) {
-      const int e = t + i * P2_NT;
-      pre[i] = {0.0, 0.0};
-      if (e < SE) {
-        const int r = e / P2_HX, c = e % P2_HX;
-        const int x = x0 - 2 + c, yy = y0 - 2 + r;
-        int j, kk;
-        if (cell_ok(k, yy, x, j, kk)) pre[i] = SJ[k * P + yy * nx + x];
-      }
-    }
-  };
-  auto storeS = [&](int k) {
-    const int sl = p2slot(k);
-#pragma unroll
-    for (int i = 0; i < SPT; ++i) {
-      const int e = t + i * P2_NT;
-      if (e < SE) Sr[sl][e / P2_HX][e % P2_HX] = pre[i];
-    }
-  };
-  auto compL1 = [&](int k) {  // L S_J at plane k, rows -1..TY, x -1..64
-    const int sp = p2slot(k - 1), sc = p2slot(k), sn = p2slot(k + 1);
-#pragma unroll 1
-    for (int e = t; e < LE; e += P2_NT) {
-      const int r = e / P2_LX, c = e % P2_LX;
-      const int x = x0 - 1 + c, yy = y0 - 1 + r;
-      int j, kk;
-      cplx v = {0.0, 0.0};
-      if (cell_ok(k, yy, x, j, kk)) {
-        const cplx nbs = Sr[sc][r + 1][c] + Sr[sc][r + 1][c + 2] + Sr[sc][r][c + 1] +
-                         Sr[sc][r + 2][c + 1] + Sr[sp][r + 1][c + 1] + Sr[sn][r + 1][c + 1];
-        v = diag(x, j, kk) * Sr[sc][r + 1][c + 1] + s * nbs;
-      }
-      Lr[p2slot(k)][r][c] = v;
-    }
-  };
-
-  cplx acc[NC];
-#pragma unroll
-  for (int i = 0; i < NC; ++i) acc[i] = {0.0, 0.0};
-
-  fetchS(k0 - 2);
-  storeS(k0 - 2);
-  fetchS(k0 - 1);
-  storeS(k0 - 1);
-  fetchS(k0);
-  storeS(k0);
-  fetchS(k0 + 1);
-  __syncthreads();
-  compL1(k0 - 1);
-  __syncthreads();
-  storeS(k0 + 1);  // the slot of k0 - 2
-  fetchS(k0 + 2);
-  __syncthreads();
-  compL1(k0);
-  __syncthreads();
-  const int x = x0 + lane;
-  // coefficients re-read from LDS at each use (broadcast reads) instead of being
-  // hoisted into 8(J+1) registers
-  const volatile cplx *vX = cX, *vZ = cZ;
-  auto ldc = [](const volatile cplx *p) { return cplx{p->re, p->im}; };
-  for (int k = k0; k < k1; ++k) {
-    storeS(k + 2);  // the slot of k - 1 (last read by compL1(k), before the last barrier)
-    fetchS(k + 3);  // in flight during this plane's work
-    __syncthreads();
-    compL1(k + 1);
-    __syncthreads();
-    const int lp = p2slot(k - 1), lc = p2slot(k), ln = p2slot(k + 1);
-#pragma unroll 1
-    for (int i0 = 0; i0 < RPW; i0 += RU) {
-      cplx sv[RU][J + 1];
-#pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        const int r = w * RPW + i0 + u;
-        const int flat = k * P + (y0 + r) * nx + x;
-#pragma unroll
-        for (int l = 0; l < J; ++l) sv[u][l] = ld_nt(W + l * vs + flat);
-        sv[u][J] = Sr[lc][r + 2][lane + 2];
-      }
-#pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        const int r = w * RPW + i0 + u;
-        const int flat = k * P + (y0 + r) * nx + x;
-        const cplx l1 = Lr[lc][r + 1][lane + 1];
-        cplx X = cmul(bX1, l1);
-#pragma unroll
-        for (int l = 0; l <= J; ++l) X += cmul(ldc(vX + l), sv[u][l]);
-#pragma unroll
-        for (int l = 0; l <= J; ++l) acc[l] += cj_mul(sv[u][l], X);
-        st_nt(Xo + flat, X);
-        if constexpr (HZ) {
-          const cplx nbs = Lr[lc][r + 1][lane] + Lr[lc][r + 1][lane + 2] + Lr[lc][r][lane + 1] +
-                           Lr[lc][r + 2][lane + 1] + Lr[lp][r + 1][lane + 1] + Lr[ln][r + 1][lane + 1];
-          const cplx l2 = diag(x, y0 + r, k) * l1 + s * nbs;
-          cplx Z = cmul(bZ2, l2) + cmul(bZ1, l1);
-#pragma unroll
-          for (int l = 0; l <= J; ++l) Z += cmul(ldc(vZ + l), sv[u][l]);
-#pragma unroll
-          for (int l = 0; l <= J; ++l) acc[J + 1 + l] += cj_mul(sv[u][l], Z);
-          acc[2 * J + 2].re += abs2(X);
-          acc[2 * J + 3] += cj_mul(X, Z);
-          acc[2 * J + 4].re += abs2(Z);
-          st_nt(Zo + flat, Z);
-        } else {
-          acc[J + 1].re += abs2(X);
-        }
-      }
-    }
-  }
-  // workgroup reduction, fixed order
-#pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const double a = wave_sum(acc[i].re), b = wave_sum(acc[i].im);
-    if (lane == 0) red[w][i] = {a, b};
-  }
-  __syncthreads();
-  for (int i = t; i < NC; i += P2_NT) {
-    cplx v = red[0][i];
-    for (int q = 1; q < NW; ++q) v += red[q][i];
-    part[(int64_t)i * nb + blockIdx.x] = v;
-  }
-}
-
-// Register-march form of the same pass (k_pass2 above is the LDS form).  Each
+// Register-march form of the same pass (the LDS-DMA form k_p2d, nls_pass2d.hpp, is the default).  Each
 // wave owns a column of 64 lanes x P2R_RB rows and marches z on its own, no LDS,
 // no barriers: lanes hold x = 60 xt - 2 + lane, of which lanes 2..61 are outputs
 // and lanes 0,1,62,63 the x halo (x neighbours by lane shuffles; L S_J is valid

@@ -35,8 +35,10 @@ sys.path.insert(0, ROOT)
 from oracle import np_ref  # noqa: E402  (design study: compared against the oracle)
 
 
-def lanczos2(apply, u, m, shift=True):
-    """T (m x m tridiagonal as the reference builds it), S (stored vectors), C, beta."""
+def lanczos2(apply, u, m, shift=True, nstore=None, raw=False):
+    """T (m x m tridiagonal as the reference builds it), S (stored vectors), C, beta.
+    nstore: stop once S_0..S_{nstore-1} are stored (the fused-tail end game);
+    raw: return (S, C, H, G, beta) at that point instead of T."""
     u = np.asarray(u, dtype=np.complex128)
     beta = np.linalg.norm(u)
     S = [u / beta]
@@ -48,7 +50,8 @@ def lanczos2(apply, u, m, shift=True):
     Cinv = np.zeros_like(C)
     J = 0
     sigma = 0.0
-    while J + 1 < m:
+    mm = m if nstore is None else nstore
+    while J + 1 < mm:
         n_s = J + 1
         Cb = C[:n_s, :n_s]
         Ci = np.linalg.inv(Cb)  # small upper-triangular inverse (device: back-substitution)
@@ -76,7 +79,7 @@ def lanczos2(apply, u, m, shift=True):
         for l in range(n_s):
             X = X + aX[l] * S[l]
             Z = Z + aZ[l] * S[l]
-        last = J + 2 >= m  # only W_{m-1} needed: no Z
+        last = J + 2 >= mm  # only one more vector needed: no Z
         gX = np.array([np.vdot(S[l], X) for l in range(n_s)])
         gZ = np.array([np.vdot(S[l], Z) for l in range(n_s)])
         xx, xz, zz = np.vdot(X, X), np.vdot(X, Z), np.vdot(Z, Z)
@@ -135,6 +138,8 @@ def lanczos2(apply, u, m, shift=True):
         if shift:
             sigma = H[J + 1, J + 1].real
         J += 2
+    if raw:
+        return S, C, H, G, beta
     # reference T: alpha_j on the diagonal (j < m-1), norms on the off-diagonals, T[m-1,m-1] = 0
     T = np.zeros((m, m))
     for j in range(m - 1):
@@ -153,6 +158,66 @@ def krylov2(apply, u, t, m, func):
     for l in range(m):
         out = out + coef[l] * S[l]
     return beta * out, C, G
+
+
+def tail_coefficients(S, C, H, beta, a, l2, m, t, func):
+    """Fused-tail end game of the two-vector scheme (the device's k_p2tail + k_tail):
+    S_0..S_j stored (j = m-2), W = S C orthonormal, H columns < j known.  One alpha
+    pass over S_j measures a = S_j^H L S_j and l2 = ||L S_j||^2; with y = L S_j,
+      t_k = W_k^H y = sum_i conj(H[i,k]) D[i,j]             (k < j, D = C^-1)
+      t_j = conj(C_jj) (a - sum_{i<j} conj(D[i,j]) t_i)
+      lw  = -C_jj H[:, :j] D[:j, j]      (L W_j = C_jj y + sum_k lw_k W_k)
+      H[k,j] = C_jj t_k + lw_k,  beta_{j+1} = |C_jj| sqrt(l2 - sum_k |t_k|^2)
+      W_{j+1} = C_jj (y - sum_k t_k W_k) / beta_{j+1}
+    returns (coef over S_0..S_j, coefficient of y, T)."""
+    j = m - 2
+    n = j + 1
+    Cj = C[:n, :n]
+    D = np.linalg.inv(Cj)
+    cjj = Cj[j, j]
+    tk = np.zeros(n, complex)
+    for k in range(j):
+        tk[k] = np.sum(np.conj(H[:k + 2, k]) * D[:k + 2, j])
+    tk[j] = np.conj(cjj) * (a - np.sum(np.conj(D[:j, j]) * tk[:j]))
+    lw = -cjj * (H[:n, :j] @ D[:j, j]) if j > 0 else np.zeros(n, complex)
+    Hj = cjj * tk + lw
+    bet = abs(cjj) * np.sqrt(max(l2 - np.sum(np.abs(tk) ** 2), 0.0))
+    T = np.zeros((m, m))
+    for i in range(j):
+        T[i, i] = H[i, i].real
+        T[i + 1, i] = T[i, i + 1] = H[i + 1, i].real
+    T[j, j] = Hj[j].real
+    T[j + 1, j] = T[j, j + 1] = bet
+    lam, Q = np.linalg.eigh(T)
+    c = Q @ (np_ref._f(func, lam, t) * Q[0, :])
+    # result = beta (sum_{k<=j} c_k W_k + c_{j+1} W_{j+1})
+    cw = c[:n] - c[j + 1] * cjj * tk / bet
+    coefS = beta * (Cj @ cw)
+    cy = beta * c[j + 1] * cjj / bet
+    return coefS, cy, T
+
+
+def krylov2_tail(apply, u, t, m, func):
+    S, C, H, G, beta = lanczos2(apply, u, m, nstore=m - 1, raw=True)
+    j = m - 2
+    y = apply(S[j])
+    a, l2 = np.vdot(S[j], y), np.vdot(y, y).real
+    coefS, cy, T = tail_coefficients(S, C, H, beta, a, l2, m, t, func)
+    out = cy * y
+    for l in range(j + 1):
+        out = out + coefS[l] * S[l]
+    return out, T
+
+
+def nlse_steps2_tail(dim, n, dx, u, dt, nsteps, m):
+    nz = n if dim == 3 else 1
+    ap = lambda v: np_ref.laplacian_apply(dim, n, n, nz, dx, dx, v)
+    u = u.ravel().astype(np.complex128).copy()
+    for _ in range(nsteps):
+        r = np_ref.nonlin_half(u, dt)
+        b, _ = krylov2_tail(ap, r, -1j * dt, m, np_ref.F_EXP_ABS)
+        u = np_ref.nonlin_half(b, dt)
+    return u
 
 
 def nlse_steps2(dim, n, dx, u, dt, nsteps, m):

@@ -1,8 +1,9 @@
-"""GPU parity of the two-vectors-per-pass Lanczos (NLS_PASS2=1, nls_pass2.hpp):
-3D isotropic NLSE trajectories and single Krylov actions against the CPU oracle,
-with the same tolerances as tests/test_gpu_parity.py, for both forms of the
-pass (register march k_pass2r, LDS tiles k_pass2).  The LDS form runs on tiles of
-64 x 16 cells, so the grids have nx % 64 == 0 and ny % 16 == 0."""
+"""GPU parity of the two-vectors-per-pass Lanczos (NLS_PASS2=1, nls_pass2.hpp,
+nls_pass2d.hpp): 3D isotropic NLSE trajectories against the CPU oracle, with the
+same tolerances as tests/test_gpu_parity.py, for both forms of the pass (LDS-DMA
+k_p2d, register march k_pass2r).  Every run ends each basis in the fused tail
+(k_alpha_l2 over S_{m-2}, k_p2tail, k_tail).  k_p2d takes 4-row tiles (ny % 4 == 0)
+and m <= 18; k_pass2r 64-aligned x; other shapes fall back to the other form."""
 import numpy as np
 import pytest
 
@@ -17,11 +18,19 @@ nls_amd = pytest.importorskip("nls_amd")
 TOL_KRYLOV, TOL_TRAJ = 1e-12, 1e-10
 
 
-@pytest.fixture(autouse=True, params=["reg", "lds"])
+@pytest.fixture(autouse=True, params=["dma", "reg"])
 def _pass2(monkeypatch, request):
     monkeypatch.setenv("NLS_PASS2", "1")
     monkeypatch.setenv("NLS_P2_KZ", "8")  # several z chunks per column of tiles
-    monkeypatch.setenv("NLS_P2_IMPL", "1" if request.param == "reg" else "0")
+    monkeypatch.setenv("NLS_P2_IMPL", "2" if request.param == "dma" else "1")
+    return request.param
+
+
+def _eligible(form, nx, ny, m):
+    """Does the handle run the two-vector pass (nls_api.cpp alloc_all)?  dma falls
+    back to the register march where its tiles do not fit, reg never falls back."""
+    reg = nx % 64 == 0 and ny % 2 == 0
+    return reg if form == "reg" else ((ny % 4 == 0 and m <= 18) or reg)
 
 
 def _ran_pass2(s, m):
@@ -32,9 +41,10 @@ def _ran_pass2(s, m):
 
 
 @pytest.mark.parametrize("nx,ny,nz,m", [(64, 16, 12, 16), (64, 32, 20, 10), (128, 16, 9, 15),
-                                        (64, 16, 16, 25), (64, 16, 10, 3), (64, 48, 8, 4)])
+                                        (64, 16, 16, 25), (64, 16, 10, 3), (64, 48, 8, 4),
+                                        (64, 20, 11, 18), (50, 12, 13, 16), (130, 8, 9, 5)])
 @pytest.mark.parametrize("eq", [0, 1])
-def test_pass2_trajectory_matches_oracle(nx, ny, nz, m, eq):
+def test_pass2_trajectory_matches_oracle(_pass2, nx, ny, nz, m, eq):
     L = 10.0
     dx = spacing(nx, L)
     u0 = soliton_field(3, nx, ny, nz, L, seed=11)
@@ -47,7 +57,7 @@ def test_pass2_trajectory_matches_oracle(nx, ny, nz, m, eq):
         s.set_timing(True)
         s.step(dt, nsteps)
         u = s.get_field()
-        assert _ran_pass2(s, m)
+        assert _ran_pass2(s, m) == _eligible(_pass2, nx, ny, m)
     assert np.all(np.isfinite(u))
     assert rel_l2(u, ref) <= TOL_TRAJ
 

@@ -43,6 +43,8 @@ TOL = 1e-10
 LARGE = {"NLS_FUSED_ALPHA": "1", "NLS_GRID_MULT": "16", "NLS_KZ": "1", "NLS_KZ_ALPHA": "4",
          "NLS_FUSED_TAIL": "1"}
 PLAIN = {"NLS_FUSED_ALPHA": "0", "NLS_FUSED_TAIL": "1"}
+# two new vectors per basis pass (LDS-DMA k_p2d), several z chunks per tile column
+PASS2 = {"NLS_PASS2": "1", "NLS_P2_KZ": "8", "NLS_P2_IMPL": "2"}
 
 
 def _with_env(env, fn):
@@ -142,18 +144,20 @@ STIFF = [(3, 128, 20.0 / 511), (2, 1024, 20.0 / 4095)]
 
 @pytest.mark.parametrize("dim,n,dx", STIFF, ids=["3d128_dx512", "2d1024_dx4096"])
 @pytest.mark.parametrize("eq", [0, 1], ids=["cubic", "cq"])
-@pytest.mark.parametrize("mode", ["large", "plain"])
+@pytest.mark.parametrize("mode", ["large", "plain", "pass2"])
 def test_nlse_stiff_matches_oracle(dim, n, dx, eq, mode):
     m, dt = 16, 1e-3
+    if mode == "pass2" and dim != 3:
+        pytest.skip("the two-vector pass is 3D only")
     u0 = _ic(dim, n, dx, 41 + eq)
-    env = LARGE if mode == "large" else PLAIN
+    env = {"large": LARGE, "plain": PLAIN, "pass2": PASS2}[mode]
     gpu, tm = _gpu_nlse(dim, n, dx, u0, dt, m, eq, env)
     steps = CHECK[-1]
     assert all(np.all(np.isfinite(v)) for v in gpu.values())
     # the fused tail ran every step; with the folded alpha only alpha_0 and the
     # tail's k_alpha_l2 remain per step (2 alpha launches instead of m - 1)
     assert tm["class_count"]["final"] == steps
-    if mode == "large":
+    if mode in ("large", "pass2"):
         assert tm["class_count"]["alpha"] == 2 * steps
     else:
         assert tm["class_count"]["alpha"] == (m - 1) * steps
