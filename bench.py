@@ -411,10 +411,29 @@ def main():
 
     # dominant kernel: the fused final pass k_final_fused<m> when the step uses it
     # (NLSE, m >= 3: W_0..W_{m-2} read, u and the next W_0 written, + m(x) on G2),
-    # else the largest update pass k_update<J = m-2> (J+1 reads + 1 write)
+    # else the largest update pass k_update<J = m-2> (J+1 reads + 1 write); with
+    # the two-vector passes (update launches at even J only) the longer of the
+    # tail and the largest pass k_p2d<J> (J+1 reads + 2 writes)
     esz = 8 if w["eq"] in (2, 4) else 16
     fcnt = tm["class_count"].get("final", 0)
-    if fcnt and w["eq"] in (0, 1, 3) and not w.get("sewi"):
+    ucnt = tm["update_count"]
+    pass2 = m >= 4 and ucnt[0] > 0 and all(ucnt[j] == 0 for j in range(1, m - 1, 2))
+    p2J = max([j for j, c in enumerate(ucnt) if c] or [0])
+    p2_ms = tm["update_ms"][p2J] / ucnt[p2J] if pass2 and ucnt[p2J] else 0.0
+    tail_ms = tm["class_ms"]["final"] / fcnt if fcnt else 0.0
+    own_bytes = None
+    if pass2:  # alpha_0 + sum_J (J+1 reads + 2 or 1 writes) + the tail's alpha + tail (m+1)
+        own_bytes = esz * (1 + sum(J + 3 if J + 2 < m - 1 else J + 2 for J in range(0, m - 2, 2)) + 1 + (m + 1))
+    if pass2 and p2_ms > tail_ms:
+        J = p2J
+        cnt = ucnt[J]
+        avg_ms = p2_ms
+        hz = J + 2 < m - 1
+        bytes_launch = (J + 1 + (2 if hz else 1)) * esz * n_local
+        kname = f"k_p2d<J={J}> (two-vector Lanczos pass: radius-2 stencil + CGS coefficients, " \
+                f"{J + 1} reads + {2 if hz else 1} writes)"
+        kprefix = "k_p2d<"
+    elif fcnt and w["eq"] in (0, 1, 3) and not w.get("sewi"):
         J = m - 2
         cnt = fcnt
         avg_ms = tm["class_ms"]["final"] / fcnt
@@ -470,6 +489,9 @@ def main():
             "achieved_GBs": step_bytes / (step_ms * 1e-3) / 1e9,
             "frac": step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "gpu_kernel_ms_per_step": {k: v / max(tm["steps"], 1) for k, v in tm["class_ms"].items()},
+            "lanczos": "two-vector passes (k_p2d) + fused tail" if pass2 else "one-vector passes + fused tail",
+            "moved_bytes_per_cell_step": own_bytes,
+            "moved_GBs": own_bytes * n_local / (step_ms * 1e-3) / 1e9 if own_bytes else None,
         },
     }
     s.close()

@@ -115,7 +115,7 @@ struct nls_handle {
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
   int p2impl = 2;              // 2: LDS-DMA k_p2d; 1: register-march k_pass2r (NLS_P2_IMPL)
-  cplx *zbuf = nullptr;        // 1 KiB of zeros: the DMA source of out-of-grid cells
+  cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
@@ -780,8 +780,9 @@ void alloc_all(nls_handle *h) {
     hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes(), h->stream), "hipMemset");
     hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (2 * MMAX + 8) * sizeof(cplx)),
               "hipMalloc(partP2)");
-    hip_check(h, hipMalloc(&h->zbuf, 64 * sizeof(cplx)), "hipMalloc(zbuf)");
-    hip_check(h, hipMemsetAsync(h->zbuf, 0, 64 * sizeof(cplx), h->stream), "hipMemset");
+    const size_t zb = (size_t)std::max<int64_t>(g.nx, 64) * sizeof(cplx);
+    hip_check(h, hipMalloc(&h->zbuf, zb), "hipMalloc(zbuf)");
+    hip_check(h, hipMemsetAsync(h->zbuf, 0, zb, h->stream), "hipMemset");
   }
   // fused tails first: a basis that always ends in one never stores W_{m-1}
   h->fused_tail = h->m >= 3;

@@ -7,26 +7,32 @@
 // bytes in flight (the register-march k_pass2r streamed at ~55 % of the
 // pattern's rate).  Here every byte the pass reads moves HBM -> LDS by
 // global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR destination),
-// issued D planes ahead of its use, so the in-flight bytes no longer compete
+// issued ahead of its use, so the in-flight bytes no longer compete
 // with the accumulators for registers:
 //
-//   workgroup = 4 waves = one tile of 60 x-cells x 4 rows (one row per wave),
-//               marched over kz planes; one workgroup per CU (LDS-bound).
-//   S ring:     S_J rows y0-2 .. y0+5 of D+3 planes (shared by the 4 waves;
+//   workgroup = 4 waves = one tile of 64 x-cells x 4 rows (one row per wave),
+//               marched over kz planes; one or two workgroups per CU (p2d_occ).
+//   S ring:     S_J rows y0-2 .. y0+5 of DS+3 planes (shared by the 4 waves;
 //               each wave DMAs 2 rows of each plane).  L S_J of the next plane
 //               is computed from it for the wave's rows -1, 0, +1 and kept in a
 //               register queue (3 planes), L^2 S_J of the current plane from
 //               that queue (x neighbours by lane shuffles).
 //   J ring:     the J other stored vectors S_0..S_{J-1} of the wave's row,
-//               D+1 planes per wave (private to the wave).
-//   lanes:      x = x0 - 2 + lane; lanes 2..61 are outputs (L S_J valid on
-//               1..62, L^2 S_J on 2..61).
+//               RS rows of 1 KiB per wave (private to the wave): RS/J planes,
+//               as deep as the LDS left by the S ring allows (2.2 planes at
+//               J = 14, up to 5).
+//   lanes:      x = x0 + lane, x0 a multiple of 64: every streamed row is one
+//               aligned 1 KiB (a 60-wide tile read 20 % more than it used:
+//               9 lines per 1 KiB and the x halo, PMC-measured).  The S_J rows
+//               add their 4 x-halo cells by a 4-byte DMA on 16 lanes; the two
+//               L S_J values just outside the tile come from one extra pass.
 //
 // Completion is counted by hand (hipcc does not track LDS-DMA writes): every
 // wave issues, per step, exactly one group of J + 2 DMAs (its 2 S rows of
-// plane k+D+2, its J rows of plane k+D) followed by STW (1 or 2) stores, so
-// the group a step needs is retired by a constant s_waitcnt vmcnt(N_i)
-// (N_i below); groups beyond the tile's planes DMA a zero block instead, and
+// plane k+DS+2, the next J rows of its J ring) followed by STW (1 or 2)
+// stores, so the ops issued after the last one a step needs are a known count
+// N_i and s_waitcnt vmcnt(N_i) retires exactly that much; groups beyond the
+// tile's planes DMA a zero row (zbuf, nx cells) instead, and
 // stores from non-output lanes duplicate an output lane's store (same value,
 // same address), so no instruction is ever skipped by an all-false branch.
 // A raw s_barrier after the wait publishes the other waves' S rows.
@@ -35,40 +41,127 @@
 
 namespace nls {
 
-constexpr int P2D_XO = 60;            // output x per wave
+constexpr int P2D_XO = 64;            // output x per wave (128-B aligned rows)
 constexpr int P2D_TR = 4;             // rows per tile (one per wave)
 constexpr int P2D_SR = P2D_TR + 4;    // S_J rows staged per plane (y0-2 .. y0+5)
+constexpr int P2D_SRB = 1024 + 64;    // bytes per staged S_J row: x0..x0+63, then x0-2, x0-1, x0+64, x0+65
+constexpr int P2D_LR = P2D_TR + 2;    // L S_J rows shared per plane (y0-1 .. y0+4)
 constexpr int P2D_JMAX = 14;          // largest J whose rings fit 160 KiB of LDS
-__host__ __device__ constexpr int p2d_depth(int J) {  // planes of DMA lookahead
-  return J >= 8 ? 1 : J >= 6 ? 2 : J >= 4 ? 3 : J >= 2 ? 4 : 6;
+constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
+#ifndef NLS_P2D_OCC2_MAXJ
+#define NLS_P2D_OCC2_MAXJ 2   // two workgroups per CU up to this J (measured: J = 2 yes, J = 4 no)
+#endif
+#ifndef NLS_P2D_EARLY
+#define NLS_P2D_EARLY 1  // issue a step's DMAs before its wait (needs the extra S slot)
+#endif
+#ifndef NLS_P2D_NP_MAX
+#define NLS_P2D_NP_MAX 5      // J-ring depth cap in planes
+#endif
+// Workgroups per CU: two where the registers (<= 256 per lane) and the rings
+// (<= 80 KiB) allow, so the second workgroup's waves cover the first's barriers
+// and LDS latencies; one for the long passes.
+__host__ __device__ constexpr int p2d_occ(int J) { return J <= NLS_P2D_OCC2_MAXJ ? 2 : 1; }
+// S ring: the planes k .. k+2 being read, DS planes of look-ahead and the slot of
+// plane k-2 (free since the previous step's barrier), into which a step issues
+// before its own wait and barrier
+__host__ __device__ constexpr int p2d_ds(int J) {
+  return p2d_occ(J) == 2 ? (J == 0 ? 3 : 2) : (J == 0 ? 6 : (J <= 6 ? 3 : (J <= 12 || !NLS_P2D_EARLY ? 1 : 0)));
 }
-__host__ __device__ constexpr int p2d_nsl(int J) { return p2d_depth(J) + 3; }
-__host__ __device__ constexpr int p2d_nj(int J) { return p2d_depth(J) + 1; }
-// byte offsets inside the one LDS array
-__host__ __device__ constexpr int p2d_off_j(int J) { return p2d_nsl(J) * P2D_SR * 64 * 16; }
-__host__ __device__ constexpr int p2d_off_c(int J) { return p2d_off_j(J) + p2d_nj(J) * P2D_TR * (J > 0 ? J : 1) * 64 * 16; }
+__host__ __device__ constexpr int p2d_nsl(int J) { return p2d_ds(J) + 3 + NLS_P2D_EARLY; }
+__host__ __device__ constexpr int p2d_off_l(int J) { return p2d_nsl(J) * P2D_SR * P2D_SRB; }
+__host__ __device__ constexpr int p2d_off_j(int J) { return p2d_off_l(J) + 2 * P2D_LR * 1024; }
+__host__ __device__ constexpr int p2d_avail(int J) {
+  return P2D_LDS / p2d_occ(J) - p2d_off_j(J) - 2 * (J + 1) * 16;
+}
+// J ring: NP whole planes of the J stored vectors of the wave's row (1 KiB each),
+// the plane being read + NP-1 planes of look-ahead
+__host__ __device__ constexpr int p2d_np(int J) {
+  return J == 0 ? 0
+                : (p2d_avail(J) / (P2D_TR * 1024 * J) < NLS_P2D_NP_MAX ? p2d_avail(J) / (P2D_TR * 1024 * J)
+                                                                       : NLS_P2D_NP_MAX);
+}
+__host__ __device__ constexpr int p2d_off_c(int J) { return p2d_off_j(J) + p2d_np(J) * J * P2D_TR * 1024; }
 __host__ __device__ constexpr int p2d_lds_bytes(int J) { return p2d_off_c(J) + 2 * (J + 1) * 16; }
+__host__ __device__ constexpr bool p2d_rings_ok(int J) {
+  return J == 0 || (J <= P2D_JMAX && p2d_np(J) >= 2 && p2d_lds_bytes(J) * p2d_occ(J) <= P2D_LDS);
+}
+static_assert(p2d_rings_ok(2) && p2d_rings_ok(4) && p2d_rings_ok(6) && p2d_rings_ok(8) && p2d_rings_ok(10) &&
+              p2d_rings_ok(12) && p2d_rings_ok(14), "rings do not fit the LDS");
 
-__device__ __forceinline__ void dma16(const cplx *g, char *lds, unsigned aux) {
+// VMEM ops issued after the last one step i needs, up to its wait (see k_p2d):
+// per step the wave issues [4 S-row DMAs (2 rows: main + halo)][J J-row DMAs]
+// (then waits, with NLS_P2D_EARLY) ... [STW stores]; the prologue issues the S
+// groups of planes k0+2 .. k0+1+DS, then the J planes 0 .. NP-2.  Step i needs
+// S(k+2) and J plane k.
+constexpr int P2D_NSD = 4;  // S DMAs per wave and plane
+__host__ __device__ constexpr int p2d_after(int J, int STW, int i) {
+  const int DS = p2d_ds(J), NP = p2d_np(J), G = P2D_NSD + J + STW, own = NLS_P2D_EARLY ? P2D_NSD + J : 0;
+  // S(k+2): issued by step i-DS (first group; at i itself when DS = 0) or the prologue
+  const int nS = i >= DS ? (DS == 0 ? J : J + STW + (DS - 1) * G + own)
+                         : P2D_NSD * (DS - 1 - i) + (NP > 0 ? NP - 1 : 0) * J + i * G + own;
+  if (J == 0) return nS;
+  const int nJ = i >= NP - 1 ? STW + (NP - 2) * G + own : (NP - 2 - i) * J + i * G + own;
+  return nJ < nS ? nJ : nS;
+}
+__host__ __device__ constexpr int p2d_i0(int J) {
+  return J == 0 ? p2d_ds(J) : (p2d_np(J) - 1 > p2d_ds(J) ? p2d_np(J) - 1 : p2d_ds(J));
+}
+template <int N> __device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 0 ? 0 : (N > 63 ? 63 : N)) : "memory");
+}
+template <int J, int STW, int I = 0> __device__ __forceinline__ void wait_step(int i) {
+  if constexpr (I >= p2d_i0(J)) {
+    wait_vm<p2d_after(J, STW, I)>();
+  } else {
+    if (i == I) {
+      wait_vm<p2d_after(J, STW, I)>();
+      return;
+    }
+    wait_step<J, STW, I + 1>(i);
+  }
+}
+
+// 16 lanes x 4 B (one 64-B piece: the four halo cells of a staged row) into lds
+__device__ __forceinline__ void dma4(const void *base, uint32_t voff, char *lds) {
+  const void *g = static_cast<const char *>(base) + voff;
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
+}
+// one wave-instruction: 64 lanes x 16 B from base + voff (base wave-uniform, so the
+// SGPR-base + 32-bit VGPR-offset form is selected) into lds .. lds + 1 KiB
+__device__ __forceinline__ void dma16(const void *base, uint32_t voff, char *lds, unsigned aux) {
+  const void *g = static_cast<const char *>(base) + voff;
   if (aux) __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 2);
   else __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
 }
-template <int N> __device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// wait for the group issued for step i: N_i = NB + STW * min(i, D)
-template <int NB, int STW, int D, int I = 0> __device__ __forceinline__ void wait_group(int i) {
-  if constexpr (I >= D) {
-    wait_vm<NB + STW * D>();
+// lane i <- lane i-1 / i+1 by DPP wave shifts (GFX9 wave_shr:1 / wave_shl:1; the
+// lane shifted in from outside the wave reads 0)
+__device__ __forceinline__ double dpp_d(double v, int ctrl_shr) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  int a, b;
+  if (ctrl_shr) {
+    a = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xf, 0xf, true);
+    b = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xf, 0xf, true);
   } else {
-    if (i == I) {
-      wait_vm<NB + STW * I>();
-      return;
-    }
-    wait_group<NB, STW, D, I + 1>(i);
+    a = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xf, 0xf, true);
+    b = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xf, 0xf, true);
   }
+  return __hiloint2double(b, a);
 }
+// acc += a b and acc += conj(a) b as four FMAs (no rounded product temporaries)
+__device__ __forceinline__ void cmac(cplx &acc, cplx a, cplx b) {
+  acc.re = fma(a.re, b.re, acc.re);
+  acc.re = fma(-a.im, b.im, acc.re);
+  acc.im = fma(a.re, b.im, acc.im);
+  acc.im = fma(a.im, b.re, acc.im);
+}
+__device__ __forceinline__ void cjmac(cplx &acc, cplx a, cplx b) {
+  acc.re = fma(a.re, b.re, acc.re);
+  acc.re = fma(a.im, b.im, acc.re);
+  acc.im = fma(a.re, b.im, acc.im);
+  acc.im = fma(-a.im, b.re, acc.im);
+}
+__device__ __forceinline__ cplx lane_prev(cplx v) { return {dpp_d(v.re, 1), dpp_d(v.im, 1)}; }
+__device__ __forceinline__ cplx lane_next(cplx v) { return {dpp_d(v.re, 0), dpp_d(v.im, 0)}; }
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -76,22 +169,24 @@ __device__ __forceinline__ void raw_barrier() {
 }
 
 template <int J, bool HZ>
-__global__ __launch_bounds__(NTHREADS, 1) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
-                                                     const P2State *__restrict__ ps,
-                                                     cplx *__restrict__ part, int nb,
-                                                     const cplx *__restrict__ zbuf) {
-  static_assert(J <= P2D_JMAX, "rings exceed LDS");
-  constexpr int D = p2d_depth(J), NSL = p2d_nsl(J), NJ = p2d_nj(J);
-  constexpr int STW = HZ ? 2 : 1;           // stores per step
-  constexpr int NB = (D - 1) * (J + 2);     // DMAs of the groups issued after the awaited one
+__global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
+                                                              const P2State *__restrict__ ps,
+                                                              cplx *__restrict__ part, int nb,
+                                                              const cplx *__restrict__ zbuf) {
+  static_assert(p2d_rings_ok(J), "rings exceed LDS");
+  constexpr int DS = p2d_ds(J), NSL = p2d_nsl(J), NP = p2d_np(J);
+  constexpr int STW = HZ ? 2 : 1;            // stores per step
   constexpr int NC = HZ ? 2 * (J + 1) + 3 : J + 2;
-  constexpr int JS = J > 0 ? J : 1;
+  constexpr int NPD = NP > 0 ? NP : 1;
+  constexpr int RW = P2D_SRB / 16;           // cplx per staged S row (68)
   __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J)];
-  cplx *Sr = reinterpret_cast<cplx *>(smem);                    // [NSL][P2D_SR][64]
-  cplx *Jr = reinterpret_cast<cplx *>(smem + p2d_off_j(J));     // [NJ][4][JS][64]
-  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J));     // [J+1]
-  cplx *cZ = cX + (J + 1);                                      // [J+1]
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const cplx *Sr = reinterpret_cast<const cplx *>(smem);             // [NSL][P2D_SR][RW]
+  cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J));          // [2][P2D_LR][64]
+  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J));          // [J+1]
+  cplx *cZ = cX + (J + 1);                                           // [J+1]
+  // w through readfirstlane: wave-uniform for the compiler too, so row and plane
+  // logic stays scalar
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int nx = (int)g.nx, ny = (int)g.nyp, P = (int)g.P, nz = (int)g.npl;
   const int ntx = (nx + P2D_XO - 1) / P2D_XO, nty = ny / P2D_TR;
   const int nzc = (nz + g.kz - 1) / g.kz;
@@ -103,154 +198,226 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_p2d(cplx *__restrict__ W, int64
   const int yt = tile % nty, rest = tile / nty, xt = rest % ntx, zc = rest / ntx;
   const int x0 = xt * P2D_XO, y0 = yt * P2D_TR;
   const int k0 = zc * g.kz, k1 = min(k0 + g.kz, nz);
-  const int x = x0 - 2 + lane;
-  const bool xin = x >= 0 && x < nx;
-  const int nvalid = min(P2D_XO, nx - x0);  // output lanes 2 .. nvalid+1
-  const bool out = lane >= 2 && lane < 2 + nvalid;
-  const int src_lane = lane < 2 ? 2 : (lane >= 2 + nvalid ? 1 + nvalid : lane);
+  const int x = x0 + lane;
+  const bool xin = x < nx;
+  const bool full = x0 + P2D_XO <= nx;                    // uniform
+  const int src_lane = xin ? lane : nx - 1 - x0;          // last valid lane of a ragged tile
   const int y = y0 + w;  // this wave's row (ny % 4 == 0: always a real row)
-
   for (int l = t; l <= J; l += NTHREADS) {
     cX[l] = ps->aX[l];
     cZ[l] = ps->aZ[l];
   }
   const cplx bX1 = ps->bX1, bZ1 = ps->bZ1, bZ2 = ps->bZ2;
   const double s = g.s, sdi = g.sd_in, sdb = g.sd_bd;
-  const cplx *__restrict__ SJ = W + (int64_t)J * vs;
+  const int64_t P16 = (int64_t)P * 16;
+  const char *__restrict__ SJb = reinterpret_cast<const char *>(W + (int64_t)J * vs);
   cplx *__restrict__ Xo = W + (int64_t)(J + 1) * vs;
   cplx *__restrict__ Zo = W + (int64_t)(J + 2) * vs;
   __syncthreads();  // coefficients in LDS (no DMA in flight yet)
 
-  // (no lambdas capturing by reference here: hipcc kept their captures on the
+  // per lane: the cell byte offset (clamped into the row; unused when outside),
+  // the halo piece (lanes 0..15: dword lane&3 of cell x0-2, x0-1, x0+64, x0+65)
+  auto clampx = [nx](int v) { return v < 0 ? 0 : (v >= nx ? nx - 1 : v); };
+  const uint32_t xoff = (uint32_t)clampx(x) * 16u;
+  const int hc = (lane >> 2) & 3;
+  const uint32_t hoff = (uint32_t)clampx(hc < 2 ? x0 - 2 + hc : x0 + 62 + hc) * 16u + (uint32_t)(lane & 3) * 4u;
+  // L S_J positions: main lane i -> x0 + i (row index i, x neighbours i-1 / i+1,
+  // the halo cells 65 / 66 at the tile edges); extra pass lane 0 -> x0-1, lane 1
+  // -> x0+64 (row indices 65 / 66, neighbours 64,0 / 63,67)
+  const int mi = lane > 0 ? lane - 1 : 65, pi = lane < 63 ? lane + 1 : 66;
+  const int xe = lane == 1 ? x0 + 64 : x0 - 1;
+  const int eci = lane == 1 ? 66 : 65, emi = lane == 1 ? 63 : 64, epi = lane == 1 ? 67 : 0;
+  // (macros, not lambdas capturing by reference: hipcc kept such captures on the
   // stack, and every scratch access is a VMEM op that breaks the vmcnt counting)
 #define P2D_PLANE(p, yy) ((yy) < 0 ? (p) - 1 : ((yy) >= ny ? (p) + 1 : (p)))
 #define P2D_ROW(yy) ((yy) < 0 ? (yy) + ny : ((yy) >= ny ? (yy) - ny : (yy)))
-#define P2D_DIAG(j, kk) \
-  ((xedge || (j) == 0 || (j) == ny - 1 || (kk) == 0 || (kk) == nz - 1) ? sdb : sdi)
-#define P2D_SSLOT(p) (((p) - k0 + 2) % NSL)
-  const bool xedge = x == 0 || x == nx - 1;
-  // DMA this wave's two S_J rows of plane p (zero block past the tile's last needed plane)
-#define P2D_ISSUE_S(p)                                                                  \
+#define P2D_DIAG(xx, j, kk) \
+  ((((xx) == 0) | ((xx) == nx - 1) | ((j) == 0) | ((j) == ny - 1) | ((kk) == 0) | ((kk) == nz - 1)) ? sdb : sdi)
+  // DMA this wave's two S_J rows of plane p into ring slot sl: the 64 aligned
+  // cells and the 4 halo cells (the zero row outside the grid and past the
+  // tile's last needed plane)
+#define P2D_ISSUE_S(p, sl)                                                              \
   do {                                                                                  \
     const int p_ = (p);                                                                 \
-    char *dst_ = smem + (P2D_SSLOT(p_) * P2D_SR + 2 * w) * 1024;                        \
+    char *dst_ = smem + ((sl) * P2D_SR + 2 * w) * P2D_SRB;                              \
     _Pragma("unroll") for (int r_ = 0; r_ < 2; ++r_) {                                  \
       const int yy_ = y0 - 2 + 2 * w + r_, kk_ = P2D_PLANE(p_, yy_);                    \
-      const bool ok_ = xin && kk_ >= 0 && kk_ < nz && p_ <= k1 + 1;                     \
-      dma16(ok_ ? SJ + (p_ * P + yy_ * nx + x) : zbuf + lane, dst_ + r_ * 1024, 0);     \
+      const bool ok_ = kk_ >= 0 && kk_ < nz && p_ <= k1 + 1;                            \
+      const char *b_ = ok_ ? SJb + (p_ * P16 + (int64_t)yy_ * nx * 16)                  \
+                           : reinterpret_cast<const char *>(zbuf);                      \
+      dma16(b_, xoff, dst_ + r_ * P2D_SRB, 0);                                          \
+      if (lane < 16) dma4(b_, hoff, dst_ + r_ * P2D_SRB + 1024);                        \
     }                                                                                   \
   } while (0)
-  // DMA the J stored vectors of this wave's row of plane p into J slot (i % NJ)
-#define P2D_ISSUE_J(p, i)                                                               \
+  // DMA the J stored vectors of this wave's row of plane p into J-ring slot sl
+  // (planes past the tile load the zero row)
+  const char *sb[J > 0 ? J : 1];
+#pragma unroll
+  for (int l = 0; l < J; ++l) sb[l] = reinterpret_cast<const char *>(W + l * vs) + (int64_t)y * nx * 16;
+#define P2D_ISSUE_J(p, sl)                                                              \
   do {                                                                                  \
     const int p_ = (p);                                                                 \
-    char *dst_ = smem + p2d_off_j(J) + ((((i) % NJ) * P2D_TR + w) * JS) * 1024;          \
-    const bool ok_ = out && p_ < k1;                                                    \
-    const int off_ = ok_ ? p_ * P + y * nx + x : 0;                                     \
-    _Pragma("unroll") for (int l_ = 0; l_ < J; ++l_)                                    \
-      dma16(ok_ ? W + (l_ * vs + off_) : zbuf + lane, dst_ + l_ * 1024, 1);             \
+    const int64_t po_ = p_ * P16;                                                       \
+    char *dst_ = smem + p2d_off_j(J) + (((sl) * J) * P2D_TR + w) * 1024;                \
+    _Pragma("unroll") for (int l_ = 0; l_ < J; ++l_) {                                  \
+      const void *b_ = p_ < k1 ? (const void *)(sb[l_] + po_) : (const void *)zbuf;    \
+      dma16(b_, xoff, dst_ + l_ * P2D_TR * 1024, 1);                                    \
+    }                                                                                   \
   } while (0)
-  const int lm = lane > 0 ? lane - 1 : 0, lp = lane < 63 ? lane + 1 : 63;
-  // L S_J at plane p for S tile row tr (yy = y0 - 2 + tr), from ring planes p-1, p, p+1
-#define P2D_LAP(dst, p, tr)                                                             \
+  // L S_J at plane p, S tile row tr (yy = y0 - 2 + tr), x position xx with row
+  // indices ci (centre), mi_ / pi_ (x - 1 / x + 1), from ring slots sm, sc, sp
+  // (planes p-1, p, p+1)
+#define P2D_LAP(dst, p, tr, sm, sc, sp, xx, ci, mi_, pi_)                               \
   do {                                                                                  \
-    const int p_ = (p), tr_ = (tr);                                                     \
-    const cplx *Sm_ = Sr + P2D_SSLOT(p_ - 1) * (P2D_SR * 64);                           \
-    const cplx *Sc_ = Sr + P2D_SSLOT(p_) * (P2D_SR * 64);                               \
-    const cplx *Sp_ = Sr + P2D_SSLOT(p_ + 1) * (P2D_SR * 64);                           \
+    const int p_ = (p), tr_ = (tr), xx_ = (xx);                                         \
+    const cplx *Sm_ = Sr + ((sm) * P2D_SR + tr_) * RW;                                  \
+    const cplx *Sc_ = Sr + ((sc) * P2D_SR + tr_) * RW;                                  \
+    const cplx *Sp_ = Sr + ((sp) * P2D_SR + tr_) * RW;                                  \
     const int yy_ = y0 - 2 + tr_, kk_ = P2D_PLANE(p_, yy_);                             \
-    const cplx c_ = Sc_[tr_ * 64 + lane];                                               \
-    const cplx xm_ = Sc_[tr_ * 64 + lm], xp_ = Sc_[tr_ * 64 + lp];                      \
-    const cplx ym_ = Sc_[(tr_ - 1) * 64 + lane], yp_ = Sc_[(tr_ + 1) * 64 + lane];      \
-    const cplx zm_ = Sm_[tr_ * 64 + lane], zp_ = Sp_[tr_ * 64 + lane];                  \
-    const double dg_ = P2D_DIAG(P2D_ROW(yy_), kk_);                                     \
-    const bool ok_ = xin && kk_ >= 0 && kk_ < nz;                                       \
+    const cplx c_ = Sc_[(ci)];                                                          \
+    const cplx xm_ = xx_ > 0 ? Sc_[(mi_)] : cplx{0.0, 0.0};                             \
+    const cplx xp_ = xx_ + 1 < nx ? Sc_[(pi_)] : cplx{0.0, 0.0};                        \
+    const cplx ym_ = Sc_[(ci) - RW], yp_ = Sc_[(ci) + RW];                              \
+    const cplx zm_ = Sm_[(ci)], zp_ = Sp_[(ci)];                                        \
+    const double dg_ = P2D_DIAG(xx_, P2D_ROW(yy_), kk_);                                \
+    const bool ok_ = xx_ >= 0 && xx_ < nx && kk_ >= 0 && kk_ < nz;                      \
     const cplx v_ = dg_ * c_ + s * (((zm_ + zp_) + (xm_ + xp_)) + (ym_ + yp_));         \
     dst = ok_ ? v_ : cplx{0.0, 0.0};                                                    \
+  } while (0)
+  // per plane a wave computes L S_J of its own row (main lanes, kept in a
+  // register; extra pass: the two x-halo values, lanes 0 / 1), and on the edge
+  // waves the tile's halo row (L row 0 on wave 0, P2D_LR-1 on wave 3); the main
+  // rows go to the L ring for the y neighbours of the other waves' L^2 S_J
+#define P2D_LROWS(p, sm, sc, sp, slot, own, ext)                                        \
+  do {                                                                                  \
+    P2D_LAP(own, p, w + 2, sm, sc, sp, x, lane, mi, pi);                                \
+    P2D_LAP(ext, p, w + 2, sm, sc, sp, xe, eci, emi, epi);                              \
+    Lr[((slot) * P2D_LR + w + 1) * 64 + lane] = own;                                    \
+    if (w == 0 || w == P2D_TR - 1) {                                                    \
+      const int er_ = w == 0 ? 0 : P2D_LR - 1;                                          \
+      cplx e_;                                                                          \
+      P2D_LAP(e_, p, er_ + 1, sm, sc, sp, x, lane, mi, pi);                             \
+      Lr[((slot) * P2D_LR + er_) * 64 + lane] = e_;                                     \
+    }                                                                                   \
   } while (0)
 
   cplx acc[NC];
 #pragma unroll
-  for (int i = 0; i < NC; ++i) acc[i] = {0.0, 0.0};
+  for (int c = 0; c < NC; ++c) acc[c] = {0.0, 0.0};
 
-  // prologue: S planes k0-2 .. k0+1, L S_J of planes k0-1 (centre row) and k0
-  for (int p = k0 - 2; p <= k0 + 1; ++p) P2D_ISSUE_S(p);
+  // prologue: S planes k0-2 .. k0+1 (slots 0..3), L S_J of planes k0-1 (own row,
+  // register) and k0 (own row + halo values; L ring slot 0); then the look-ahead
+  // S planes and J planes
+  for (int p = k0 - 2; p <= k0 + 1; ++p) P2D_ISSUE_S(p, p - k0 + 2);
   wait_vm<0>();
   raw_barrier();
-  cplx lq0;      // L S_J(k-1), centre row
-  cplx lq1[3];   // L S_J(k), rows -1, 0, +1
-  P2D_LAP(lq0, k0 - 1, w + 2);
+  cplx lq0, lq1, le1;  // L S_J of planes k-1 and k (own row), halo values of plane k
+  P2D_LAP(lq0, k0 - 1, w + 2, 0, 1, 2, x, lane, mi, pi);
+  P2D_LROWS(k0, 1, 2, 3, 0, lq1, le1);
+  raw_barrier();  // L ring slot 0 published; every wave is done with S slot 0 (plane k0-2)
 #pragma unroll
-  for (int r = 0; r < 3; ++r) P2D_LAP(lq1[r], k0, w + 1 + r);
-  raw_barrier();  // every wave is done with the slot of plane k0-2
+  for (int d = 0; d < DS; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
+  if constexpr (J > 0) {
 #pragma unroll
-  for (int i = 0; i < D; ++i) {
-    P2D_ISSUE_S(k0 + 2 + i);
-    P2D_ISSUE_J(k0 + i, i);
+    for (int d = 0; d + 1 < NP; ++d) P2D_ISSUE_J(k0 + d, d);
   }
+  // ring slots as running counters (no divisions in the loop)
+  int sk = 2;                  // S slot of plane k (k+1, k+2 follow cyclically)
+  int sis = (DS + 4) % NSL;    // S slot of the next issued plane k+DS+2
+  int jr = 0;                  // J slot of plane k
+  int jis = NP > 0 ? NP - 1 : 0;  // J slot of the next issued plane k+NP-1
+  int lsl = 0;                 // L ring slot of plane k
 
   for (int k = k0; k < k1; ++k) {
     const int i = k - k0;
-    wait_group<NB, STW, D>(i);
+    // NLS_P2D_EARLY: issue first (the slots are free: S plane k-2 since the last
+    // barrier, the wave's own J plane k-1 since its last step), then wait
+    if constexpr (NLS_P2D_EARLY) {
+      P2D_ISSUE_S(k + DS + 2, sis);
+      if constexpr (J > 0) P2D_ISSUE_J(k + NP - 1, jis);
+    }
+    wait_step<J, STW>(i);
     raw_barrier();
-    P2D_ISSUE_S(k + D + 2);
-    P2D_ISSUE_J(k + D, i + D);
-    // L S_J of plane k+1, rows -1, 0, +1
-    cplx ln[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) P2D_LAP(ln[r], k + 1, w + 1 + r);
+    if constexpr (!NLS_P2D_EARLY) {
+      P2D_ISSUE_S(k + DS + 2, sis);
+      if constexpr (J > 0) P2D_ISSUE_J(k + NP - 1, jis);
+    }
+    const int s1 = sk + 1 == NSL ? 0 : sk + 1, s2 = s1 + 1 == NSL ? 0 : s1 + 1;
+    // L S_J of plane k+1: own row (register) + halo values, shared rows into L slot lsl^1
+    cplx ln, lne;
+    P2D_LROWS(k + 1, sk, s1, s2, lsl ^ 1, ln, lne);
     // the J stored vectors of this cell and S_J itself
-    const cplx *jr = Jr + (((i % NJ) * P2D_TR + w) * JS) * 64;
     cplx sv[J + 1];
+    if constexpr (J > 0) {
+      const cplx *jv = reinterpret_cast<const cplx *>(smem + p2d_off_j(J) + ((jr * J) * P2D_TR + w) * 1024);
 #pragma unroll
-    for (int l = 0; l < J; ++l) sv[l] = jr[l * 64 + lane];
-    sv[J] = Sr[(P2D_SSLOT(k) * P2D_SR + w + 2) * 64 + lane];
-    const cplx l1 = lq1[1];
-    cplx X = cmul(bX1, l1);
+      for (int l = 0; l < J; ++l) sv[l] = jv[l * P2D_TR * 64 + lane];
+    }
+    sv[J] = Sr[(sk * P2D_SR + w + 2) * RW + lane];
+    const cplx l1 = lq1;
+    // X (and Z) as two partial sums: shorter dependent FMA chains
+    cplx Xa = cmul(bX1, l1), Xb = {0.0, 0.0};
 #pragma unroll
-    for (int l = 0; l <= J; ++l) X += cmul(cX[l], sv[l]);
+    for (int l = 0; l <= J; ++l) cmac((l & 1) ? Xb : Xa, cX[l], sv[l]);
+    const cplx X = Xa + Xb;
     cplx Z = {0.0, 0.0};
     if constexpr (HZ) {
-      const cplx xm = shfl_up1(l1), xp = shfl_dn1(l1);  // zero outside [0, nx): L S_J = 0 there
-      const cplx l2 = P2D_DIAG(y, k) * l1 + s * (((lq0 + ln[1]) + (xm + xp)) + (lq1[0] + lq1[2]));
-      Z = cmul(bZ2, l2) + cmul(bZ1, l1);
+      // x neighbours: lanes i-1 / i+1 by DPP, the tile-edge ones from the halo values
+      // (x0-1 on lane 0 of le1, x0+64 on its lane 1)
+      cplx xm = lane_prev(l1), xp = lane_next(l1);
+      const cplx er = {__hiloint2double(__builtin_amdgcn_readlane(__double2hiint(le1.re), 1),
+                                        __builtin_amdgcn_readlane(__double2loint(le1.re), 1)),
+                       __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(le1.im), 1),
+                                        __builtin_amdgcn_readlane(__double2loint(le1.im), 1))};
+      if (lane == 0) xm = le1;
+      if (lane == 63) xp = er;
+      const cplx ym = Lr[(lsl * P2D_LR + w) * 64 + lane], yp = Lr[(lsl * P2D_LR + w + 2) * 64 + lane];
+      const cplx l2 = P2D_DIAG(x, y, k) * l1 + s * (((lq0 + ln) + (xm + xp)) + (ym + yp));
+      cplx Za = cmul(bZ2, l2) + cmul(bZ1, l1), Zb = {0.0, 0.0};
 #pragma unroll
-      for (int l = 0; l <= J; ++l) Z += cmul(cZ[l], sv[l]);
+      for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, cZ[l], sv[l]);
+      Z = Za + Zb;
     }
-    // stores from every lane: non-output lanes repeat an output lane's store
-    const int flat = k * P + y * nx + (x0 - 2 + src_lane);
-    {
-      const cplx Xs = {__shfl(X.re, src_lane, 64), __shfl(X.im, src_lane, 64)};
-      st_nt(Xo + flat, Xs);
+    // stores from every lane (a ragged last tile repeats its last valid lane's store)
+    const int flat = k * P + y * nx + x0 + src_lane;
+    if (full) {
+      st_nt(Xo + flat, X);
+      if constexpr (HZ) st_nt(Zo + flat, Z);
+    } else {
+      st_nt(Xo + flat, cplx{__shfl(X.re, src_lane, 64), __shfl(X.im, src_lane, 64)});
+      if constexpr (HZ) st_nt(Zo + flat, cplx{__shfl(Z.re, src_lane, 64), __shfl(Z.im, src_lane, 64)});
     }
-    if constexpr (HZ) {
-      const cplx Zs = {__shfl(Z.re, src_lane, 64), __shfl(Z.im, src_lane, 64)};
-      st_nt(Zo + flat, Zs);
-    }
-    if (out) {
+    if (xin) {
 #pragma unroll
-      for (int l = 0; l <= J; ++l) acc[l] += cj_mul(sv[l], X);
+      for (int l = 0; l <= J; ++l) cjmac(acc[l], sv[l], X);
       if constexpr (HZ) {
 #pragma unroll
-        for (int l = 0; l <= J; ++l) acc[J + 1 + l] += cj_mul(sv[l], Z);
-        acc[2 * J + 2].re += abs2(X);
-        acc[2 * J + 3] += cj_mul(X, Z);
-        acc[2 * J + 4].re += abs2(Z);
+        for (int l = 0; l <= J; ++l) cjmac(acc[J + 1 + l], sv[l], Z);
+        acc[2 * J + 2].re = fma(X.re, X.re, fma(X.im, X.im, acc[2 * J + 2].re));
+        cjmac(acc[2 * J + 3], X, Z);
+        acc[2 * J + 4].re = fma(Z.re, Z.re, fma(Z.im, Z.im, acc[2 * J + 4].re));
       } else {
-        acc[J + 1].re += abs2(X);
+        acc[J + 1].re = fma(X.re, X.re, fma(X.im, X.im, acc[J + 1].re));
       }
     }
-    lq0 = lq1[1];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) lq1[r] = ln[r];
+    lq0 = lq1;
+    lq1 = ln;
+    le1 = lne;
+    sk = s1;
+    sis = sis + 1 == NSL ? 0 : sis + 1;
+    if constexpr (J > 0) {
+      jr = jr + 1 == NPD ? 0 : jr + 1;
+      jis = jis + 1 == NPD ? 0 : jis + 1;
+    }
+    lsl ^= 1;
   }
 #undef P2D_PLANE
 #undef P2D_ROW
 #undef P2D_DIAG
-#undef P2D_SSLOT
 #undef P2D_ISSUE_S
 #undef P2D_ISSUE_J
 #undef P2D_LAP
+#undef P2D_LROWS
   wait_vm<0>();  // the look-ahead DMAs land before the LDS is reused
   raw_barrier();
   cplx *red = reinterpret_cast<cplx *>(smem);  // [4][NC]
