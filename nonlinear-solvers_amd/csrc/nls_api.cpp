@@ -761,18 +761,27 @@ void alloc_all(nls_handle *h) {
   const bool c = h->cplx_;
   const int dim = h->cfg.dim;
   const bool ani = h->ani;
-  // two-vectors-per-pass Lanczos (NLS_PASS2=1): stores S_0..S_{m-2}, ends in the fused tail
+  // two-vectors-per-pass Lanczos: stores S_0..S_{m-2}, ends in the fused tail.
+  // Default on for the 3D isotropic NLSE on one rank (k_p2d: 4-row tiles, m <= 18);
+  // NLS_PASS2=0/1 forces it off / on where a pass form exists.
   h->pass2 = false;
   if (const char *e = std::getenv("NLS_P2_IMPL")) h->p2impl = std::atoi(e) == 1 ? 1 : 2;
-  if (const char *e = std::getenv("NLS_PASS2"); e && std::atoi(e) != 0) {
+  {
+    const char *e = std::getenv("NLS_PASS2");
+    const bool want = e ? std::atoi(e) != 0 : true;
     const bool base = c && !ani && dim == 3 && !h->collective && h->nbasis == 1 && h->m >= 3 &&
                       g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
     // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS; k_pass2r: 64-aligned x
     const bool dma = g.nyp % P2D_ROWS == 0 && g.nyp >= 4 && h->m - 4 <= P2D_MAXJ;
-    if (h->p2impl == 2 && !dma) h->p2impl = 1;
-    h->pass2 = base && (h->p2impl == 2 || (g.nx % 64 == 0 && g.nyp % 2 == 0));
+    if (h->p2impl == 2 && !dma) h->p2impl = e ? 1 : 0;  // the register march only on request
+    h->pass2 = want && base && (h->p2impl == 2 || (h->p2impl == 1 && g.nx % 64 == 0 && g.nyp % 2 == 0));
   }
   if (h->pass2) {
+    // z depth of a k_p2d tile: deep (the prologue is not overlapped), but at least
+    // ~2048 tiles so that every CU gets several (256 at 512^3, 32 at 256^3)
+    const int64_t cols = ((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * std::max<int64_t>(1, g.nyp / P2D_ROWS);
+    const int64_t nzc = std::max<int64_t>(1, (2048 + cols - 1) / cols);
+    h->p2kz = (int)std::max<int64_t>(16, std::min<int64_t>(256, (g.npl + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
     h->p2grid = 0;
     for (int J = 0; J + 1 < h->m - 1; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));

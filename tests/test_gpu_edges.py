@@ -25,13 +25,17 @@ pytestmark = pytest.mark.gpu
 nls_amd = pytest.importorskip("nls_amd")
 
 
-@pytest.fixture(autouse=True, params=["default", "folded"])
+@pytest.fixture(autouse=True, params=["default", "folded", "onevec"])
 def _alpha_mode(request, monkeypatch):
-    """Every edge case twice: the default sequence, and with the folded alpha forced
-    on (NLS_FUSED_ALPHA=1), whose near-breakdown fallback (k_reduce_qa) these cases
-    reach; the variable is read when a handle is created."""
+    """Every edge case three times: the default sequence (the two-vector passes for
+    the 3D isotropic NLSE), the one-vector passes (NLS_PASS2=0), and those with the
+    folded alpha forced on (NLS_FUSED_ALPHA=1), whose near-breakdown fallback
+    (k_reduce_qa) these cases reach; the variables are read when a handle is created."""
     if request.param == "folded":
         monkeypatch.setenv("NLS_FUSED_ALPHA", "1")
+        monkeypatch.setenv("NLS_PASS2", "0")
+    elif request.param == "onevec":
+        monkeypatch.setenv("NLS_PASS2", "0")
     yield
 
 TOL = 1e-10

@@ -17,6 +17,13 @@ import oracle_py as O
 from conftest import rel_l2
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _one_vector_path(monkeypatch):
+    """These tests compare variants of the one-vector Lanczos passes (fused tail on /
+    off, folded alpha on / off); the 3D NLSE runs the two-vector passes by default."""
+    monkeypatch.setenv("NLS_PASS2", "0")
 nls_amd = pytest.importorskip("nls_amd")
 
 

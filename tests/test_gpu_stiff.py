@@ -41,9 +41,10 @@ nls_amd = pytest.importorskip("nls_amd")
 TOL = 1e-10
 
 LARGE = {"NLS_FUSED_ALPHA": "1", "NLS_GRID_MULT": "16", "NLS_KZ": "1", "NLS_KZ_ALPHA": "4",
-         "NLS_FUSED_TAIL": "1"}
-PLAIN = {"NLS_FUSED_ALPHA": "0", "NLS_FUSED_TAIL": "1"}
-# two new vectors per basis pass (LDS-DMA k_p2d), several z chunks per tile column
+         "NLS_FUSED_TAIL": "1", "NLS_PASS2": "0"}
+PLAIN = {"NLS_FUSED_ALPHA": "0", "NLS_FUSED_TAIL": "1", "NLS_PASS2": "0"}
+# two new vectors per basis pass (LDS-DMA k_p2d; the library default for the 3D
+# NLSE on one rank), several z chunks per tile column
 PASS2 = {"NLS_PASS2": "1", "NLS_P2_KZ": "8", "NLS_P2_IMPL": "2"}
 
 
