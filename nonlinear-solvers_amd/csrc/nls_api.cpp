@@ -82,7 +82,7 @@ struct nls_handle {
   bool cplx_ = true;
   size_t esize = 16;
   Geo geo{};
-  int64_t vs = 0;  // elements per stored vector (incl. 2 ghost planes)
+  int64_t vs = 0;  // elements per stored vector (incl. 2 x GHOST ghost planes)
   int m = 10;
   int nbasis = 1;
   Basis B[2];
@@ -203,8 +203,12 @@ void fail(nls_handle *h, int code, const std::string &msg) {
   throw Fail{code};
 }
 
+// Basis vectors carry GHOST ghost planes below and above the slab: one for the
+// radius-1 stencil of the one-vector passes, two for the radius-2 march of the
+// two-vector passes (k_p2d) on multi-rank handles.
+constexpr int GHOST = 2;  // == P2D_GHOST (nls_pass2d.hpp)
 char *vec_ptr(nls_handle *h, int b, int k) {  // local plane 0 of vector k of basis b
-  return static_cast<char *>(h->B[b].W) + ((int64_t)k * h->vs + h->geo.P) * (int64_t)h->esize;
+  return static_cast<char *>(h->B[b].W) + ((int64_t)k * h->vs + GHOST * h->geo.P) * (int64_t)h->esize;
 }
 
 hipEvent_t get_event(nls_handle *h) {
@@ -302,16 +306,17 @@ void halo_local(nls_handle *h, hipStream_t st, char *first, char *last, char *gb
   }
 }
 
-// Exchange the boundary planes of a slab-stored array (local plane 0 at v,
-// ghost planes at -P and nzl*P) into the neighbours' ghost planes (z-slab
-// decomposition; one plane covers the 3D y-wrap too).
-void halo_planes(nls_handle *h, char *v, int64_t es, hipStream_t st = nullptr) {
+// Exchange the np boundary planes of a slab-stored array (local plane 0 at v,
+// ghost planes at -np*P .. -P and nzl*P ..) into the neighbours' ghost planes
+// (z-slab decomposition; one plane covers the 3D y-wrap of a radius-1 stencil,
+// the two-vector passes' radius-2 march needs two).
+void halo_planes(nls_handle *h, char *v, int64_t es, hipStream_t st = nullptr, int np = 1) {
   if (!h->collective) return;
   if (!st) st = h->stream;
   const int64_t P = h->geo.P;
-  const size_t cnt = (size_t)P * (size_t)(es / 8);
-  char *first = v, *last = v + (h->geo.nzl - 1) * P * es;
-  char *gbelow = v - P * es, *gabove = v + h->geo.nzl * P * es;
+  const size_t cnt = (size_t)P * (size_t)(es / 8) * (size_t)np;
+  char *first = v, *last = v + (h->geo.nzl - np) * P * es;
+  char *gbelow = v - np * P * es, *gabove = v + h->geo.nzl * P * es;
   TimingRec rec{4, -1, nullptr, nullptr};
   if (h->timing) {
     rec.a = get_event(h);
@@ -319,7 +324,7 @@ void halo_planes(nls_handle *h, char *v, int64_t es, hipStream_t st = nullptr) {
     hip_check(h, hipEventRecord(rec.a, st), "hipEventRecord");
   }
   if (h->group) {
-    halo_local(h, st, first, last, gbelow, gabove, (size_t)P * es);
+    halo_local(h, st, first, last, gbelow, gabove, (size_t)P * es * np);
     if (h->timing) {
       hip_check(h, hipEventRecord(rec.b, st), "hipEventRecord");
       h->recs.push_back(rec);
@@ -342,8 +347,11 @@ void halo_planes(nls_handle *h, char *v, int64_t es, hipStream_t st = nullptr) {
   }
 }
 
-// vector k of basis b
-void halo(nls_handle *h, int b, int k) { halo_planes(h, vec_ptr(h, b, k), (int64_t)h->esize); }
+// vector k of basis b (two planes on two-vector handles: every halo'd basis vector
+// of theirs is, or may become, the radius-2 stencil vector of a pass)
+void halo(nls_handle *h, int b, int k) {
+  halo_planes(h, vec_ptr(h, b, k), (int64_t)h->esize, nullptr, h->pass2 ? 2 : 1);
+}
 
 // Overlapped form: called once the boundary planes of vector k are enqueued on
 // the compute stream; the exchange runs on cstream while the interior planes
@@ -361,8 +369,8 @@ void halo_wait(nls_handle *h) {
   h->halo_pending = false;
 }
 
-void allreduce_sums(nls_handle *h, int b, int ncplx) {
-  void *p = &h->B[b].st->sums[0];
+void allreduce_sums(nls_handle *h, int b, int ncplx, void *where = nullptr) {
+  void *p = where ? where : static_cast<void *>(&h->B[b].st->sums[0]);
   if (h->group) {
     // publish my partial sums, rendezvous, then every rank sums all ranks'
     // publications in rank order (identical result on every rank)
@@ -657,9 +665,13 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
     int nbA = 0, ncA = 0, ncU = hz ? 2 * J + 5 : J + 2;
     void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
     launch(h, 2, J, kernel_colsum(), ncU, cargs);
+    if (h->collective) allreduce_sums(h, 0, ncU, sums);
     int mm = nstore, mode = 1, jj = J;
     void *a2[] = {&ps, &st, &jj, &mm, &mode};
     launch(h, 2, J, kernel_p2coef(), 1, a2);
+    // multi-rank: the next stencil vector's two boundary planes (Z, or the X of a
+    // last X-only pass, which the tail's alpha pass and k_tail march over)
+    if (h->collective) halo(h, 0, hz ? J + 2 : J + 1);
     J += hz ? 2 : 1;
   }
   // the tail's alpha pass over S_{m-2}: a = S^H L S, ||S||^2, ||L S||^2
@@ -669,6 +681,7 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
     int nbA = h->grid_alpha2, ncA = 3, nbU = 0;
     void *cargs[] = {(void *)&h->partA, &nbA, &ncA, (void *)&pU, &nbU, &sums};
     launch(h, 2, m - 2, kernel_colsum(), ncA, cargs);
+    if (h->collective) allreduce_sums(h, 0, ncA, sums);
     int mm = m;
     void *a2[] = {&ps, &st, &sums, &mm};
     launch(h, 2, m - 2, kernel_p2tail(), 1, a2);
@@ -740,7 +753,7 @@ void setup_geometry(nls_handle *h) {
   // 4 KiB pad, within 1 % elsewhere; no pad at all is ~15 % slower (tools/bw_probe.hip)
   int64_t pad = 4096;
   if (const char *e = std::getenv("NLS_VEC_PAD")) pad = std::max<int64_t>(0, std::atoll(e));
-  h->vs = (g.nzl + 2) * g.P + pad;
+  h->vs = (g.nzl + 2 * GHOST) * g.P + pad;
 }
 
 // scalar type of a tail kernel on this handle: the NLSE and sEWI epilogues are
@@ -769,12 +782,14 @@ void alloc_all(nls_handle *h) {
   {
     const char *e = std::getenv("NLS_PASS2");
     const bool want = e ? std::atoi(e) != 0 : true;
-    const bool base = c && !ani && dim == 3 && !h->collective && h->nbasis == 1 && h->m >= 3 &&
-                      g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
+    // multi-rank: slabs of >= 4 planes (two-plane halos)
+    const bool base = c && !ani && dim == 3 && (!h->collective || g.nzl >= 4) && h->nbasis == 1 &&
+                      h->m >= 3 && g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
     // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS; k_pass2r: 64-aligned x
     const bool dma = g.nyp % P2D_ROWS == 0 && g.nyp >= 4 && h->m - 4 <= P2D_MAXJ;
     if (h->p2impl == 2 && !dma) h->p2impl = e ? 1 : 0;  // the register march only on request
-    h->pass2 = want && base && (h->p2impl == 2 || (h->p2impl == 1 && g.nx % 64 == 0 && g.nyp % 2 == 0));
+    h->pass2 = want && base &&
+               (h->p2impl == 2 || (h->p2impl == 1 && !h->collective && g.nx % 64 == 0 && g.nyp % 2 == 0));
   }
   if (h->pass2) {
     // z depth of a k_p2d tile: deep (the prologue is not overlapped), but at least
@@ -959,7 +974,7 @@ bool slab_index_limit_exceeded(const nls_config &c) {
   const uint64_t P = c.dim == 3 ? (uint64_t)c.nx * c.ny : (uint64_t)c.nx;
   uint32_t z0 = 0, nzl = 0;
   if (nls_slab_planes((uint32_t)npl, c.nranks, 0, &z0, &nzl) != NLS_OK) return true;
-  return ((uint64_t)nzl + 2) * P + 4096 >= (uint64_t(1) << 31);
+  return ((uint64_t)nzl + 2 * GHOST) * P + 4096 >= (uint64_t(1) << 31);
 }
 
 }  // namespace

@@ -47,6 +47,7 @@ constexpr int P2D_SR = P2D_TR + 4;    // S_J rows staged per plane (y0-2 .. y0+5
 constexpr int P2D_SRB = 1024 + 64;    // bytes per staged S_J row: x0..x0+63, then x0-2, x0-1, x0+64, x0+65
 constexpr int P2D_LR = P2D_TR + 2;    // L S_J rows shared per plane (y0-1 .. y0+4)
 constexpr int P2D_JMAX = 14;          // largest J whose rings fit 160 KiB of LDS
+constexpr int P2D_GHOST = 2;          // ghost planes per side of a stored vector (radius-2 march)
 constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
 #ifndef NLS_P2D_OCC2_MAXJ
 #define NLS_P2D_OCC2_MAXJ 2   // two workgroups per CU up to this J (measured: J = 2 yes, J = 4 no)
@@ -187,9 +188,12 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   // w through readfirstlane: wave-uniform for the compiler too, so row and plane
   // logic stays scalar
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
+  // planes: local k (slab of nzl planes, ghost planes -2, -1, nzl, nzl+1 filled by the
+  // halo exchange on multi-rank handles), global z0 + k for the reference's couplings
   const int nx = (int)g.nx, ny = (int)g.nyp, P = (int)g.P, nz = (int)g.npl;
+  const int nzl = (int)g.nzl, z0 = (int)g.z0;
   const int ntx = (nx + P2D_XO - 1) / P2D_XO, nty = ny / P2D_TR;
-  const int nzc = (nz + g.kz - 1) / g.kz;
+  const int nzc = (nzl + g.kz - 1) / g.kz;
   const int ntiles = ntx * nty * nzc;
   // XCD-banded order: the 8 XCDs take contiguous tile ranges, so the y-adjacent
   // tiles sharing S_J halo rows run on one XCD (its L2) at the same time
@@ -197,7 +201,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   const int tile = b < 8 * T8 ? (b % 8) * T8 + b / 8 : b;
   const int yt = tile % nty, rest = tile / nty, xt = rest % ntx, zc = rest / ntx;
   const int x0 = xt * P2D_XO, y0 = yt * P2D_TR;
-  const int k0 = zc * g.kz, k1 = min(k0 + g.kz, nz);
+  const int k0 = zc * g.kz, k1 = min(k0 + g.kz, nzl);
   const int x = x0 + lane;
   const bool xin = x < nx;
   const bool full = x0 + P2D_XO <= nx;                    // uniform
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   const int eci = lane == 1 ? 66 : 65, emi = lane == 1 ? 63 : 64, epi = lane == 1 ? 67 : 0;
   // (macros, not lambdas capturing by reference: hipcc kept such captures on the
   // stack, and every scratch access is a VMEM op that breaks the vmcnt counting)
-#define P2D_PLANE(p, yy) ((yy) < 0 ? (p) - 1 : ((yy) >= ny ? (p) + 1 : (p)))
+#define P2D_PLANE(p, yy) (z0 + ((yy) < 0 ? (p) - 1 : ((yy) >= ny ? (p) + 1 : (p))))  // global
 #define P2D_ROW(yy) ((yy) < 0 ? (yy) + ny : ((yy) >= ny ? (yy) - ny : (yy)))
 #define P2D_DIAG(xx, j, kk) \
   ((((xx) == 0) | ((xx) == nx - 1) | ((j) == 0) | ((j) == ny - 1) | ((kk) == 0) | ((kk) == nz - 1)) ? sdb : sdi)
@@ -241,8 +245,11 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
     const int p_ = (p);                                                                 \
     char *dst_ = smem + ((sl) * P2D_SR + 2 * w) * P2D_SRB;                              \
     _Pragma("unroll") for (int r_ = 0; r_ < 2; ++r_) {                                  \
-      const int yy_ = y0 - 2 + 2 * w + r_, kk_ = P2D_PLANE(p_, yy_);                    \
-      const bool ok_ = kk_ >= 0 && kk_ < nz && p_ <= k1 + 1;                            \
+      const int yy_ = y0 - 2 + 2 * w + r_, kk_ = P2D_PLANE(p_, yy_), lp_ = kk_ - z0;    \
+      /* global plane in the grid, local plane inside the allocation (ghosts), and   \
+         not past the tile's last needed plane */                                     \
+      const bool ok_ = kk_ >= 0 && kk_ < nz && lp_ >= -P2D_GHOST && lp_ < nzl + P2D_GHOST && \
+                       p_ <= k1 + 1;                                                    \
       const char *b_ = ok_ ? SJb + (p_ * P16 + (int64_t)yy_ * nx * 16)                  \
                            : reinterpret_cast<const char *>(zbuf);                      \
       dma16(b_, xoff, dst_ + r_ * P2D_SRB, 0);                                          \
@@ -372,7 +379,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
       if (lane == 0) xm = le1;
       if (lane == 63) xp = er;
       const cplx ym = Lr[(lsl * P2D_LR + w) * 64 + lane], yp = Lr[(lsl * P2D_LR + w + 2) * 64 + lane];
-      const cplx l2 = P2D_DIAG(x, y, k) * l1 + s * (((lq0 + ln) + (xm + xp)) + (ym + yp));
+      const cplx l2 = P2D_DIAG(x, y, z0 + k) * l1 + s * (((lq0 + ln) + (xm + xp)) + (ym + yp));
       cplx Za = cmul(bZ2, l2) + cmul(bZ1, l1), Zb = {0.0, 0.0};
 #pragma unroll
       for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, cZ[l], sv[l]);

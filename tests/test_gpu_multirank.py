@@ -136,3 +136,59 @@ def test_rccl_collective_path_single_rank(monkeypatch, eq):
             s.step(0.01, 4)
             got = s.get_field()
     assert rel_l2(got, ref) <= 1e-10
+
+
+def _ran_pass2(s, m):
+    cnt = s.timing()["update_count"]
+    return cnt[0] > 0 and all(cnt[j] == 0 for j in range(1, m - 1, 2))
+
+
+@pytest.mark.parametrize("nranks,m", [(4, 16), (3, 15), (2, 10)])
+def test_pass2_slabs_match_oracle(nranks, m):
+    """The two-vector passes (k_p2d, the default for the 3D NLSE) on z slabs: two
+    ghost planes per stored vector, two-plane halos of every stencil vector (incl.
+    the 3D y-wrap across slab boundaries at the radius-2 march), all-reduced pass
+    sums; uneven slabs (40 planes over 3 ranks) and an odd m (X-only last pass).
+    Spacing of the 512^3 bench (dx = 20/511): the stiff regime."""
+    nx, ny, nz = 64, 24, 40
+    dx = 20.0 / 511
+    P = nx * ny
+    u0 = field(nx * ny * nz, seed=nranks)
+    dt, steps = 1e-3, 5
+    ref = O.nlse_steps(O.grid(3, nx, ny, nz, dx, dx), u0, dt, steps, m)
+
+    def mk(r, grp):
+        return nls_amd.Solver(3, nx, ny, nz, dx, dx, m=m, device=0, nranks=nranks, rank=r, group=grp)
+
+    def body(s):
+        s.set_field(u0[s.z0 * P:(s.z0 + s.nzl) * P])
+        s.set_timing(True)
+        s.step(dt, steps)
+        return s.z0, s.get_field(), _ran_pass2(s, m)
+
+    res = sorted(run_ranks(nranks, mk, body), key=lambda t: t[0])
+    assert all(r[2] for r in res)
+    got = np.concatenate([r[1] for r in res])
+    assert rel_l2(got, ref) <= 1e-10
+    with nls_amd.Solver(3, nx, ny, nz, dx, dx, m=m, device=0) as s:
+        s.set_field(u0)
+        s.step(dt, steps)
+        one = s.get_field()
+    assert rel_l2(got, one) <= 1e-12
+
+
+def test_pass2_rccl_collective_path_single_rank(monkeypatch):
+    """NLS_FORCE_RCCL=1: the two-vector passes through a real RCCL communicator
+    (ncclAllReduce of the pass sums, grouped two-plane send/recv)."""
+    monkeypatch.setenv("NLS_FORCE_RCCL", "1")
+    n, m = 16, 10
+    dx = 20.0 / (n - 1)
+    u0 = field(n ** 3, 8)
+    ref = O.nlse_steps(O.grid(3, n, n, n, dx, dx), u0, 1e-3, 4, m)
+    with nls_amd.Solver(3, n, n, n, dx, dx, m=m, device=0) as s:
+        s.set_field(u0)
+        s.set_timing(True)
+        s.step(1e-3, 4)
+        got = s.get_field()
+        assert _ran_pass2(s, m)
+    assert rel_l2(got, ref) <= 1e-10
