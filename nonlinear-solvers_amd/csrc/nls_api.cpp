@@ -145,7 +145,7 @@ struct nls_handle {
   uint64_t evnext = 0, ar_count = 0;
   // halo/compute overlap (collective handles): exchange on cstream
   hipStream_t cstream = nullptr;
-  hipEvent_t ev_bnd = nullptr, ev_halo = nullptr;
+  hipEvent_t ev_bnd = nullptr, ev_halo = nullptr, ev_bdone = nullptr;
   bool halo_pending = false;
   bool bnd_side = true;  // boundary-plane launches on cstream (NLS_BND_SIDE=0: in order on the compute stream)
   // asynchronous snapshots: staging copy on the compute stream, D2H on xstream
@@ -359,7 +359,7 @@ void halo(nls_handle *h, int b, int k) {
 void halo_begin(nls_handle *h, int b, int k) {
   hip_check(h, hipEventRecord(h->ev_bnd, h->stream), "hipEventRecord");
   hip_check(h, hipStreamWaitEvent(h->cstream, h->ev_bnd, 0), "hipStreamWaitEvent");
-  halo_planes(h, vec_ptr(h, b, k), (int64_t)h->esize, h->cstream);
+  halo_planes(h, vec_ptr(h, b, k), (int64_t)h->esize, h->cstream, h->pass2 ? 2 : 1);
   hip_check(h, hipEventRecord(h->ev_halo, h->cstream), "hipEventRecord");
   h->halo_pending = true;
 }
@@ -619,16 +619,26 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   reduce_final(h, b, nf, f0, f1, tr, ti);
 }
 
-// grid of one two-vector pass: k_p2d one workgroup per 60 x 4-row tile of
-// p2kz planes; k_pass2r one wave per 60 x rb output column, 4 waves per workgroup
-int p2_grid(const nls_handle *h, int J) {
+// tiles of one two-vector launch over local planes [qa, qb) with tile depth kz:
+// k_p2d one workgroup per 64 x 4-row tile column chunk; k_pass2r one wave per
+// 60 x rb output column chunk, 4 waves per workgroup
+int p2_tiles(const nls_handle *h, int J, int64_t qa, int64_t qb, int64_t kz) {
   const Geo &g = h->geo;
-  const int64_t nzc = (g.npl + h->p2kz - 1) / h->p2kz;
+  const int64_t nzc = (qb - qa + kz - 1) / kz;
   if (h->p2impl == 2)
     return (int)(((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * (g.nyp / P2D_ROWS) * nzc);
   const int rb = P2R_ROWS(J);
   const int64_t waves = ((g.nx + P2R_WAVE_XO - 1) / P2R_WAVE_XO) * (g.nyp / rb) * nzc;
   return (int)((waves + NTHREADS / 64 - 1) / (NTHREADS / 64));
+}
+// Multi-rank handles (slabs of >= 8 planes) launch each pass as the two boundary
+// plane pairs (tile depth 2, on the halo stream, followed there by the two-plane
+// halo exchange of the new stencil vector) and the interior (compute stream).
+bool p2_split(const nls_handle *h) { return h->collective && h->geo.nzl >= 8 && h->p2impl == 2; }
+int p2_grid(const nls_handle *h, int J) {
+  const int64_t nzl = h->geo.nzl;
+  if (!p2_split(h)) return p2_tiles(h, J, 0, nzl, h->p2kz);
+  return 2 * p2_tiles(h, J, 0, 2, 2) + p2_tiles(h, J, 2, nzl - 2, h->p2kz);
 }
 
 // Two new vectors per pass (nls_pass2.hpp): the alpha pass + reduction of W_0
@@ -656,11 +666,44 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
   g.kz = h->p2kz;
   cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(h->p2) + p2state_sums_offset());
   int J = 0;
+  const bool split = p2_split(h);
   while (J + 1 < nstore) {
     const bool hz = J + 2 < nstore;
+    const int out = hz ? J + 2 : J + 1;  // the next stencil vector (Z, or a last X-only pass's X)
     int nb = p2_grid(h, J);
-    void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb, &h->zbuf};
-    launch(h, 1, J, kernel_pass2(J, hz, h->p2impl), nb, args);
+    const void *fn = kernel_pass2(J, hz, h->p2impl);
+    halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
+    if (!split) {
+      int poff = 0;
+      void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb, &h->zbuf, &poff};
+      launch(h, 1, J, fn, nb, args);
+      if (h->collective) halo_begin(h, 0, out);
+    } else {
+      const int64_t nzl = h->geo.nzl;
+      const int tb = p2_tiles(h, J, 0, 2, 2);
+      hip_check(h, hipEventRecord(h->ev_bnd, h->stream), "hipEventRecord");
+      hip_check(h, hipStreamWaitEvent(h->cstream, h->ev_bnd, 0), "hipStreamWaitEvent");
+      Geo gb = g;
+      gb.kz = 2;
+      for (int side = 0; side < 2; ++side) {
+        gb.qa = side == 0 ? 0 : (int32_t)(nzl - 2);
+        gb.qb = gb.qa + 2;
+        int poff = side * tb;
+        void *args[] = {&W, &vs, &gb, &ps, &h->partP2, &nb, &h->zbuf, &poff};
+        launch(h, 1, J, fn, tb, args, h->cstream);
+      }
+      hip_check(h, hipEventRecord(h->ev_bdone, h->cstream), "hipEventRecord");
+      halo_planes(h, vec_ptr(h, 0, out), (int64_t)h->esize, h->cstream, 2);
+      hip_check(h, hipEventRecord(h->ev_halo, h->cstream), "hipEventRecord");
+      h->halo_pending = true;
+      Geo gi = g;
+      gi.qa = 2;
+      gi.qb = (int32_t)(nzl - 2);
+      int poff = 2 * tb;
+      void *args[] = {&W, &vs, &gi, &ps, &h->partP2, &nb, &h->zbuf, &poff};
+      launch(h, 1, J, fn, nb - 2 * tb, args);
+      hip_check(h, hipStreamWaitEvent(h->stream, h->ev_bdone, 0), "hipStreamWaitEvent");
+    }
     const cplx *pA = nullptr;
     int nbA = 0, ncA = 0, ncU = hz ? 2 * J + 5 : J + 2;
     void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
@@ -669,11 +712,9 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
     int mm = nstore, mode = 1, jj = J;
     void *a2[] = {&ps, &st, &jj, &mm, &mode};
     launch(h, 2, J, kernel_p2coef(), 1, a2);
-    // multi-rank: the next stencil vector's two boundary planes (Z, or the X of a
-    // last X-only pass, which the tail's alpha pass and k_tail march over)
-    if (h->collective) halo(h, 0, hz ? J + 2 : J + 1);
     J += hz ? 2 : 1;
   }
+  halo_wait(h);
   // the tail's alpha pass over S_{m-2}: a = S^H L S, ||S||^2, ||L S||^2
   alpha_l2_pass(h, 0, m - 2);
   {
@@ -1093,6 +1134,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
       hip_check(h, hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking), "hipStreamCreate");
       hip_check(h, hipEventCreateWithFlags(&h->ev_bnd, hipEventDisableTiming), "hipEventCreate");
       hip_check(h, hipEventCreateWithFlags(&h->ev_halo, hipEventDisableTiming), "hipEventCreate");
+      hip_check(h, hipEventCreateWithFlags(&h->ev_bdone, hipEventDisableTiming), "hipEventCreate");
     }
     alloc_all(h);  // the update launch plan depends on h->collective
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
@@ -1101,7 +1143,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
     g_create_error = h->err;
     free_all(h);
     if (h->comm) ncclCommDestroy(h->comm);
-    for (hipEvent_t e : {h->ev_bnd, h->ev_halo})
+    for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_bdone})
       if (e) (void)hipEventDestroy(e);
     for (auto e : h->evring)
       if (e) (void)hipEventDestroy(e);
@@ -1121,7 +1163,7 @@ int nls_destroy(nls_handle *h) {
   if (h->cstream) (void)hipStreamSynchronize(h->cstream);
   if (h->xstream) (void)hipStreamSynchronize(h->xstream);
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
-  for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_snap, h->ev_snap_done})
+  for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_bdone, h->ev_snap, h->ev_snap_done})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->stepev)
     if (e) (void)hipEventDestroy(e);

@@ -169,11 +169,14 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Output planes [g.qa, g.qb) of the slab (multi-rank handles launch the two
+// boundary plane pairs apart from the interior, so the halo exchange overlaps);
+// partial sums at part[c * nb + poff + blockIdx.x].
 template <int J, bool HZ>
 __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
                                                               const P2State *__restrict__ ps,
                                                               cplx *__restrict__ part, int nb,
-                                                              const cplx *__restrict__ zbuf) {
+                                                              const cplx *__restrict__ zbuf, int poff) {
   static_assert(p2d_rings_ok(J), "rings exceed LDS");
   constexpr int DS = p2d_ds(J), NSL = p2d_nsl(J), NP = p2d_np(J);
   constexpr int STW = HZ ? 2 : 1;            // stores per step
@@ -193,7 +196,8 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   const int nx = (int)g.nx, ny = (int)g.nyp, P = (int)g.P, nz = (int)g.npl;
   const int nzl = (int)g.nzl, z0 = (int)g.z0;
   const int ntx = (nx + P2D_XO - 1) / P2D_XO, nty = ny / P2D_TR;
-  const int nzc = (nzl + g.kz - 1) / g.kz;
+  const int qa = g.qa, qb = g.qb;
+  const int nzc = (qb - qa + g.kz - 1) / g.kz;
   const int ntiles = ntx * nty * nzc;
   // XCD-banded order: the 8 XCDs take contiguous tile ranges, so the y-adjacent
   // tiles sharing S_J halo rows run on one XCD (its L2) at the same time
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   const int tile = b < 8 * T8 ? (b % 8) * T8 + b / 8 : b;
   const int yt = tile % nty, rest = tile / nty, xt = rest % ntx, zc = rest / ntx;
   const int x0 = xt * P2D_XO, y0 = yt * P2D_TR;
-  const int k0 = zc * g.kz, k1 = min(k0 + g.kz, nzl);
+  const int k0 = qa + zc * g.kz, k1 = min(k0 + g.kz, qb);
   const int x = x0 + lane;
   const bool xin = x < nx;
   const bool full = x0 + P2D_XO <= nx;                    // uniform
@@ -438,7 +442,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
     cplx v = red[c];
 #pragma unroll
     for (int q = 1; q < P2D_TR; ++q) v += red[q * NC + c];
-    part[(int64_t)c * nb + blockIdx.x] = v;
+    part[(int64_t)c * nb + poff + blockIdx.x] = v;
   }
 }
 

@@ -51,7 +51,7 @@ __device__ __forceinline__ double face_w(bool e, double ca, double cb) { return 
 
 // fn(p, cur, lap) for every local cell p of the workgroup's tiles, with
 // cur = V[p] and lap = (L V)[p] (laplacians.hpp:10-105, flat-index form).
-// Local indices are 32-bit (the host guarantees (nzl+2)*P < 2^31); the flat
+// Local indices are 32-bit (the host guarantees (nzl+4)*P + pad < 2^31); the flat
 // range tests of the reference (idx-nx >= 0, idx+nx < N) are evaluated on
 // (plane, row) coordinates so they never need 64-bit global indices.
 //

@@ -73,14 +73,18 @@ def run(args, **kw):
 
 
 def test_index_limit_boundary_not_rejected_early():
-    """Just below the limit the config passes validation (it then needs a device:
-    on this CPU-only host creation fails with a HIP error, not NLS_ERR_ARG)."""
+    """Just below the limit ((nzl + 4) * P + pad < 2^31: two ghost planes per side)
+    the config passes validation (it then needs a device: on this CPU-only host
+    creation fails with a HIP error, not NLS_ERR_ARG); one plane more is rejected."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("would allocate ~ 2^31 cells on a GPU")
     with pytest.raises(nls_amd.NlsError) as e:
-        nls_amd.Solver(3, 1024, 1024, 2045, 0.1, m=3)
+        nls_amd.Solver(3, 1024, 1024, 2043, 0.1, m=3)
     assert "32-bit" not in str(e.value)
+    with pytest.raises(nls_amd.NlsError) as e:
+        nls_amd.Solver(3, 1024, 1024, 2044, 0.1, m=3)
+    assert e.value.code == -1 and "32-bit" in str(e.value)
 
 
 @pytest.mark.parametrize("prog", ["nlse_call", "nlse_cq_call", "to_nlse_call", "to_nlse_cq_call"])
