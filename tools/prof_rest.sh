@@ -1,15 +1,8 @@
-# Full measurement pass for profiles/<tag>: bench lines, the bench under rocprofv3
-# --kernel-trace --stats (its own line + the kernel stats of the SAME process, so
-# the roofline frac can be recomputed from the committed summary), PMC passes
-# (one counter group per run).  Usage: bash tools/profile_round.sh r02
 set -e
-TAG=${1:-r02}
+TAG=r02
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/$TAG
-mkdir -p $OUT $OUT/pmc
-timeout -k 10 400 python bench.py > $OUT/bench_nlse3d_512.json 2> $OUT/bench_nlse3d_512.err
-cat $OUT/bench_nlse3d_512.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/trace.log
+mkdir -p $OUT/pmc
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
