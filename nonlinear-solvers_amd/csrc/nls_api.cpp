@@ -116,6 +116,8 @@ struct nls_handle {
   int p2grid = 0, p2kz = 32;
   int p2impl = 2;              // 2: LDS-DMA k_p2d; 1: register-march k_pass2r (NLS_P2_IMPL)
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
+  bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
+  bool p2_warm = false;        // the P2State holds a previous basis' alpha_0
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
@@ -649,17 +651,23 @@ int p2_grid(const nls_handle *h, int J) {
 // (S_0..S_{m-2} and L S_{m-2}: the last Lanczos vector is never stored).
 void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
   const int m = h->m, nstore = m - 1;
-  Geo ga = h->geo;
-  ga.kz = h->kz_alpha;
-  alpha_pass(h, 0, 0, ga);
-  reduce_iter(h, 0, 0);
   KState *st = h->B[0].st;
   void *ps = h->p2;
+  // blind start once a previous basis left its alpha_0 (the shift of the J = 0
+  // pass): no alpha pass over W_0, beta from the pass's own ||S_0||^2
+  const bool blind = h->p2_warm && h->p2_blind && h->p2impl == 2;  // k_p2d<0> reduces ||S_0||^2
+  if (!blind) {
+    Geo ga = h->geo;
+    ga.kz = h->kz_alpha;
+    alpha_pass(h, 0, 0, ga);
+    reduce_iter(h, 0, 0);
+  }
   {
-    int J = 0, mm = nstore, mode = 0;
+    int J = 0, mm = nstore, mode = blind ? 2 : 0;
     void *args[] = {&ps, &st, &J, &mm, &mode};
     launch(h, 2, 0, kernel_p2coef(), 1, args);
   }
+  h->p2_warm = true;
   void *W = vec_ptr(h, 0, 0);
   int64_t vs = h->vs;
   Geo g = h->geo;
@@ -705,7 +713,7 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
       hip_check(h, hipStreamWaitEvent(h->stream, h->ev_bdone, 0), "hipStreamWaitEvent");
     }
     const cplx *pA = nullptr;
-    int nbA = 0, ncA = 0, ncU = hz ? 2 * J + 5 : J + 2;
+    int nbA = 0, ncA = 0, ncU = (hz ? 2 * J + 5 : J + 2) + (J == 0 ? 1 : 0);
     void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
     launch(h, 2, J, kernel_colsum(), ncU, cargs);
     if (h->collective) allreduce_sums(h, 0, ncU, sums);
@@ -839,6 +847,7 @@ void alloc_all(nls_handle *h) {
     const int64_t nzc = std::max<int64_t>(1, (2048 + cols - 1) / cols);
     h->p2kz = (int)std::max<int64_t>(16, std::min<int64_t>(256, (g.npl + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("NLS_P2_BLIND")) h->p2_blind = std::atoi(e) != 0;
     h->p2grid = 0;
     for (int J = 0; J + 1 < h->m - 1; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
     hip_check(h, hipMalloc(&h->p2, p2state_bytes()), "hipMalloc(p2)");
@@ -1211,6 +1220,7 @@ int nls_set_field(nls_handle *h, const double *u, uint64_t n) {
       hip_check(h, hipMemcpyAsync(h->u, u, (size_t)n * h->esize, hipMemcpyHostToDevice, h->stream),
                 "hipMemcpy H2D");
       h->w0_ready = false;
+      h->p2_warm = false;  // a new field: the next basis measures alpha_0 again
     } else {
       copy_in_vector(h, 0, 0, u);
       halo(h, 0, 0);

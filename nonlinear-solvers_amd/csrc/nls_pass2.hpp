@@ -28,6 +28,7 @@ struct P2State {
   cplx sums[2 * P2M + 8];
   cplx tk[P2M];   // fused tail: t_k = W_k^H L S_{m-2} (k_p2tail)
   double beta_t;  // fused tail: beta_{m-1}
+  int32_t blind;  // the J = 0 pass ran on the raw start vector (mode 2), beta from its sums
 };
 
 // Register-march form of the same pass (the LDS-DMA form k_p2d, nls_pass2d.hpp, is the default).  Each
@@ -193,8 +194,12 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2r(cplx *__restrict__ W, int64
 }
 
 // Coefficient kernel (one workgroup).  mode 0: start (after the alpha pass and
-// reduction of W_0: s[0] = beta, H[0][0] = alpha_0); mode 1: after the pass at
-// J (sums = the pass's columns, summed).  Computes the new columns of C, D, H
+// reduction of W_0: s[0] = beta, H[0][0] = alpha_0); mode 2: blind start, no
+// alpha pass: the J = 0 pass runs on the raw start vector (C00 = 1) with the
+// previous step's alpha_0 as its shift and also reduces ||S_0||^2; mode 1 at
+// J = 0 then takes beta from it, rescales the sums to the normalised scheme and
+// the stored S_1, S_2 columns of C (and D) by 1/beta (beta); mode 1: after the
+// pass at J (sums = the pass's columns, summed).  Computes the new columns of C, D, H
 // and, if another pass follows (J' + 1 < m), its coefficients; otherwise T into
 // the KState for k_reduce_final (s[] = 1, so fin is in the W basis; k_p2fin
 // converts it).
@@ -203,9 +208,12 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
   __shared__ cplx p[P2M], q[P2M], lw[P2M], xw[P2M], zw[P2M];
   __shared__ cplx gz[P2M];
   __shared__ double nu[2];
+  __shared__ double s_prev, s_beta;
   const int t = threadIdx.x;
   int Jn;  // J of the next pass
-  if (mode == 0) {
+  if (t == 0) s_prev = ps->H[0][0].re;  // mode 2's shift: the previous step's alpha_0
+  __syncthreads();
+  if (mode == 0 || mode == 2) {
     for (int e = t; e < P2M * P2M; e += NTHREADS) {
       const int i = e / P2M, k = e % P2M;
       ps->C[i][k] = {0.0, 0.0};
@@ -214,16 +222,49 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
     }
     __syncthreads();
     if (t == 0) {
-      const double b = st->s[0];
-      ps->beta = b;
-      ps->C[0][0] = {b > 0.0 ? 1.0 / b : 0.0, 0.0};
-      ps->D[0][0] = {b, 0.0};
-      ps->sigma = st->H[0][0].re;
+      if (mode == 0) {
+        const double b = st->s[0];
+        ps->beta = b;
+        ps->C[0][0] = {b > 0.0 ? 1.0 / b : 0.0, 0.0};
+        ps->D[0][0] = {b, 0.0};
+        ps->sigma = st->H[0][0].re;
+        ps->blind = 0;
+      } else {
+        ps->beta = 1.0;
+        ps->C[0][0] = {1.0, 0.0};
+        ps->D[0][0] = {1.0, 0.0};
+        ps->sigma = s_prev;
+        ps->blind = 1;
+      }
     }
     __syncthreads();
     Jn = 0;
   } else {
     const int hz = J + 2 < m;  // the pass also produced Z
+    if (J == 0 && ps->blind) {
+      // the J = 0 pass ran on the raw S_0 (C00 = 1): its sums are beta (gX, gZ) and
+      // beta^2 (xx, xz, zz) times those of the normalised scheme; ||S_0||^2 follows them
+      cplx *sw = ps->sums;
+      const int ns = hz ? 5 : 2;
+      if (t == 0) {
+        const double b = sqrt(sw[ns].re);
+        const double ib = b > 0.0 ? 1.0 / b : 0.0;
+        s_beta = b;
+        sw[0] = ib * sw[0];
+        if (hz) {
+          sw[1] = ib * sw[1];
+          sw[2] = (ib * ib) * sw[2];
+          sw[3] = (ib * ib) * sw[3];
+          sw[4] = (ib * ib) * sw[4];
+        } else {
+          sw[1] = (ib * ib) * sw[1];
+        }
+        ps->beta = b;
+        ps->C[0][0] = {ib, 0.0};
+        ps->D[0][0] = {b, 0.0};
+      }
+      __syncthreads();
+    }
     const cplx *sm = ps->sums;
     // sums: hz: gX[0..J], gZ[0..J], xx, xz, zz; else gX[0..J], xx
     const int o = 2 * J + 2;
@@ -307,6 +348,19 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       Jn = J + 1;  // W_{m-1} done
     }
     __syncthreads();
+    if (J == 0 && ps->blind) {
+      // the stored S_1 (and S_2) are beta times the normalised scheme's: their C rows
+      // scale by 1/beta, their D columns by beta (C = D^-1 stays consistent)
+      const double b = s_beta, ib = b > 0.0 ? 1.0 / b : 0.0;
+      const int nl = hz ? 2 : 1;
+      for (int e = t; e < nl * P2M; e += NTHREADS) {
+        const int l = 1 + e / P2M, k = e % P2M;
+        ps->C[l][k] = ib * ps->C[l][k];
+        ps->D[k][l] = b * ps->D[k][l];
+      }
+      __syncthreads();
+      if (t == 0) ps->blind = 0;
+    }
   }
   if (Jn + 1 < m) {
     // coefficients of the pass at Jn

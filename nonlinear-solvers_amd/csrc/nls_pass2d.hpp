@@ -50,10 +50,10 @@ constexpr int P2D_JMAX = 14;          // largest J whose rings fit 160 KiB of LD
 constexpr int P2D_GHOST = 2;          // ghost planes per side of a stored vector (radius-2 march)
 constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
 #ifndef NLS_P2D_OCC2_MAXJ
-#define NLS_P2D_OCC2_MAXJ 2   // two workgroups per CU up to this J (measured: J = 2 yes, J = 4 no)
+#define NLS_P2D_OCC2_MAXJ 4   // two workgroups per CU up to this J
 #endif
 #ifndef NLS_P2D_EARLY
-#define NLS_P2D_EARLY 1  // issue a step's DMAs before its wait (needs the extra S slot)
+#define NLS_P2D_EARLY 1  // one workgroup per CU: issue a step's DMAs before its wait (needs an extra S slot)
 #endif
 #ifndef NLS_P2D_NP_MAX
 #define NLS_P2D_NP_MAX 5      // J-ring depth cap in planes
@@ -66,9 +66,12 @@ __host__ __device__ constexpr int p2d_occ(int J) { return J <= NLS_P2D_OCC2_MAXJ
 // plane k-2 (free since the previous step's barrier), into which a step issues
 // before its own wait and barrier
 __host__ __device__ constexpr int p2d_ds(int J) {
-  return p2d_occ(J) == 2 ? (J == 0 ? 3 : 2) : (J == 0 ? 6 : (J <= 6 ? 3 : (J <= 12 || !NLS_P2D_EARLY ? 1 : 0)));
+  return p2d_occ(J) == 2 ? (J == 0 ? 3 : (J <= 2 ? 2 : 1)) : (J == 0 ? 6 : (J <= 6 ? 3 : (J <= 12 || !NLS_P2D_EARLY ? 1 : 0)));
 }
-__host__ __device__ constexpr int p2d_nsl(int J) { return p2d_ds(J) + 3 + NLS_P2D_EARLY; }
+// early issue only at one workgroup per CU (two: the other workgroup covers the wait,
+// and the LDS is short)
+__host__ __device__ constexpr bool p2d_early(int J) { return NLS_P2D_EARLY && p2d_occ(J) == 1; }
+__host__ __device__ constexpr int p2d_nsl(int J) { return p2d_ds(J) + 3 + (p2d_early(J) ? 1 : 0); }
 __host__ __device__ constexpr int p2d_off_l(int J) { return p2d_nsl(J) * P2D_SR * P2D_SRB; }
 __host__ __device__ constexpr int p2d_off_j(int J) { return p2d_off_l(J) + 2 * P2D_LR * 1024; }
 __host__ __device__ constexpr int p2d_avail(int J) {
@@ -96,7 +99,7 @@ static_assert(p2d_rings_ok(2) && p2d_rings_ok(4) && p2d_rings_ok(6) && p2d_rings
 // S(k+2) and J plane k.
 constexpr int P2D_NSD = 4;  // S DMAs per wave and plane
 __host__ __device__ constexpr int p2d_after(int J, int STW, int i) {
-  const int DS = p2d_ds(J), NP = p2d_np(J), G = P2D_NSD + J + STW, own = NLS_P2D_EARLY ? P2D_NSD + J : 0;
+  const int DS = p2d_ds(J), NP = p2d_np(J), G = P2D_NSD + J + STW, own = p2d_early(J) ? P2D_NSD + J : 0;
   // S(k+2): issued by step i-DS (first group; at i itself when DS = 0) or the prologue
   const int nS = i >= DS ? (DS == 0 ? J : J + STW + (DS - 1) * G + own)
                          : P2D_NSD * (DS - 1 - i) + (NP > 0 ? NP - 1 : 0) * J + i * G + own;
@@ -180,7 +183,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   static_assert(p2d_rings_ok(J), "rings exceed LDS");
   constexpr int DS = p2d_ds(J), NSL = p2d_nsl(J), NP = p2d_np(J);
   constexpr int STW = HZ ? 2 : 1;            // stores per step
-  constexpr int NC = HZ ? 2 * (J + 1) + 3 : J + 2;
+  // columns: gX[0..J], (HZ: gZ[0..J], xx, xz, zz | xx); J = 0 also ||S_0||^2 (the
+  // blind start, k_p2coef mode 2)
+  constexpr int NC = (HZ ? 2 * (J + 1) + 3 : J + 2) + (J == 0 ? 1 : 0);
   constexpr int NPD = NP > 0 ? NP : 1;
   constexpr int RW = P2D_SRB / 16;           // cplx per staged S row (68)
   __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J)];
@@ -343,13 +348,13 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
     const int i = k - k0;
     // NLS_P2D_EARLY: issue first (the slots are free: S plane k-2 since the last
     // barrier, the wave's own J plane k-1 since its last step), then wait
-    if constexpr (NLS_P2D_EARLY) {
+    if constexpr (p2d_early(J)) {
       P2D_ISSUE_S(k + DS + 2, sis);
       if constexpr (J > 0) P2D_ISSUE_J(k + NP - 1, jis);
     }
     wait_step<J, STW>(i);
     raw_barrier();
-    if constexpr (!NLS_P2D_EARLY) {
+    if constexpr (!p2d_early(J)) {
       P2D_ISSUE_S(k + DS + 2, sis);
       if constexpr (J > 0) P2D_ISSUE_J(k + NP - 1, jis);
     }
@@ -410,6 +415,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
       } else {
         acc[J + 1].re = fma(X.re, X.re, fma(X.im, X.im, acc[J + 1].re));
       }
+      if constexpr (J == 0) acc[NC - 1].re = fma(sv[0].re, sv[0].re, fma(sv[0].im, sv[0].im, acc[NC - 1].re));
     }
     lq0 = lq1;
     lq1 = ln;

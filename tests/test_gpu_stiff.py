@@ -158,8 +158,10 @@ def test_nlse_stiff_matches_oracle(dim, n, dx, eq, mode):
     # the fused tail ran every step; with the folded alpha only alpha_0 and the
     # tail's k_alpha_l2 remain per step (2 alpha launches instead of m - 1)
     assert tm["class_count"]["final"] == steps
-    if mode in ("large", "pass2"):
+    if mode == "large":
         assert tm["class_count"]["alpha"] == 2 * steps
+    elif mode == "pass2":  # the tail's alpha pass; alpha_0 only on the first step (then blind start)
+        assert tm["class_count"]["alpha"] == steps + 1
     else:
         assert tm["class_count"]["alpha"] == (m - 1) * steps
     ora, twin = _cpu_nlse(dim, n, dx, u0, dt, m, eq)
