@@ -167,11 +167,35 @@ def cpu_baseline(args):
             out["cores"] = nthr
             out["sample"] = allc["sample"].replace("1 thread", f"OpenMP {nthr} threads")
             out["single_thread"] = {"value": one["value"], "seconds": one["seconds"]}
+        if args.workload == "nlse3d_512":
+            out["c1_full_run"] = _cpu_c1(oracle_py, nthr)
     except (OSError, FileNotFoundError):
         pass
     finally:
         oracle_py.use_openmp(False)
     return out
+
+
+def _cpu_c1(oracle_py, nthr):
+    """BASELINE C1 timed in full on the host: the reference's CPU driver
+    (nlse_driver.cpp:27-106: 256^2, L = 10, T = 1.5, nt = 500 -> 499 SS2 steps of
+    dt = 0.003, Krylov m = 10, the two-soliton collision IC normalised to unit
+    mass) through the oracle restatement, all cores."""
+    n, L, T, nt, m = 256, 10.0, 1.5, 500, 10
+    dx = 2 * L / (n - 1)
+    x = np.linspace(-L, L, n)
+    Y, X = np.meshgrid(x, x, indexing="ij")
+    sig = 0.2
+    u = (np.exp(-((X - 3) ** 2 + (Y - 3) ** 2) / 4 / sig / sig) * np.exp(-1j * (X + Y))
+         + np.exp(-((X + 3) ** 2 + (Y + 3) ** 2) / 4 / sig / sig) * np.exp(1j * (X + Y))).ravel()
+    u = u / np.sqrt(np.sum(np.abs(u) ** 2) * dx * dx)
+    g = oracle_py.grid(2, n, n, 1, dx, dx)
+    t0 = time.perf_counter()
+    oracle_py.nlse_steps(g, u, T / nt, nt - 1, m)
+    el = time.perf_counter() - t0
+    return {"workload": "C1: 2D cubic NLSE 256^2, dt = 3e-3, 499 steps, m = 10 (nlse_driver.cpp)",
+            "seconds": el, "value": n * n * (nt - 1) / el / 1e6, "unit": "Mcells*steps/s",
+            "cores": nthr}
 
 
 def _cpu_sample(args, oracle_py):

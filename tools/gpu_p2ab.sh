@@ -1,10 +1,8 @@
-# same-box A/B of the two-vector pass: lib (A) vs lib_v (B), alternating; tests on A first
+# same-box A/B: lib (A) vs lib_v (B), alternating probes
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_pass2.py > gpurun_out/t_p2.log 2>&1 || { tail -30 gpurun_out/t_p2.log; exit 1; }
-tail -1 gpurun_out/t_p2.log
 for rep in 1 2 3; do for v in lib lib_v; do
-  echo "== $v" ; NLS_AMD_LIB=$PWD/nonlinear-solvers_amd/$v/libnls_amd.so timeout -k 10 120 python tools/p2_probe.py 512 16 4 || exit 1
+  echo "== $v" ; NLS_AMD_LIB=$PWD/nonlinear-solvers_amd/$v/libnls_amd.so timeout -k 10 120 python tools/p2_probe.py ${N:-512} 16 4 || exit 1
 done; done > gpurun_out/p2ab.log 2>&1
 python - <<'PY'
 import re
