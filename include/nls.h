@@ -92,7 +92,15 @@ enum nls_equation {
   NLS_SG_G2 = 5,           /* F = sin u                sg_single.cuh:14-20 */
   NLS_SG_DOUBLE = 6,       /* F = sin u + sin(u/2)     sg_double.cuh:14-21 */
   NLS_SG_HYPERBOLIC = 7,   /* F = sinh u               sg_hyperbolic.cuh:14-20 */
-  NLS_PHI4 = 8             /* F = u + u^3              phi4_single.cuh:14-20 */
+  NLS_PHI4 = 8,            /* F = u + u^3              phi4_single.cuh:14-20 */
+  NLS_NLSE_CQ_G2 = 9       /* G2 cubic-quintic NLSE (nlsolvers/device/include/nlse_cubic_quintic.cuh:9-40,
+                              nlse_cubic_quintic_dev.hpp:79-95, driver nlse_cubic_quintic_driver_dev.cpp):
+                              rho = m (s1|u|^2 + s2|u|^4) with REAL s1 = sigma1[0], s2 = sigma2[0]
+                              (the imaginary parts are ignored), N = exp(-tau/2 rho), linear flow
+                              exp(t*lambda) with t = -tau on the isotropic operator; m(x) via
+                              nls_set_coefficients (cfield NULL; required before the first step,
+                              as for G2); Neumann copy BC
+                              via nls_apply_bc (the driver's apply_bc) */
 };
 
 /* Krylov matrix functions f, applied as f(L) u (nls_krylov_apply) */
@@ -154,7 +162,8 @@ int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past,
 /* G2 only (NLS_NLSE_G2): the focusing field m(x) and the anisotropy c(x) of the
  * operator div(c grad u) (face weights (c_a + c_b)/2, diagonal -sum of weights,
  * scale 1/(dx*dy) in 2D and 1/(dx*dx) in 3D), both real, local slab.  Must be
- * called before the first nls_step. */
+ * called before the first nls_step.  NLS_NLSE_CQ_G2: m(x) only (cfield NULL,
+ * isotropic operator); optional, m = 1 until called. */
 int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfield,
                          uint64_t n_local);
 /* Neumann "copy" boundary condition of the G2 drivers, applied after every step

@@ -909,7 +909,7 @@ void alloc_all(nls_handle *h) {
   if (h->cplx_) {
     if (h->u_slot) h->u = vec_ptr(h, 0, h->nvec[0]) + h->u_off * (int64_t)h->esize;
     else hip_check(h, hipMalloc(&h->u, nbytes), "hipMalloc(u)");
-    if (h->ani) hip_check(h, hipMalloc(&h->mf, (size_t)g.nloc * sizeof(double)), "hipMalloc(m)");
+    if (h->ani || h->nonlin == 3) hip_check(h, hipMalloc(&h->mf, (size_t)g.nloc * sizeof(double)), "hipMalloc(m)");
   } else {
     hip_check(h, hipMalloc(&h->up, nbytes), "hipMalloc(u_past)");
     hip_check(h, hipMalloc(&h->mf, nbytes), "hipMalloc(m)");
@@ -1060,7 +1060,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   const nls_config &c = *cfg;
   std::string why;
   if (c.dim != 2 && c.dim != 3) why = "dim must be 2 or 3";
-  else if (c.equation < 0 || c.equation > NLS_PHI4) why = "unknown equation";
+  else if (c.equation < 0 || c.equation > NLS_NLSE_CQ_G2) why = "unknown equation";
   else if (c.equation == NLS_SG_GAUTSCHI && c.dim != 2 && c.dim != 3) why = "bad dim";
   else if (c.nx < 2 || c.ny < 2 || (c.dim == 3 && c.nz < 2)) why = "grid too small (need >= 2 per dimension)";
   else if (!(c.dx > 0.0) || !(c.dy > 0.0)) why = "dx, dy must be > 0";
@@ -1094,7 +1094,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   h->esize = h->cplx_ ? 16 : 8;
   h->m = (int)c.krylov_m;
   h->nbasis = h->cplx_ ? 1 : 2;
-  h->nonlin = c.equation == NLS_NLSE_CQ ? 1 : (c.equation == NLS_NLSE_G2 ? 2 : 0);
+  h->nonlin = c.equation == NLS_NLSE_CQ ? 1 : (c.equation == NLS_NLSE_G2 ? 2 : (c.equation == NLS_NLSE_CQ_G2 ? 3 : 0));
   h->kg = c.equation == NLS_KG_GAUTSCHI;
   h->ani = c.equation == NLS_NLSE_G2 || h->kg;
   h->s1 = {c.sigma1[0], c.sigma1[1]};
@@ -1251,14 +1251,17 @@ int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past, const
 
 int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfield, uint64_t n) {
   return guarded(h, [&] {
-    if (!h->ani) fail(h, NLS_ERR_STATE, "nls_set_coefficients on a non-G2 handle");
-    if (!mfield || !cfield) fail(h, NLS_ERR_ARG, "NULL input");
+    const bool cq_g2 = h->nonlin == 3;  // m(x) only: isotropic operator, cfield ignored
+    if (!h->ani && !cq_g2) fail(h, NLS_ERR_STATE, "nls_set_coefficients on a non-G2 handle");
+    if (!mfield || (!cfield && !cq_g2)) fail(h, NLS_ERR_ARG, "NULL input");
     check_len(h, n);
     const size_t bytes = (size_t)n * sizeof(double);
     hip_check(h, hipMemcpyAsync(h->mf, mfield, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
-    hip_check(h, hipMemcpyAsync(h->cfb + h->geo.P, cfield, bytes, hipMemcpyHostToDevice, h->stream),
-              "H2D");
-    halo_planes(h, reinterpret_cast<char *>(h->cfb + h->geo.P), (int64_t)sizeof(double));
+    if (!cq_g2) {
+      hip_check(h, hipMemcpyAsync(h->cfb + h->geo.P, cfield, bytes, hipMemcpyHostToDevice, h->stream),
+                "H2D");
+      halo_planes(h, reinterpret_cast<char *>(h->cfb + h->geo.P), (int64_t)sizeof(double));
+    }
     h->coef_set = true;
     h->w0_ready = false;  // the start vector depends on m
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
@@ -1344,9 +1347,13 @@ void ss2_step(nls_handle *h, double dt) {
     halo(h, 0, 0);
   }
   const bool tail = use_tail(h, TAIL_NLSE);
-  if (h->pass2) run_lanczos2(h, 1, NLS_F_EXP_ABS, 0, -0.0, -dt);
-  else if (h->ani) run_lanczos(h, 0, 1, NLS_F_EXP, 0, 0.0, dt, tail);
-  else run_lanczos(h, 0, 1, NLS_F_EXP_ABS, 0, -0.0, -dt, tail);
+  // the linear flow: G1 exp(t|lambda|), t = -tau (eigen_krylov_complex.hpp:71-77); G2
+  // cubic exp(t lambda), t = +tau (nlse_dev.hpp:196); G2 cubic-quintic exp(t lambda),
+  // t = -tau (nlse_cubic_quintic_dev.hpp:86)
+  const int lf = (h->ani || h->nonlin == 3) ? NLS_F_EXP : NLS_F_EXP_ABS;
+  const double ltr = h->ani ? 0.0 : -0.0, lti = h->ani ? dt : -dt;
+  if (h->pass2) run_lanczos2(h, 1, lf, 0, ltr, lti);
+  else run_lanczos(h, 0, 1, lf, 0, ltr, lti, tail);
   void *W = vec_ptr(h, 0, 0);
   KState *st = h->B[0].st;
   int nl = h->nonlin;
@@ -1555,7 +1562,7 @@ bool graph_ready(nls_handle *h, double dt) {
 int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
   return guarded(h, [&] {
     if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
-    if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
+    if ((h->ani || h->nonlin == 3) && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");
     if (h->kg && !(dt > 0.0)) fail(h, NLS_ERR_ARG, "KG: dt must be > 0 (v = (u - u_past)/dt)");
     for (uint32_t s = 0; s < nsteps; ++s) {
@@ -1676,7 +1683,7 @@ int nls_krylov_apply(nls_handle *h, const double *in, double t_re, double t_im, 
   return guarded(h, [&] {
     if (!in || !out) fail(h, NLS_ERR_ARG, "NULL buffer");
     if (func < 0 || func > 7) fail(h, NLS_ERR_ARG, "unknown func");
-    if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
+    if ((h->ani || h->nonlin == 3) && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     check_len(h, n);
     const int b = h->cplx_ ? 0 : 1;  // SG: the scratch basis keeps u intact
     ensure_scratch(h);
@@ -1706,7 +1713,7 @@ int nls_krylov_apply(nls_handle *h, const double *in, double t_re, double t_im, 
 int nls_laplacian_apply(nls_handle *h, const double *x, double *y, uint64_t n) {
   return guarded(h, [&] {
     if (!x || !y) fail(h, NLS_ERR_ARG, "NULL buffer");
-    if (h->ani && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
+    if ((h->ani || h->nonlin == 3) && !h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     check_len(h, n);
     const int b = h->cplx_ ? 0 : 1;
     ensure_scratch(h);

@@ -77,6 +77,8 @@ __device__ __forceinline__ cplx bcast(cplx v, int l) { return {__shfl(v.re, l, 6
 //  1 cubic-quintic (device/nlse_cq_solver.hpp:16-39): d = |u|*|u|, rho = s1 d + s2 d^2
 //  2 G2 cubic with focusing field (nlsolvers/device/include/nlse_dev.hpp:20-40):
 //    out = u * exp(0.5*tau * m|u|^2)   (note the sign: G2 integrates with +tau)
+//  3 G2 cubic-quintic (nlsolvers/device/include/nlse_cubic_quintic.cuh:9-40):
+//    out = u * exp(-0.5*tau * m (s1 d + s2 d^2)), real s1, s2
 //
 // sin/cos of the phase without OCML's sincos, whose large-argument (Payne-Hanek)
 // path needs so many registers that it sets the register budget of every
@@ -143,6 +145,13 @@ __device__ __forceinline__ double gg_force(double y, int kind) {
 }
 
 __device__ __forceinline__ cplx nl_half(cplx u, double mval, double dt, int nonlin, cplx s1, cplx s2) {
+  if (nonlin == 3) {  // G2 cubic-quintic: rho = m (s1 d + s2 d^2), real s (nlse_cubic_quintic.cuh:21-22)
+    const double d = u.re * u.re + u.im * u.im;
+    const double ph = (-0.5 * dt) * (mval * (s1.re * d + s2.re * (d * d)));
+    double sn, cs;
+    nl_sincos(ph, sn, cs);
+    return {cs * u.re - sn * u.im, cs * u.im + sn * u.re};
+  }
   if (nonlin == 0 || nonlin == 2) {
     const double x = u.re * u.re + u.im * u.im;
     const double ph = nonlin == 0 ? (-0.5 * dt) * x : (0.5 * dt) * (mval * x);

@@ -382,7 +382,7 @@ __global__ __launch_bounds__(NTHREADS) void k_nl_init(const cplx *__restrict__ u
                                                       double dt, int nonlin, cplx s1, cplx s2) {
   for (int64_t p = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; p < n;
        p += (int64_t)gridDim.x * NTHREADS)
-    w0[p] = nl_half(u[p], nonlin == 2 ? mf[p] : 0.0, dt, nonlin, s1, s2);
+    w0[p] = nl_half(u[p], nonlin >= 2 ? mf[p] : 0.0, dt, nonlin, s1, s2);
 }
 
 // u = N(sum_k fin_k W_k) ; W_0 <- N(u) for the next step (fused start of step)
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(NTHREADS) void k_final_nlse(cplx *__restrict__ W, i
       cplx y = {0.0, 0.0};
 #pragma unroll
       for (int k = 0; k < M; ++k) y += cmul(cf[k], w[q][k]);
-      const double mv = nonlin == 2 ? mf[p] : 0.0;
+      const double mv = nonlin >= 2 ? mf[p] : 0.0;
       const cplx un = nl_half(y, mv, dt, nonlin, s1, s2);
       st_nt(u + p, un);
       st_nt(W + p, nl_half(un, mv, dt, nonlin, s1, s2));
@@ -488,7 +488,7 @@ __global__ __launch_bounds__(NTHREADS) void k_neumann_bc(cplx *__restrict__ u, c
     if (src == dst) continue;
     const cplx v = u[src];
     u[dst] = v;
-    if (w0_ready) w0[dst] = nl_half(v, nonlin == 2 ? mf[dst] : 0.0, dt, nonlin, s1, s2);
+    if (w0_ready) w0[dst] = nl_half(v, nonlin >= 2 ? mf[dst] : 0.0, dt, nonlin, s1, s2);
   }
 }
 

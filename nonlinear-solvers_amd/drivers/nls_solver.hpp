@@ -421,6 +421,53 @@ class NLSESolverDevice {
   uint32_t stored_ = 0;
 };
 
+// G2 cubic-quintic stepper (nlsolvers/device/include/nlse_cubic_quintic_dev.hpp:
+// 16-95): real sigma1, sigma2 and m(x), no-flux 5-point Laplacian; the
+// constructor stores snapshot 0 (:62), step() stores the pre-BC field when
+// i % freq == 0 (:87-89).  Snapshots past num_snapshots are dropped (the
+// reference writes past the end of its trajectory buffer there).
+class NLSECubicQuinticSolverDevice {
+ public:
+  struct Parameters {
+    uint32_t num_snapshots, snapshot_freq, krylov_dim;
+    double sigma1, sigma2;
+    Parameters(uint32_t ns = 100, uint32_t freq = 5, uint32_t m = 10, double s1 = 1.0,
+               double s2 = 1.0)  // nlse_cubic_quintic_dev.hpp:18-29
+        : num_snapshots(ns), snapshot_freq(freq), krylov_dim(m), sigma1(s1), sigma2(s2) {}
+  };
+  using SnapshotFn = std::function<void(uint32_t index, const std::complex<double> *u, uint64_t n)>;
+
+  NLSECubicQuinticSolverDevice(const Grid &g, const std::complex<double> *host_u0, const double *host_m,
+                               const Parameters &p, SnapshotFn on_snapshot, int device = -1)
+      : h_(g, NLS_NLSE_CQ_G2, p.krylov_dim, device, {p.sigma1, 0.0}, {p.sigma2, 0.0}), p_(p),
+        cb_(std::move(on_snapshot)), pipe_(h_.get(), h_.n(), cb_) {
+    check(nls_set_field(h_.get(), reinterpret_cast<const double *>(host_u0), h_.n()), h_.get());
+    check(nls_set_coefficients(h_.get(), host_m, nullptr, h_.n()), h_.get());
+    store_snapshot();
+  }
+
+  // nlse_cubic_quintic_dev.hpp:79-95
+  void step(std::complex<double> tau, uint32_t step_number) {
+    check(nls_step(h_.get(), tau.imag(), 1), h_.get());
+    if (p_.snapshot_freq && step_number % p_.snapshot_freq == 0) store_snapshot();
+  }
+  void apply_bc() { check(nls_apply_bc(h_.get()), h_.get()); }  // :75-77
+  void finish() { pipe_.finish(); }
+  uint32_t snapshots_stored() const { return stored_; }
+  uint64_t n() const { return h_.n(); }
+
+ private:
+  void store_snapshot() {
+    if (stored_ >= p_.num_snapshots) return;
+    pipe_.push(stored_++);
+  }
+  Handle h_;
+  Parameters p_;
+  SnapshotFn cb_;
+  SnapshotPipe<std::complex<double>> pipe_;
+  uint32_t stored_ = 0;
+};
+
 }  // namespace g2
 
 }  // namespace nls

@@ -15,7 +15,7 @@ import numpy as np
 
 __all__ = [
     "NLSE_CUBIC", "NLSE_CQ", "SG_GAUTSCHI", "NLSE_G2", "KG_GAUTSCHI", "SG_G2", "SG_DOUBLE", "SG_HYPERBOLIC",
-    "PHI4", "REAL_EQUATIONS", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
+    "PHI4", "NLSE_CQ_G2", "REAL_EQUATIONS", "F_EXP_ABS", "F_EXP", "F_COS_SQRT", "F_SINC_SQRT",
     "F_SINC2_SQRT", "F_ID_SQRT", "F_SINC2_HALF", "F_SINC", "MAX_KRYLOV", "NlsError", "Config", "Solver",
     "lib", "lib_path", "rccl_unique_id", "slab_planes", "EXPORTED_SYMBOLS",
 ]
@@ -23,6 +23,9 @@ __all__ = [
 NLSE_CUBIC, NLSE_CQ, SG_GAUTSCHI, NLSE_G2, KG_GAUTSCHI = 0, 1, 2, 3, 4
 # G2 device Gautschi family (nlsolvers/device/include/{sg_single,sg_double,sg_hyperbolic,phi4_single}.cuh)
 SG_G2, SG_DOUBLE, SG_HYPERBOLIC, PHI4 = 5, 6, 7, 8
+# G2 cubic-quintic (nlsolvers/device/include/nlse_cubic_quintic{.cuh,_dev.hpp}): real sigmas,
+# pass sigma1=(s1, 0), sigma2=(s2, 0); m(x) via set_coefficients(m)
+NLSE_CQ_G2 = 9
 REAL_EQUATIONS = (SG_GAUTSCHI, KG_GAUTSCHI, SG_G2, SG_DOUBLE, SG_HYPERBOLIC, PHI4)
 F_EXP_ABS, F_EXP, F_COS_SQRT, F_SINC_SQRT, F_SINC2_SQRT, F_ID_SQRT, F_SINC2_HALF, F_SINC = range(8)
 MAX_KRYLOV = 32
@@ -253,10 +256,15 @@ class Solver:
         self._call(lib().nls_set_sg_state, _dptr(a), _dptr(b), _dptr(c) if c is not None else None,
                    self.n_local)
 
-    def set_coefficients(self, mfield, cfield):
-        """G2: focusing field m(x) and anisotropy c(x) of div(c grad u) (local slab)."""
-        a, b = self._in(mfield, np.float64), self._in(cfield, np.float64)
-        self._call(lib().nls_set_coefficients, _dptr(a), _dptr(b), self.n_local)
+    def set_coefficients(self, mfield, cfield=None):
+        """G2: focusing field m(x) and anisotropy c(x) of div(c grad u) (local slab);
+        NLSE_CQ_G2: m(x) only (cfield None)."""
+        a = self._in(mfield, np.float64)
+        if cfield is None:
+            self._call(lib().nls_set_coefficients, _dptr(a), None, self.n_local)
+        else:
+            b = self._in(cfield, np.float64)
+            self._call(lib().nls_set_coefficients, _dptr(a), _dptr(b), self.n_local)
 
     def apply_bc(self):
         """Neumann copy BC of the G2 drivers (boundaries.cuh:10-81)."""

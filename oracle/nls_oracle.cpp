@@ -577,6 +577,44 @@ int oracle_nlse_g2_steps(const oracle_grid *g, const double *c, const double *mf
   return 0;
 }
 
+// G2 cubic-quintic (nlsolvers/device/include/nlse_cubic_quintic.cuh:9-40,
+// nlse_cubic_quintic_dev.hpp:79-95): rho = m (s1 |u|^2 + s2 |u|^4) with real s1, s2
+// (density_cubic_quintic), u *= exp(-tau/2 rho) (nonlin_part_cubic_quintic with
+// -.5*tau), the linear flow matfunc_->apply(u, buf, -tau): exp(t lambda) with
+// t = -tau (G2 "exp", matfunc_complex.hpp:281-287), on the isotropic no-flux
+// operator (build_laplacian_noflux, nlsolvers/common/include/laplacians.hpp:10-52 --
+// the same matrix as G1's 2D operator).  The density is recomputed from the
+// post-linear field for the second half-step (_dev.hpp:88-91).
+void nonlin_half_cq_g2(cd *u, const double *mf, uint64_t n, double dt, double s1, double s2) {
+  const cd ht = -0.5 * cd(0.0, dt);
+  for (uint64_t p = 0; p < n; ++p) {
+    const double d = u[p].real() * u[p].real() + u[p].imag() * u[p].imag();
+    const double rho = mf[p] * (s1 * d + s2 * d * d);
+    u[p] = u[p] * std::exp(ht * cd(rho, 0.0));
+  }
+}
+
+int oracle_nlse_cq_g2_steps(const oracle_grid *g, const double *mfield, double *u_, double dt,
+                            uint32_t nsteps, uint32_t m, double s1, double s2, int bc) {
+  Grid G;
+  if (!make_grid(g, G) || !mfield || m < 1) return -1;
+  if (bc && (G.nx < 3 || G.ny < 3 || (G.dim == 3 && G.nz < 3))) return -1;
+  StencilOp op{G};
+  const uint64_t n = G.N;
+  cd *u = as_c(u_);
+  std::vector<cd> buf(u, u + n), out(n);
+  const cd tau(0.0, dt);
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    std::memcpy(buf.data(), u, n * sizeof(cd));
+    nonlin_half_cq_g2(buf.data(), mfield, n, dt, s1, s2);
+    krylov_apply(op, buf.data(), -tau, m, ORACLE_F_EXP, out.data());
+    nonlin_half_cq_g2(out.data(), mfield, n, dt, s1, s2);
+    std::memcpy(u, out.data(), n * sizeof(cd));
+    if (bc) neumann_bc(G, u);
+  }
+  return 0;
+}
+
 int oracle_nlse_sewi_steps(const oracle_grid *g, const double *c, const double *mfield,
                            double *u_, double *up_, double dt, uint32_t first_step,
                            uint32_t nsteps, uint32_t m, int bc) {

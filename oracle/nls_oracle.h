@@ -97,6 +97,12 @@ int oracle_neumann_bc_c(const oracle_grid *g, double *u);
 int oracle_nlse_g2_steps(const oracle_grid *g, const double *c,
                          const double *mfield, double *u, double dt,
                          uint32_t nsteps, uint32_t m, int bc);
+/* G2 cubic-quintic SS2 steps (tau = 1j*dt): rho = m (s1|u|^2 + s2|u|^4), real
+ * s1, s2, N = exp(-tau/2 rho), linear flow exp(-tau lambda) on the isotropic
+ * operator; bc != 0: Neumann copy BC after every step (the driver's apply_bc). */
+int oracle_nlse_cq_g2_steps(const oracle_grid *g, const double *mfield, double *u,
+                            double dt, uint32_t nsteps, uint32_t m, double s1,
+                            double s2, int bc);
 
 /* G2 sEWI stepper (NLSESolverDevice::step_sewi, nlsolvers/device/include/nlse_dev.hpp:205-238)
  * for step numbers first_step .. first_step+nsteps-1: step 1 is an SS2 step that

@@ -146,6 +146,26 @@ def nlse_g2_steps(dim, nx, ny, nz, dx, dy, c, mfield, u, dt, nsteps, m, bc=True)
     return u
 
 
+def nlse_cq_g2_steps(dim, nx, ny, nz, dx, dy, mfield, u, dt, nsteps, m, s1, s2, bc=True):
+    """G2 cubic-quintic (nlsolvers/device/include/nlse_cubic_quintic{.cuh:9-40,_dev.hpp:79-95}):
+    rho = m (s1 d + s2 d^2), N = exp(-tau/2 rho), linear exp(-tau lambda) on the
+    isotropic operator (laplacians.hpp:10-52), driver BC after every step."""
+    A = laplacian_triplets(dim, nx, dx, dy) if (dim == 2 and nx == ny) else None
+    mf = np.asarray(mfield, dtype=np.float64).ravel()
+    u = np.asarray(u, dtype=np.complex128).ravel().copy()
+
+    def N(v):
+        d = v.real * v.real + v.imag * v.imag
+        return v * np.exp(-0.5 * 1j * dt * (mf * (s1 * d + s2 * d * d)))
+    ap = (lambda v: A @ v) if A is not None else (lambda v: laplacian_apply(dim, nx, ny, nz, dx, dy, v))
+    for _ in range(nsteps):
+        b = krylov(ap, N(u), -1j * dt, m, F_EXP)
+        u = N(b)
+        if bc:
+            u = neumann_bc(dim, nx, ny, nz, u)
+    return u
+
+
 def nlse_sewi_steps(dim, nx, ny, nz, dx, dy, c, mfield, u, u_prev, dt, first_step, nsteps, m, bc=True):
     """G2 sEWI (nlsolvers/device/include/nlse_dev.hpp:205-238) + driver BC."""
     A = aniso_laplacian(dim, nx, ny, nz, dx, dy, c)

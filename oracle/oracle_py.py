@@ -58,6 +58,8 @@ def lib():
         L.oracle_neumann_bc_c.argtypes = [g, dp]
         L.oracle_nlse_g2_steps.argtypes = [g, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
                                            C.c_int]
+        L.oracle_nlse_cq_g2_steps.argtypes = [g, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
+                                              C.c_double, C.c_double, C.c_int]
         L.oracle_kg_steps.argtypes = [g, dp, dp, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32, C.c_int]
         L.oracle_neumann_bc_r.argtypes = [g, dp]
         L.oracle_gautschi_g2_steps.argtypes = [g, C.c_int, dp, dp, dp, C.c_double, C.c_uint32, C.c_uint32,
@@ -174,6 +176,13 @@ def neumann_bc(g, u):
 def nlse_g2_steps(g, c, mfield, u, dt, nsteps, m, bc=True):
     ui = _c(u).copy()
     _check(lib().oracle_nlse_g2_steps(C.byref(g), _r(c), _r(mfield), ui, dt, nsteps, m, 1 if bc else 0))
+    return ui.view(np.complex128)
+
+
+def nlse_cq_g2_steps(g, mfield, u, dt, nsteps, m, s1, s2, bc=True):
+    """G2 cubic-quintic (nlse_cubic_quintic_dev.hpp:79-95) + the driver's BC."""
+    ui = _c(u).copy()
+    _check(lib().oracle_nlse_cq_g2_steps(C.byref(g), _r(mfield), ui, dt, nsteps, m, s1, s2, 1 if bc else 0))
     return ui.view(np.complex128)
 
 

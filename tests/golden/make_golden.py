@@ -154,6 +154,19 @@ def main():
         assert np.linalg.norm(ku - tu) / np.linalg.norm(tu) < 1e-12, kname
         gg[f"u_{kname}"], gg[f"u_past_{kname}"] = ku, kup
     cases["gautschi_g2"] = gg
+    # --- G2 cubic-quintic (nlse_cubic_quintic_driver_dev.cpp: m=15), real sigmas,
+    #     m(x), isotropic operator, BC per step ------------------------------------
+    n, m, steps, L = 24, 15, 10, 4.0
+    dx = 2 * L / (n - 1)
+    rng = np.random.default_rng(51)
+    u0 = field(2, n, L, 52)
+    mf = 1.0 + 0.3 * rng.standard_normal(u0.size)
+    s1, s2 = 1.0, -0.5
+    g = O.grid(2, n, n, 1, dx, dx)
+    out = O.nlse_cq_g2_steps(g, mf, u0, dt, steps, m, s1, s2, bc=True)
+    tw = np_ref.nlse_cq_g2_steps(2, n, n, 1, dx, dx, mf, u0, dt, steps, m, s1, s2, bc=True)
+    assert np.linalg.norm(out - tw) / np.linalg.norm(tw) < 1e-12
+    cases["cq_g2_2d"] = dict(dim=2, n=n, dx=dx, dt=dt, steps=steps, m=m, s1=s1, s2=s2, u0=u0, mfield=mf, u=out)
     only = sys.argv[1:]  # optional: regenerate only the named fixtures
     for name, d in cases.items():
         if only and name not in only:

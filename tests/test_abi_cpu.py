@@ -48,7 +48,7 @@ def test_config_default_matches_reference_defaults():
 @pytest.mark.parametrize("kw,msg", [
     (dict(m=0), "krylov_m"), (dict(m=33), "krylov_m"), (dict(dim=4), "dim"),
     (dict(nx=1), "grid too small"), (dict(dx=0.0), "dx"), (dict(nranks=2), "rccl_id"),
-    (dict(equation=9), "unknown equation"), (dict(equation=3, nx=2), "need >= 3 cells"), (dict(equation=4, ny=2), "need >= 3 cells"),
+    (dict(equation=10), "unknown equation"), (dict(equation=3, nx=2), "need >= 3 cells"), (dict(equation=4, ny=2), "need >= 3 cells"),
     (dict(equation=3, dim=3, nz=3, nranks=2, group=True), "2 planes per rank"),
     # 32-bit cell indices of the stencil march: (planes + 2) * plane + pad < 2^31
     (dict(dim=2, nx=50000, ny=50000, equation=2), "32-bit cell indices"),
@@ -197,3 +197,29 @@ def test_g2_driver_shape_checks(tmp_path):
     u, mf, cf = _g2_files(tmp_path, (6, 6), (6, 6), (6, 5))
     r = run([os.path.join(BIN, "nlse_2d_dev"), "6", "6", "2", "2", u, out, "1", "10", "5", mf, cf])
     assert r.returncode == 1 and "Faulty c" in r.stderr
+
+
+# ---- G2 cubic-quintic driver (nlse_cubic_quintic_dev): argv and input contract
+
+
+def test_cq_g2_driver_usage_and_shape(tmp_path):
+    """nlse_cubic_quintic_driver_dev.cpp:16-27: 11 or 12 positional args, else usage +
+    exit 1; :58-63 u0 must be [ny, nx] ("Expected: nyxnx")."""
+    exe = os.path.join(BIN, "nlse_cubic_quintic_dev")
+    for k in (0, 10, 13):
+        r = run([exe] + ["8"] * k)
+        assert r.returncode == 1 and "Usage:" in r.stderr and "[input_m.npy]" in r.stderr
+    f = tmp_path / "u0.npy"
+    np.save(f, np.ones((6, 5), complex))
+    out = str(tmp_path / "o.npy")
+    r = run([exe, "6", "5", "2", "2", "1", "0.5", str(f), out, "1", "10", "5"])
+    assert r.returncode == 1 and "Input array dimensions mismatch" in r.stderr and "Expected: 5x6" in r.stderr
+    np.save(f, np.ones((5, 6), complex))
+    r = run([exe, "6", "5", "2", "2", "1", "0.5", str(f), out, "1", "3", "5"])
+    assert r.returncode == 1 and "num_snapshots" in r.stderr
+
+
+def test_abi_exports_cq_g2_equation():
+    assert nls_amd.NLSE_CQ_G2 == 9
+    with open(os.path.join(ROOT, "include", "nls.h")) as fh:
+        assert "NLS_NLSE_CQ_G2 = 9" in fh.read()

@@ -323,3 +323,133 @@ def test_sewi_driver_matches_oracle(tmp_path, dim):
     assert np.array_equal(traj[0].ravel(), u)
     for k in range(1, ns):
         assert rel_l2(traj[k].ravel(), expect[k]) <= TOL_TRAJ, k
+
+
+# ---- G2 cubic-quintic (nlse_cubic_quintic_dev.hpp:16-95) ----------------------
+
+CQ_S = (1.0, -0.5)
+
+
+def cq_solver(dim, nx, ny, nz, dx, m, s1=CQ_S[0], s2=CQ_S[1], **kw):
+    return nls_amd.Solver(dim, nx, ny, nz, dx, dx, equation=nls_amd.NLSE_CQ_G2, m=m,
+                          sigma1=(s1, 0.0), sigma2=(s2, 0.0), **kw)
+
+
+@pytest.mark.parametrize("pass2", ["1", "0"])
+@pytest.mark.parametrize("dim,nx,ny,nz,m", [(2, 32, 32, 1, 15), (2, 300, 20, 1, 15), (2, 7, 5, 1, 10),
+                                            (3, 12, 12, 12, 15), (3, 70, 9, 11, 15), (3, 64, 16, 12, 16)])
+def test_cq_g2_trajectory_with_bc_matches_oracle(monkeypatch, pass2, dim, nx, ny, nz, m):
+    """The driver loop (nlse_cubic_quintic_driver_dev.cpp:95-98): step, then apply_bc.
+    NLS_PASS2 toggles the two-vector basis passes (3D) against the one-vector path."""
+    monkeypatch.setenv("NLS_PASS2", pass2)
+    L, dt, steps = 4.0, 1e-3, 10
+    dx = 2 * L / (nx - 1)
+    u, mf, _ = fields(dim, nx, ny, nz, seed=12)
+    g = O.grid(dim, nx, ny, nz, dx, dx)
+    m = min(m, nx * ny * nz)
+    ref = O.nlse_cq_g2_steps(g, mf, u, dt, steps, m, *CQ_S, bc=True)
+    ref_nobc = O.nlse_cq_g2_steps(g, mf, u, dt, steps, m, *CQ_S, bc=False)
+    with cq_solver(dim, nx, ny, nz, dx, m) as s:
+        s.set_coefficients(mf)
+        s.set_field(u)
+        for _ in range(steps):
+            s.step(dt, 1)
+            s.apply_bc()
+        out = s.get_field()
+        s.set_field(u)
+        s.step(dt, steps)
+        out_nobc = s.get_field()
+    assert rel_l2(out, ref) <= TOL_TRAJ
+    assert rel_l2(out_nobc, ref_nobc) <= TOL_TRAJ
+
+
+def test_cq_g2_golden_fixture_and_errors():
+    d = np.load(os.path.join(GOLD, "cq_g2_2d.npz"))
+    n, m, dt = int(d["n"]), int(d["m"]), float(d["dt"])
+    with cq_solver(2, n, n, 1, float(d["dx"]), m, float(d["s1"]), float(d["s2"])) as s:
+        s.set_field(d["u0"])
+        with pytest.raises(nls_amd.NlsError) as e:
+            s.step(dt)                      # m(x) not uploaded yet
+        assert e.value.code == -6
+        s.set_coefficients(d["mfield"])
+        for _ in range(int(d["steps"])):
+            s.step(dt, 1)
+            s.apply_bc()
+        assert rel_l2(s.get_field(), d["u"]) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("dim,n,nranks", [(3, 16, 2), (3, 13, 3)])
+def test_cq_g2_slabs_match_single_rank(dim, n, nranks):
+    m, dt, steps = 15, 1e-3, 6
+    dx = 8.0 / (n - 1)
+    u, mf, _ = fields(dim, n, n, n, seed=13)
+    P = n * n
+    ref = O.nlse_cq_g2_steps(O.grid(dim, n, n, n, dx, dx), mf, u, dt, steps, m, *CQ_S, bc=True)
+    grp = nls_amd.Group(nranks)
+    out = [None] * nranks
+    err = []
+
+    def work(r):
+        try:
+            s = cq_solver(dim, n, n, n, dx, m, device=0, nranks=nranks, rank=r, group=grp)
+            sl = slice(s.z0 * P, (s.z0 + s.nzl) * P)
+            s.set_coefficients(mf[sl])
+            s.set_field(u[sl])
+            for _ in range(steps):
+                s.step(dt, 1)
+                s.apply_bc()
+            out[r] = s.get_field()
+            s.close()
+        except Exception as e:  # noqa: BLE001
+            err.append((r, e))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    grp.close()
+    assert not err, err
+    assert rel_l2(np.concatenate(out), ref) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("mcase", ["file", "none", "bad_shape"])
+def test_cq_g2_driver_matches_oracle(tmp_path, mcase):
+    """nlse_cubic_quintic_dev end to end: 11/12 args, m = 15, snapshot 0 = u0, pre-BC
+    snapshots every nt/ns steps, BC after each step; a missing m file means m = 1, a
+    wrong-shaped one falls back to m = 1 with the reference's message (:65-85)."""
+    n, ny, L, T, nt, ns = 24, 20, 4.0, 0.02, 11, 5
+    s1, s2 = 0.8, -0.3
+    dx = 2 * L / (n - 1)
+    dy = 2 * L / (ny - 1)
+    u, mf, _ = fields(2, n, ny, 1, seed=14, L=L)
+    paths = {k: str(tmp_path / f"{k}.npy") for k in ("u0", "m", "out")}
+    np.save(paths["u0"], u.reshape(ny, n))
+    args = [os.path.join(BIN, "nlse_cubic_quintic_dev"), str(n), str(ny), str(L), str(L), str(s1), str(s2),
+            paths["u0"], paths["out"], str(T), str(nt), str(ns)]
+    if mcase == "file":
+        np.save(paths["m"], mf.reshape(ny, n))
+        args.append(paths["m"])
+    elif mcase == "bad_shape":
+        np.save(paths["m"], mf.reshape(ny, n)[:, :-1])
+        args.append(paths["m"])
+        mf = np.ones_like(mf)
+    else:
+        mf = np.ones_like(mf)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    if mcase == "bad_shape":
+        assert "Coupling array dimensions mismatch" in r.stderr and "Using default m=1.0" in r.stderr
+    assert r.stdout == ""
+    traj = np.load(paths["out"])
+    assert traj.shape == (ns, ny, n) and traj.dtype == np.complex128
+    g = O.grid(2, n, ny, 1, dx, dy)
+    dt, freq = T / nt, nt // ns
+    cur = u.copy()
+    expect = [u.copy()]
+    for i in range(1, nt):
+        cur = O.nlse_cq_g2_steps(g, mf, cur, dt, 1, 15, s1, s2, bc=False)
+        if i % freq == 0 and len(expect) < ns:
+            expect.append(cur.copy())
+        cur = O.neumann_bc(g, cur)
+    assert np.array_equal(traj[0].ravel(), u)
+    for k in range(1, ns):
+        assert rel_l2(traj[k].ravel(), expect[k]) <= TOL_TRAJ, k

@@ -262,6 +262,37 @@ def test_golden_g2(name):
     assert rel_l2(out, d["u"]) < 1e-13
 
 
+@pytest.mark.parametrize("dim,n,m", [(2, 16, 15), (3, 8, 15)])
+def test_cq_g2_oracle_matches_numpy_twin(dim, n, m):
+    """G2 cubic-quintic (nlse_cubic_quintic_dev.hpp:79-95), two restatements; in 2D the
+    twin uses the triplet builder (laplacians.hpp:10-52), in 3D the stencil."""
+    rng = np.random.default_rng(60 + dim)
+    N = n ** dim
+    mf = rng.uniform(0.5, 1.5, N)
+    u = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    g = O.grid(dim, n, n, n, 0.5, 0.5)
+    for bc in (False, True):
+        a = O.nlse_cq_g2_steps(g, mf, u, 1e-3, 4, m, 1.0, -0.5, bc=bc)
+        b = np_ref.nlse_cq_g2_steps(dim, n, n, n, 0.5, 0.5, mf, u, 1e-3, 4, m, 1.0, -0.5, bc=bc)
+        assert rel_l2(a, b) < 1e-12
+    # real sigmas: the phase has unit modulus and T is Hermitian, so no BC = unitary
+    a = O.nlse_cq_g2_steps(g, mf, u, 1e-3, 4, m, 1.0, -0.5, bc=False)
+    assert abs(np.linalg.norm(a) / np.linalg.norm(u) - 1) < 1e-12
+    # rho = m (s1 d + s2 d^2): m = 2 with (s1, s2) is m = 1 with (2 s1, 2 s2)
+    a = O.nlse_cq_g2_steps(g, 2.0 * np.ones(N), u, 1e-3, 2, m, 1.0, -0.5, bc=True)
+    c = O.nlse_cq_g2_steps(g, np.ones(N), u, 1e-3, 2, m, 2.0, -1.0, bc=True)
+    assert rel_l2(a, c) < 1e-14
+
+
+def test_golden_cq_g2():
+    d = np.load(os.path.join(GOLD, "cq_g2_2d.npz"))
+    n = int(d["n"])
+    g = O.grid(2, n, n, 1, float(d["dx"]), float(d["dx"]))
+    out = O.nlse_cq_g2_steps(g, d["mfield"], d["u0"], float(d["dt"]), int(d["steps"]), int(d["m"]),
+                             float(d["s1"]), float(d["s2"]), bc=True)
+    assert rel_l2(out, d["u"]) < 1e-13
+
+
 @pytest.mark.parametrize("dim,n,m", [(2, 14, 25), (3, 7, 15)])
 def test_sewi_oracle_matches_numpy_twin(dim, n, m):
     """G2 sEWI (nlsolvers/device/include/nlse_dev.hpp:205-238), two restatements."""
