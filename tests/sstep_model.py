@@ -256,3 +256,136 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+# ---- s-step generalisation: one, two or three new vectors per pass ----------------
+#
+# A pass at J with ns new vectors writes V_1 = (L - sigma) W_J - sum_{k<J} conj(H[J,k]) W_k
+# and V_{i+1} = (L - sigma) V_i, each V_i = sum_{l<=J} a_i[l] S_l + sum_p b_i[p] L^p S_J
+# (p = 1..i: a radius-ns stencil of S_J only), and reduces S_l^H V_i and the Gram
+# V_a^H V_b.  In coefficient space, with q^(i) = W^H V_i and nu_i its new norm,
+#   C[:, J+i] = (e_{J+i} - C q^(i)) / nu_i,   D[:, J+i] = (q^(i), nu_i)
+#   H[:, J] = q^(1) + sigma e_J + conj(H[J, :J]) (+ nu_1 e_{J+1})
+#   H[:, J+i-1] = (wv_i + sigma wv_{i-1} - sum_{k < J+i-1} q^(i-1)_k H[:, k]) / nu_{i-1}   (i >= 2)
+# (wv_i = (q^(i), nu_i)), and the next pass's W-coefficients follow the recurrence
+#   w' = H[:, :j] w[:j] + w_j lw - sigma w,  b'_1 = w_j C_jj - sigma b_1,
+#   b'_{p+1} = b_p - sigma b_{p+1}    (L W_j = C_jj L S_j + lw, lw = -C_jj H[:, :j] D[:j, j]).
+
+
+def sstep_schedule(nstore, p3max=5):
+    """[(J, ns)] of the passes storing S_0..S_{nstore-1}: J = 0 two vectors, three while
+    1 <= J <= p3max and they fit, then two, the last pass one or two."""
+    out, J = [], 0
+    while J + 1 < nstore:
+        left = nstore - 1 - J
+        ns = 3 if (1 <= J <= p3max and left >= 3) else min(2, left)
+        out.append((J, ns))
+        J += ns
+    return out
+
+
+def pass_coefficients(C, D, H, sigma, j, ns):
+    """S-basis coefficients a_i[0..j] and stencil coefficients b_i[1..i] of V_1..V_ns."""
+    cjj = C[j, j]
+    lw = -cjj * (H[:j + 1, :j] @ D[:j, j]) if j > 0 else np.zeros(j + 1, complex)
+    w = lw.copy()
+    w[j] -= sigma
+    w[:j] -= np.conj(H[j, :j])
+    b = np.zeros(4, complex)
+    b[1] = cjj
+    A, B = [], []
+    for i in range(ns):
+        A.append(C[:j + 1, :j + 1] @ w)
+        B.append(b.copy())
+        wn = (H[:j + 1, :j] @ w[:j] if j > 0 else np.zeros(j + 1, complex)) + w[j] * lw - sigma * w
+        bn = np.zeros(4, complex)
+        bn[1] = w[j] * cjj - sigma * b[1]
+        for p in range(1, 3):
+            bn[p + 1] = b[p] - sigma * b[p + 1]
+        w, b = wn, bn
+    return A, B
+
+
+def coef_update(C, D, H, sigma, J, ns, g, G):
+    """New columns of C, D, H from the pass's sums g[i][l] = S_l^H V_i (l <= J) and
+    G[a][b] = V_a^H V_b; returns the next shift."""
+    qs, nus = [], []
+    for i in range(ns):
+        n = J + 1 + i
+        sv = np.concatenate([g[i], [G[a][i] for a in range(i)]])  # S_l^H V_i, l < n
+        q = C[:n, :n].conj().T @ sv
+        nu = np.sqrt(max((G[i][i] - np.vdot(q, q)).real, 0.0))
+        C[:, n] = 0
+        C[n, n] = 1.0
+        C[:n, n] -= C[:n, :n] @ q
+        C[:, n] /= nu
+        D[:n, n] = q
+        D[n, n] = nu
+        qs.append(q)
+        nus.append(nu)
+    q1 = qs[0]
+    for k in range(J + 1):
+        H[k, J] = q1[k] + (sigma if k == J else 0.0) + (np.conj(H[J, k]) if k < J else 0.0)
+    H[J + 1, J] = nus[0]
+    for i in range(1, ns):
+        c = J + i  # column J+i-1+1: L W_{J+i}
+        n = c + 2
+        wv = np.zeros(n, complex)
+        wv[:c + 1] = qs[i]
+        wv[c + 1] = nus[i]
+        wp = np.zeros(n, complex)
+        wp[:c] = qs[i - 1]
+        wp[c] = nus[i - 1]
+        col = wv + sigma * wp
+        for k in range(c):
+            col[:k + 2] -= qs[i - 1][k] * H[:k + 2, k]
+        H[:n, c] = col / nus[i - 1]
+    return H[J + ns - 1, J + ns - 1].real if ns > 1 else sigma
+
+
+def lanczos_s(apply, u, m, p3max=5, nstore=None, raw=False):
+    """lanczos2 with the s-step schedule (sstep_schedule); same returns."""
+    u = np.asarray(u, dtype=np.complex128)
+    beta = np.linalg.norm(u)
+    S = [u / beta]
+    M = m + 3
+    C = np.zeros((M, M), complex)
+    D = np.zeros((M, M), complex)
+    H = np.zeros((M, M), complex)
+    C[0, 0] = D[0, 0] = 1.0
+    sigma = np.vdot(S[0], apply(S[0])).real  # the start's alpha pass
+    mm = m if nstore is None else nstore
+    for J, ns in sstep_schedule(mm, p3max):
+        A, B = pass_coefficients(C, D, H, sigma, J, ns)
+        Lp = [None, apply(S[J])]
+        for p in range(2, ns + 1):
+            Lp.append(apply(Lp[-1]))
+        V = []
+        for i in range(ns):
+            v = sum(B[i][p] * Lp[p] for p in range(1, i + 2))
+            for l in range(J + 1):
+                v = v + A[i][l] * S[l]
+            V.append(v)
+        g = [np.array([np.vdot(S[l], V[i]) for l in range(J + 1)]) for i in range(ns)]
+        G = [[np.vdot(V[a], V[b]) for b in range(ns)] for a in range(ns)]
+        sigma = coef_update(C, D, H, sigma, J, ns, g, G)
+        S.extend(V)
+    if raw:
+        return S, C, H, None, beta
+    T = np.zeros((m, m))
+    for j in range(m - 1):
+        T[j, j] = H[j, j].real
+        T[j + 1, j] = T[j, j + 1] = H[j + 1, j].real
+    return T, S[:m], C[:m, :m], beta, None
+
+
+def krylov_s_tail(apply, u, t, m, func, p3max=5):
+    S, C, H, _, beta = lanczos_s(apply, u, m, p3max, nstore=m - 1, raw=True)
+    j = m - 2
+    y = apply(S[j])
+    a, l2 = np.vdot(S[j], y), np.vdot(y, y).real
+    coefS, cy, T = tail_coefficients(S, C, H, beta, a, l2, m, t, func)
+    out = cy * y
+    for l in range(j + 1):
+        out = out + coefS[l] * S[l]
+    return out, T
