@@ -441,22 +441,28 @@ def main():
     esz = 8 if w["eq"] in (2, 4) else 16
     fcnt = tm["class_count"].get("final", 0)
     ucnt = tm["update_count"]
-    pass2 = m >= 4 and ucnt[0] > 0 and all(ucnt[j] == 0 for j in range(1, m - 1, 2))
-    p2J = max([j for j, c in enumerate(ucnt) if c] or [0])
-    p2_ms = tm["update_ms"][p2J] / ucnt[p2J] if pass2 and ucnt[p2J] else 0.0
+    # s-step passes (k_p2d / k_p3d): update launches only at the schedule's pass
+    # starts J (never at J = 1); pass J writes S_{J+1} .. S_{J+ns}, the last one S_{m-2}
+    pass2 = m >= 4 and ucnt[0] > 0 and ucnt[1] == 0
+    sched = []
+    if pass2:
+        Js = [j for j in range(m - 1) if ucnt[j]]
+        sched = [(j, (Js[i + 1] if i + 1 < len(Js) else m - 2) - j) for i, j in enumerate(Js)]
+    pass_ms = {j: tm["update_ms"][j] / ucnt[j] for j, _ in sched}
+    p2J, p2ns = max(sched, key=lambda e: pass_ms[e[0]]) if sched else (0, 0)
+    p2_ms = pass_ms.get(p2J, 0.0)
     tail_ms = tm["class_ms"]["final"] / fcnt if fcnt else 0.0
     own_bytes = None
-    if pass2:  # alpha_0 + sum_J (J+1 reads + 2 or 1 writes) + the tail's alpha + tail (m+1)
-        own_bytes = esz * (1 + sum(J + 3 if J + 2 < m - 1 else J + 2 for J in range(0, m - 2, 2)) + 1 + (m + 1))
+    if pass2:  # alpha_0 + sum over passes (J+1 reads + ns writes) + the tail's alpha + tail (m+1)
+        own_bytes = esz * (1 + sum(j + 1 + ns for j, ns in sched) + 1 + (m + 1))
     if pass2 and p2_ms > tail_ms:
         J = p2J
         cnt = ucnt[J]
         avg_ms = p2_ms
-        hz = J + 2 < m - 1
-        bytes_launch = (J + 1 + (2 if hz else 1)) * esz * n_local
-        kname = f"k_p2d<J={J}> (two-vector Lanczos pass: radius-2 stencil + CGS coefficients, " \
-                f"{J + 1} reads + {2 if hz else 1} writes)"
-        kprefix = "k_p2d<"
+        bytes_launch = (J + 1 + p2ns) * esz * n_local
+        kname = f"k_p{max(p2ns, 2)}d<J={J}> ({p2ns}-vector Lanczos pass: radius-{p2ns} stencil + CGS " \
+                f"coefficients, {J + 1} reads + {p2ns} writes)"
+        kprefix = f"k_p{max(p2ns, 2)}d<"
     elif fcnt and w["eq"] in (0, 1, 3) and not w.get("sewi"):
         J = m - 2
         cnt = fcnt
@@ -513,7 +519,8 @@ def main():
             "achieved_GBs": step_bytes / (step_ms * 1e-3) / 1e9,
             "frac": step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "gpu_kernel_ms_per_step": {k: v / max(tm["steps"], 1) for k, v in tm["class_ms"].items()},
-            "lanczos": "two-vector passes (k_p2d) + fused tail" if pass2 else "one-vector passes + fused tail",
+            "lanczos": ("s-step passes " + " ".join(f"J{j}:{ns}" for j, ns in sched) + " + fused tail")
+            if pass2 else "one-vector passes + fused tail",
             "moved_bytes_per_cell_step": own_bytes,
             "moved_GBs": own_bytes * n_local / (step_ms * 1e-3) / 1e9 if own_bytes else None,
         },

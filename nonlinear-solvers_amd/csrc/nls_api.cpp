@@ -115,6 +115,7 @@ struct nls_handle {
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
   int p2impl = 2;              // 2: LDS-DMA k_p2d; 1: register-march k_pass2r (NLS_P2_IMPL)
+  bool p3 = false;             // three-vector passes k_p3d at J = 2, 5 (single rank, k_p2d; NLS_PASS3=1)
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
   bool p2_warm = false;        // the P2State holds a previous basis' alpha_0
@@ -649,10 +650,27 @@ int p2_grid(const nls_handle *h, int J) {
 // last alpha pass (k_alpha_l2 over S_{m-2}) and k_p2tail complete T; the
 // eigensolve; k_p2tfin maps fin to the coefficients of the caller's k_tail
 // (S_0..S_{m-2} and L S_{m-2}: the last Lanczos vector is never stored).
+// The s-step schedule (tests/sstep_model.py sstep_schedule): [(J, ns)] of the
+// passes storing S_0..S_{nstore-1}, two new vectors per pass, three (k_p3d) at
+// J = 2 and 5 when the basis reaches S_8 (so the two-vector passes stay at even J),
+// the last pass one or two.
+std::vector<std::pair<int, int>> p2_schedule(const nls_handle *h, int nstore) {
+  std::vector<std::pair<int, int>> out;
+  const bool use3 = h->p3 && nstore - 1 >= 8;
+  for (int J = 0; J + 1 < nstore;) {
+    const int left = nstore - 1 - J;
+    const int ns = (use3 && (J == 2 || J == 5) && left >= 3) ? 3 : std::min(2, left);
+    out.emplace_back(J, ns);
+    J += ns;
+  }
+  return out;
+}
+
 void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
   const int m = h->m, nstore = m - 1;
   KState *st = h->B[0].st;
   void *ps = h->p2;
+  const std::vector<std::pair<int, int>> sched = p2_schedule(h, nstore);
   // blind start once a previous basis left its alpha_0 (the shift of the J = 0
   // pass): no alpha pass over W_0, beta from the pass's own ||S_0||^2
   const bool blind = h->p2_warm && h->p2_blind && h->p2impl == 2;  // k_p2d<0> reduces ||S_0||^2
@@ -663,8 +681,8 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
     reduce_iter(h, 0, 0);
   }
   {
-    int J = 0, mm = nstore, mode = blind ? 2 : 0;
-    void *args[] = {&ps, &st, &J, &mm, &mode};
+    int J = 0, mode = blind ? 2 : 0, ns = 0, nsn = sched[0].second;
+    void *args[] = {&ps, &st, &J, &mode, &ns, &nsn};
     launch(h, 2, 0, kernel_p2coef(), 1, args);
   }
   h->p2_warm = true;
@@ -673,13 +691,12 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
   Geo g = h->geo;
   g.kz = h->p2kz;
   cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(h->p2) + p2state_sums_offset());
-  int J = 0;
   const bool split = p2_split(h);
-  while (J + 1 < nstore) {
-    const bool hz = J + 2 < nstore;
-    const int out = hz ? J + 2 : J + 1;  // the next stencil vector (Z, or a last X-only pass's X)
+  for (size_t si = 0; si < sched.size(); ++si) {
+    int J = sched[si].first, ns = sched[si].second;
+    const int out = J + ns;  // the pass's last vector: the next stencil vector
     int nb = p2_grid(h, J);
-    const void *fn = kernel_pass2(J, hz, h->p2impl);
+    const void *fn = ns == 3 ? kernel_pass3(J) : kernel_pass2(J, ns == 2, h->p2impl);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
     if (!split) {
       int poff = 0;
@@ -712,15 +729,15 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
       launch(h, 1, J, fn, nb - 2 * tb, args);
       hip_check(h, hipStreamWaitEvent(h->stream, h->ev_bdone, 0), "hipStreamWaitEvent");
     }
+    // columns: S-dots per new vector, the Gram's upper triangle, J = 0: ||S_0||^2
     const cplx *pA = nullptr;
-    int nbA = 0, ncA = 0, ncU = (hz ? 2 * J + 5 : J + 2) + (J == 0 ? 1 : 0);
+    int nbA = 0, ncA = 0, ncU = ns * (J + 1) + ns * (ns + 1) / 2 + (J == 0 ? 1 : 0);
     void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
     launch(h, 2, J, kernel_colsum(), ncU, cargs);
     if (h->collective) allreduce_sums(h, 0, ncU, sums);
-    int mm = nstore, mode = 1, jj = J;
-    void *a2[] = {&ps, &st, &jj, &mm, &mode};
+    int mode = 1, nsn = si + 1 < sched.size() ? sched[si + 1].second : 0;
+    void *a2[] = {&ps, &st, &J, &mode, &ns, &nsn};
     launch(h, 2, J, kernel_p2coef(), 1, a2);
-    J += hz ? 2 : 1;
   }
   halo_wait(h);
   // the tail's alpha pass over S_{m-2}: a = S^H L S, ||S||^2, ||L S||^2
@@ -848,11 +865,15 @@ void alloc_all(nls_handle *h) {
     h->p2kz = (int)std::max<int64_t>(16, std::min<int64_t>(256, (g.npl + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("NLS_P2_BLIND")) h->p2_blind = std::atoi(e) != 0;
+    // three-vector passes: parity-green but slower than the two-vector schedule at
+    // 512^3 (k_p3d issue-bound at one wave per SIMD), so opt-in
+    h->p3 = false;
+    if (const char *e = std::getenv("NLS_PASS3")) h->p3 = h->p2impl == 2 && !h->collective && std::atoi(e) != 0;
     h->p2grid = 0;
     for (int J = 0; J + 1 < h->m - 1; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
     hip_check(h, hipMalloc(&h->p2, p2state_bytes()), "hipMalloc(p2)");
     hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes(), h->stream), "hipMemset");
-    hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (2 * MMAX + 8) * sizeof(cplx)),
+    hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)),
               "hipMalloc(partP2)");
     const size_t zb = (size_t)std::max<int64_t>(g.nx, 64) * sizeof(cplx);
     hip_check(h, hipMalloc(&h->zbuf, zb), "hipMalloc(zbuf)");

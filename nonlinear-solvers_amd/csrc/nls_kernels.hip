@@ -27,6 +27,7 @@
 #include "nls_stencil.hpp"
 #include "nls_pass2.hpp"
 #include "nls_pass2d.hpp"
+#include "nls_pass3d.hpp"
 
 namespace nls {
 
@@ -839,6 +840,18 @@ const void *kernel_pass2(int J, bool hz, int impl) {
     default: return nullptr;
   }
 }
+// three-vector passes (nls_pass3d.hpp): the s-step schedule's J = 2 and 5
+const void *kernel_pass3(int J) {
+  switch (J) {
+    case 2: return reinterpret_cast<const void *>(&k_p3d<2>);
+    case 5: return reinterpret_cast<const void *>(&k_p3d<5>);
+    default: return nullptr;
+  }
+}
+static_assert(offsetof(P2State, bZ2) == offsetof(P2State, bZ1) + sizeof(cplx) &&
+                  offsetof(P2State, bY2) == offsetof(P2State, bY1) + sizeof(cplx) &&
+                  offsetof(P2State, bY3) == offsetof(P2State, bY2) + sizeof(cplx),
+              "k_p2coef writes the b coefficients of a vector as an array");
 const void *kernel_p2tail() { return reinterpret_cast<const void *>(&k_p2tail); }
 const void *kernel_p2tfin() { return reinterpret_cast<const void *>(&k_p2tfin); }
 const void *kernel_p2coef() { return reinterpret_cast<const void *>(&k_p2coef); }

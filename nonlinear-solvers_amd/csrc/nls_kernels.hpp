@@ -70,7 +70,8 @@ constexpr int P2R_WAVE_XO = 60;  // == P2R_XO
 #define NLS_P2R_RB1 12  // k_pass2r: one row per wave from this J (registers)
 #endif
 #define P2R_ROWS(J) (((J) == 4 || (J) >= NLS_P2R_RB1) ? 1 : 2)  // 512^3: J=4 3.92 vs 4.90 ms with one row
-const void *kernel_p2coef();
+const void *kernel_p2coef();  // (P2State*, KState*, int J, int mode, int ns, int nsn)
+const void *kernel_pass3(int J);  // k_p3d<J>, J = 2, 5 (same arguments as kernel_pass2's impl 2)
 const void *kernel_p2fin();
 size_t p2state_bytes();
 size_t p2state_sums_offset();

@@ -22,10 +22,10 @@ struct P2State {
   cplx C[P2M][P2M];  // C[l][i]: W_i = sum_l S_l C[l][i]
   cplx D[P2M][P2M];  // D[i][l]: S_l = sum_i W_i D[i][l]
   cplx H[P2M][P2M];  // H[k][i] = W_k^H L W_i
-  cplx aX[P2M], aZ[P2M];
-  cplx bX1, bZ1, bZ2;
+  cplx aX[P2M], aZ[P2M], aY[P2M];  // S coefficients of V_1 (X), V_2 (Z), V_3 (Y)
+  cplx bX1, bZ1, bZ2, bY1, bY2, bY3;  // stencil coefficients: b_i[p] of L^p S_J (bZ1, bZ2 = b_2[1..2])
   double sigma, beta;
-  cplx sums[2 * P2M + 8];
+  cplx sums[3 * P2M + 8];
   cplx tk[P2M];   // fused tail: t_k = W_k^H L S_{m-2} (k_p2tail)
   double beta_t;  // fused tail: beta_{m-1}
   int32_t blind;  // the J = 0 pass ran on the raw start vector (mode 2), beta from its sums
@@ -193,21 +193,24 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2r(cplx *__restrict__ W, int64
   }
 }
 
-// Coefficient kernel (one workgroup).  mode 0: start (after the alpha pass and
-// reduction of W_0: s[0] = beta, H[0][0] = alpha_0); mode 2: blind start, no
-// alpha pass: the J = 0 pass runs on the raw start vector (C00 = 1) with the
-// previous step's alpha_0 as its shift and also reduces ||S_0||^2; mode 1 at
-// J = 0 then takes beta from it, rescales the sums to the normalised scheme and
-// the stored S_1, S_2 columns of C (and D) by 1/beta (beta); mode 1: after the
-// pass at J (sums = the pass's columns, summed).  Computes the new columns of C, D, H
-// and, if another pass follows (J' + 1 < m), its coefficients; otherwise T into
-// the KState for k_reduce_final (s[] = 1, so fin is in the W basis; k_p2fin
-// converts it).
+// Coefficient kernel (one workgroup).  A pass at J writes ns = 1, 2 or 3 new
+// vectors V_1 = L W_J - sigma W_J - sum_{k<J} conj(H[J][k]) W_k, V_{i+1} = (L - sigma) V_i
+// (k_p2d: ns <= 2, k_p3d: ns = 3) and reduces, in this order, S_l^H V_i (l <= J, per i)
+// and the Gram V_a^H V_b (a <= b, row by row); J = 0 of a blind start also ||S_0||^2.
+// mode 0: start (after the alpha pass and reduction of W_0: s[0] = beta, H[0][0] =
+// alpha_0); mode 2: blind start, no alpha pass: the J = 0 pass runs on the raw start
+// vector (C00 = 1) with the previous step's alpha_0 as its shift; mode 1 at J = 0 then
+// takes beta from ||S_0||^2, rescales the sums to the normalised scheme and the new
+// rows of C (columns of D) by 1/beta (beta); mode 1: after the pass at J (sums = its
+// columns, summed).  Computes the new columns of C, D, H (tests/sstep_model.py
+// coef_update) and, for a next pass of nsn > 0 vectors at J' = J + ns, its
+// coefficients (pass_coefficients); nsn = 0: T into the KState for k_reduce_final
+// (s[] = 1, so fin is in the W basis; k_p2fin converts it).
 __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, KState *__restrict__ st,
-                                                     int J, int m, int mode) {
-  __shared__ cplx p[P2M], q[P2M], lw[P2M], xw[P2M], zw[P2M];
-  __shared__ cplx gz[P2M];
-  __shared__ double nu[2];
+                                                     int J, int mode, int ns, int nsn) {
+  __shared__ cplx q[3][P2M], sv[P2M], lw[P2M], w[2][P2M];
+  __shared__ cplx bb[2][4];
+  __shared__ double nu[3];
   __shared__ double s_prev, s_beta;
   const int t = threadIdx.x;
   int Jn;  // J of the next pass
@@ -240,120 +243,84 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
     __syncthreads();
     Jn = 0;
   } else {
-    const int hz = J + 2 < m;  // the pass also produced Z
+    cplx *sw = ps->sums;
+    const int ng = ns * (ns + 1) / 2, og = ns * (J + 1);  // Gram entries, their offset
+    // Gram entry (a, b), a <= b
+    auto gidx = [ns, og](int a, int b) { return og + a * ns - a * (a - 1) / 2 + (b - a); };
     if (J == 0 && ps->blind) {
-      // the J = 0 pass ran on the raw S_0 (C00 = 1): its sums are beta (gX, gZ) and
-      // beta^2 (xx, xz, zz) times those of the normalised scheme; ||S_0||^2 follows them
-      cplx *sw = ps->sums;
-      const int ns = hz ? 5 : 2;
+      // the J = 0 pass ran on the raw S_0 (C00 = 1): its S-dots are beta, its Gram
+      // beta^2 times those of the normalised scheme; ||S_0||^2 follows them
       if (t == 0) {
-        const double b = sqrt(sw[ns].re);
+        const double b = sqrt(sw[og + ng].re);
         const double ib = b > 0.0 ? 1.0 / b : 0.0;
         s_beta = b;
-        sw[0] = ib * sw[0];
-        if (hz) {
-          sw[1] = ib * sw[1];
-          sw[2] = (ib * ib) * sw[2];
-          sw[3] = (ib * ib) * sw[3];
-          sw[4] = (ib * ib) * sw[4];
-        } else {
-          sw[1] = (ib * ib) * sw[1];
-        }
+        for (int e = 0; e < og; ++e) sw[e] = ib * sw[e];
+        for (int e = og; e < og + ng; ++e) sw[e] = (ib * ib) * sw[e];
         ps->beta = b;
         ps->C[0][0] = {ib, 0.0};
         ps->D[0][0] = {b, 0.0};
       }
       __syncthreads();
     }
-    const cplx *sm = ps->sums;
-    // sums: hz: gX[0..J], gZ[0..J], xx, xz, zz; else gX[0..J], xx
-    const int o = 2 * J + 2;
-    const cplx xx = hz ? sm[o] : sm[J + 1];
-    const cplx xz = hz ? sm[o + 1] : cplx{0.0, 0.0}, zz = hz ? sm[o + 2] : cplx{0.0, 0.0};
-    if (hz)
-      for (int l = t; l <= J; l += NTHREADS) gz[l] = sm[J + 1 + l];
-    __syncthreads();
-#ifdef NLS_P2_DEBUG
-    if (t == 0 && hz)
-      for (int l = 0; l <= J; ++l)
-        printf("[p2 J=%d] gz[%d] = %.15e %.15e  gX = %.15e sigma %.15e\n", J, l, gz[l].re, gz[l].im, sm[l].re, ps->sigma);
-#endif
-    // p_k = W_k^H X = sum_l conj(C[l][k]) (S_l^H X)
-    for (int k = t; k <= J; k += NTHREADS) {
-      cplx v = {0.0, 0.0};
-      for (int l = 0; l <= k; ++l) v += cj_mul(ps->C[l][k], sm[l]);
-      p[k] = v;
-    }
-    __syncthreads();
-    if (t == 0) {
-      double n2 = xx.re;
-      for (int k = 0; k <= J; ++k) n2 -= abs2(p[k]);
-      nu[0] = n2 > 0.0 ? sqrt(n2) : 0.0;
-    }
-    __syncthreads();
-    const double nu1 = nu[0], inu1 = nu1 > 0.0 ? 1.0 / nu1 : 0.0;
     const double sig = ps->sigma;
-    for (int i = t; i <= J + 1; i += NTHREADS) {
-      // C[:, J+1] = (e_{J+1} - C p) / nu1 ; D[:, J+1] = (p, nu1)
-      cplx v = {i == J + 1 ? 1.0 : 0.0, 0.0};
-      for (int k = i; k <= J; ++k) v = v - cmul(ps->C[i][k], p[k]);
-      ps->C[i][J + 1] = inu1 * v;
-      ps->D[i][J + 1] = i <= J ? p[i] : cplx{nu1, 0.0};
-      // H column J: p_k + sigma delta_kJ + conj(H[J][k]) (k < J); H[J+1][J] = nu1
-      cplx h = i <= J ? p[i] : cplx{nu1, 0.0};
-      if (i == J) h.re += sig;
-      if (i < J) h += cconj(ps->H[J][i]);
-      ps->H[i][J] = h;
-    }
-    __syncthreads();
-    if (hz) {
-      // q_k = W_k^H Z (k <= J+1): S-dots gZ (l <= J) and S_{J+1}^H Z = xz
-      for (int k = t; k <= J + 1; k += NTHREADS) {
+    for (int i = 0; i < ns; ++i) {
+      const int n = J + 1 + i;  // the new vector's index
+      // S_l^H V_i for l < n: the pass's S-dots (l <= J), the Gram (l = J + 1 + a)
+      for (int l = t; l < n; l += NTHREADS) sv[l] = l <= J ? sw[i * (J + 1) + l] : sw[gidx(l - J - 1, i)];
+      __syncthreads();
+      // q_k = W_k^H V_i = sum_{l <= k} conj(C[l][k]) S_l^H V_i
+      for (int k = t; k < n; k += NTHREADS) {
         cplx v = {0.0, 0.0};
-        for (int l = 0; l <= k && l <= J; ++l) v += cj_mul(ps->C[l][k], gz[l]);
-        if (k == J + 1) v += cj_mul(ps->C[J + 1][J + 1], xz);
-        q[k] = v;
+        for (int l = 0; l <= k; ++l) v += cj_mul(ps->C[l][k], sv[l]);
+        q[i][k] = v;
       }
       __syncthreads();
       if (t == 0) {
-        double n2 = zz.re;
-        for (int k = 0; k <= J + 1; ++k) n2 -= abs2(q[k]);
-        nu[1] = n2 > 0.0 ? sqrt(n2) : 0.0;
+        double n2 = sw[gidx(i, i)].re;
+        for (int k = 0; k < n; ++k) n2 -= abs2(q[i][k]);
+        nu[i] = n2 > 0.0 ? sqrt(n2) : 0.0;
       }
       __syncthreads();
-      const double nu2 = nu[1], inu2 = nu2 > 0.0 ? 1.0 / nu2 : 0.0;
-      for (int i = t; i <= J + 2; i += NTHREADS) {
-        cplx v = {i == J + 2 ? 1.0 : 0.0, 0.0};
-        for (int k = i; k <= J + 1; ++k) v = v - cmul(ps->C[i][k], q[k]);
-        ps->C[i][J + 2] = inu2 * v;
-        ps->D[i][J + 2] = i <= J + 1 ? q[i] : cplx{nu2, 0.0};
-      }
-      // H column J+1 = (wz + sigma wx - p_J (wx + sigma e_J + conj(H[J][:J])) - sum_{k<J} p_k H[:,k]) / nu1
-      //   wx = (p, nu1, 0), wz = (q, nu2)
-      for (int i = t; i <= J + 2; i += NTHREADS) {
-        const cplx wxi = i <= J ? p[i] : (i == J + 1 ? cplx{nu1, 0.0} : cplx{0.0, 0.0});
-        const cplx wzi = i <= J + 1 ? q[i] : cplx{nu2, 0.0};
-        cplx lwj = wxi;
-        if (i == J) lwj.re += sig;
-        if (i < J) lwj += cconj(ps->H[J][i]);
-        cplx v = wzi + sig * wxi - cmul(p[J], lwj);
-        if (i <= J)
-          for (int k = (i > 0 ? i - 1 : 0); k < J; ++k) v = v - cmul(p[k], ps->H[i][k]);
-        ps->H[i][J + 1] = inu1 * v;
+      const double nui = nu[i], inu = nui > 0.0 ? 1.0 / nui : 0.0;
+      // C[:, n] = (e_n - C q) / nu ; D[:, n] = (q, nu)
+      for (int r = t; r <= n; r += NTHREADS) {
+        cplx v = {r == n ? 1.0 : 0.0, 0.0};
+        for (int k = r; k < n; ++k) v = v - cmul(ps->C[r][k], q[i][k]);
+        ps->C[r][n] = inu * v;
+        ps->D[r][n] = r < n ? q[i][r] : cplx{nui, 0.0};
       }
       __syncthreads();
-      if (t == 0) ps->sigma = ps->H[J + 1][J + 1].re;
-      Jn = J + 2;
-    } else {
-      Jn = J + 1;  // W_{m-1} done
+    }
+    // H column J: q1_k + sigma delta_kJ + conj(H[J][k]) (k < J); H[J+1][J] = nu_1
+    for (int r = t; r <= J + 1; r += NTHREADS) {
+      cplx h = r <= J ? q[0][r] : cplx{nu[0], 0.0};
+      if (r == J) h.re += sig;
+      if (r < J) h += cconj(ps->H[J][r]);
+      ps->H[r][J] = h;
     }
     __syncthreads();
+    // H column c = J + i (i >= 1), L W_c = (V_{i+1} + sigma V_i - sum_{k<c} q^(i-1)_k L W_k) / nu_{i-1}:
+    //   (wv_i + sigma wv_{i-1} - sum_{k<c} q^(i-1)_k H[:, k]) / nu_{i-1},  wv_i = (q^(i), nu_i)
+    for (int i = 1; i < ns; ++i) {
+      const int c = J + i;
+      const double inp = nu[i - 1] > 0.0 ? 1.0 / nu[i - 1] : 0.0;
+      for (int r = t; r <= c + 1; r += NTHREADS) {
+        cplx v = r <= c ? q[i][r] : cplx{nu[i], 0.0};
+        const cplx wp = r < c ? q[i - 1][r] : (r == c ? cplx{nu[i - 1], 0.0} : cplx{0.0, 0.0});
+        v += sig * wp;
+        for (int k = (r > 0 ? r - 1 : 0); k < c; ++k) v = v - cmul(q[i - 1][k], ps->H[r][k]);
+        ps->H[r][c] = inp * v;
+      }
+      __syncthreads();
+    }
+    if (t == 0 && ns > 1) ps->sigma = ps->H[J + ns - 1][J + ns - 1].re;
+    Jn = J + ns;
+    __syncthreads();
     if (J == 0 && ps->blind) {
-      // the stored S_1 (and S_2) are beta times the normalised scheme's: their C rows
-      // scale by 1/beta, their D columns by beta (C = D^-1 stays consistent)
+      // the stored S_1..S_ns are beta times the normalised scheme's: their C rows scale
+      // by 1/beta, their D columns by beta (C = D^-1 stays consistent)
       const double b = s_beta, ib = b > 0.0 ? 1.0 / b : 0.0;
-      const int nl = hz ? 2 : 1;
-      for (int e = t; e < nl * P2M; e += NTHREADS) {
+      for (int e = t; e < ns * P2M; e += NTHREADS) {
         const int l = 1 + e / P2M, k = e % P2M;
         ps->C[l][k] = ib * ps->C[l][k];
         ps->D[k][l] = b * ps->D[k][l];
@@ -362,54 +329,60 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       if (t == 0) ps->blind = 0;
     }
   }
-  if (Jn + 1 < m) {
-    // coefficients of the pass at Jn
+  if (nsn > 0) {
+    // coefficients of the pass at j = Jn: V_i = sum_l a_i[l] S_l + sum_p b_i[p] L^p S_j
+    // through the W coefficients w of V_i (tests/sstep_model.py pass_coefficients):
+    //   lw = -C_jj H[:, :j] D[:j, j]   (L W_j = C_jj L S_j + lw)
+    //   w_1 = lw - sigma e_j - conj(H[j][:j]),  b_1 = (C_jj)
+    //   w_{i+1} = H[:, :j] w_i[:j] + w_i[j] lw - sigma w_i
+    //   b_{i+1}[1] = w_i[j] C_jj - sigma b_i[1],  b_{i+1}[p+1] = b_i[p] - sigma b_i[p+1]
     const int j = Jn;
     const double sig = ps->sigma;
     const cplx cjj = ps->C[j][j];
-    // lw = -C[j][j] H[:, :j] D[:j, j]   (the W part of L W_j besides C[j][j] L S_j)
     for (int k = t; k <= j; k += NTHREADS) {
       cplx v = {0.0, 0.0};
       for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) v += cmul(ps->H[k][i], ps->D[i][j]);
       v = cmul(cjj, v);
       lw[k] = {-v.re, -v.im};
+      cplx x = lw[k];
+      if (k == j) x.re -= sig;
+      if (k < j) x = x - cconj(ps->H[j][k]);
+      w[0][k] = x;
     }
+    if (t == 0) bb[0][0] = bb[0][1] = bb[0][2] = bb[0][3] = {0.0, 0.0};
+    if (t == 0) bb[0][1] = cjj;
     __syncthreads();
-    for (int k = t; k <= j; k += NTHREADS) {
-      cplx v = lw[k];
-      if (k == j) v.re -= sig;
-      if (k < j) v = v - cconj(ps->H[j][k]);
-      xw[k] = v;
-    }
-    __syncthreads();
-    // zw = H[:, :j] xw[:j] + xw[j] lw - sigma xw
-    for (int k = t; k <= j; k += NTHREADS) {
-      cplx v = {0.0, 0.0};
-      for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) v += cmul(ps->H[k][i], xw[i]);
-      v += cmul(xw[j], lw[k]);
-      v = v - sig * xw[k];
-      zw[k] = v;
-    }
-    __syncthreads();
-    // S-basis coefficients a = C w
-    for (int l = t; l <= j; l += NTHREADS) {
-      cplx ax = {0.0, 0.0}, az = {0.0, 0.0};
-      for (int k = l; k <= j; ++k) {
-        ax += cmul(ps->C[l][k], xw[k]);
-        az += cmul(ps->C[l][k], zw[k]);
+    cplx *adst[3] = {ps->aX, ps->aZ, ps->aY};
+    cplx *bdst[3] = {&ps->bX1, &ps->bZ1, &ps->bY1};
+    for (int i = 0; i < nsn; ++i) {
+      const int cu = i & 1, nx = cu ^ 1;
+      // S-basis coefficients a_i = C w_i
+      for (int l = t; l <= j; l += NTHREADS) {
+        cplx a = {0.0, 0.0};
+        for (int k = l; k <= j; ++k) a += cmul(ps->C[l][k], w[cu][k]);
+        adst[i][l] = a;
       }
-      ps->aX[l] = ax;
-      ps->aZ[l] = az;
-    }
-    if (t == 0) {
-      ps->bX1 = cjj;
-      ps->bZ1 = cmul(xw[j], cjj) - sig * cjj;
-      ps->bZ2 = cjj;
+      if (t == 0)
+        for (int p = 1; p <= i + 1; ++p) bdst[i][p - 1] = bb[cu][p];
+      if (i + 1 < nsn) {
+        for (int k = t; k <= j; k += NTHREADS) {
+          cplx v = {0.0, 0.0};
+          for (int i2 = (k > 0 ? k - 1 : 0); i2 < j; ++i2) v += cmul(ps->H[k][i2], w[cu][i2]);
+          v += cmul(w[cu][j], lw[k]);
+          w[nx][k] = v - sig * w[cu][k];
+        }
+        if (t == 0) {
+          bb[nx][0] = {0.0, 0.0};
+          bb[nx][1] = cmul(w[cu][j], cjj) - sig * bb[cu][1];
+          for (int p = 1; p < 3; ++p) bb[nx][p + 1] = bb[cu][p] - sig * bb[cu][p + 1];
+        }
+      }
+      __syncthreads();
     }
   } else if (t < MMAX) {
-    // T as the reference builds it (alpha_j, j < m-1; norms; T[m-1][m-1] = 0 set by
+    // T as the reference builds it (alpha_j, j < Jn; norms; T[Jn][Jn] = 0 set by
     // k_reduce_final), s[] = 1 so that k_reduce_final's fin is c = Q f(Lambda) Q^T e_1
-    if (t < m - 1) {
+    if (t < Jn) {
       st->Td[t] = ps->H[t][t].re;
       st->To[t] = ps->H[t + 1][t].re;
     }

@@ -272,13 +272,17 @@ if __name__ == "__main__":
 #   b'_{p+1} = b_p - sigma b_{p+1}    (L W_j = C_jj L S_j + lw, lw = -C_jj H[:, :j] D[:j, j]).
 
 
-def sstep_schedule(nstore, p3max=5):
-    """[(J, ns)] of the passes storing S_0..S_{nstore-1}: J = 0 two vectors, three while
-    1 <= J <= p3max and they fit, then two, the last pass one or two."""
+def sstep_schedule(nstore, p3=(2, 5)):
+    """[(J, ns)] of the passes storing S_0..S_{nstore-1}: two vectors per pass, three at
+    the J in p3 (the device: J = 2 and 5, both or neither, when the basis reaches S_8,
+    so the two-vector passes stay at even J), the last pass one or two; p3="all":
+    three wherever they fit (from J = 1)."""
+    use3 = p3 == "all" or nstore - 1 >= 8
     out, J = [], 0
     while J + 1 < nstore:
         left = nstore - 1 - J
-        ns = 3 if (1 <= J <= p3max and left >= 3) else min(2, left)
+        three = (J >= 1 if p3 == "all" else J in p3) and use3 and left >= 3
+        ns = 3 if three else min(2, left)
         out.append((J, ns))
         J += ns
     return out
@@ -343,7 +347,7 @@ def coef_update(C, D, H, sigma, J, ns, g, G):
     return H[J + ns - 1, J + ns - 1].real if ns > 1 else sigma
 
 
-def lanczos_s(apply, u, m, p3max=5, nstore=None, raw=False):
+def lanczos_s(apply, u, m, p3=(2, 5), nstore=None, raw=False):
     """lanczos2 with the s-step schedule (sstep_schedule); same returns."""
     u = np.asarray(u, dtype=np.complex128)
     beta = np.linalg.norm(u)
@@ -355,7 +359,7 @@ def lanczos_s(apply, u, m, p3max=5, nstore=None, raw=False):
     C[0, 0] = D[0, 0] = 1.0
     sigma = np.vdot(S[0], apply(S[0])).real  # the start's alpha pass
     mm = m if nstore is None else nstore
-    for J, ns in sstep_schedule(mm, p3max):
+    for J, ns in sstep_schedule(mm, p3):
         A, B = pass_coefficients(C, D, H, sigma, J, ns)
         Lp = [None, apply(S[J])]
         for p in range(2, ns + 1):
@@ -379,8 +383,8 @@ def lanczos_s(apply, u, m, p3max=5, nstore=None, raw=False):
     return T, S[:m], C[:m, :m], beta, None
 
 
-def krylov_s_tail(apply, u, t, m, func, p3max=5):
-    S, C, H, _, beta = lanczos_s(apply, u, m, p3max, nstore=m - 1, raw=True)
+def krylov_s_tail(apply, u, t, m, func, p3=(2, 5)):
+    S, C, H, _, beta = lanczos_s(apply, u, m, p3, nstore=m - 1, raw=True)
     j = m - 2
     y = apply(S[j])
     a, l2 = np.vdot(S[j], y), np.vdot(y, y).real

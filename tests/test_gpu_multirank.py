@@ -140,7 +140,7 @@ def test_rccl_collective_path_single_rank(monkeypatch, eq):
 
 def _ran_pass2(s, m):
     cnt = s.timing()["update_count"]
-    return cnt[0] > 0 and all(cnt[j] == 0 for j in range(1, m - 1, 2))
+    return cnt[0] > 0 and cnt[1] == 0  # s-step passes start at J = 0, 2, (5,) ... never at 1
 
 
 @pytest.mark.parametrize("nranks,m", [(4, 16), (3, 15), (2, 10)])

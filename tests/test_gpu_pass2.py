@@ -18,11 +18,15 @@ nls_amd = pytest.importorskip("nls_amd")
 TOL_KRYLOV, TOL_TRAJ = 1e-12, 1e-10
 
 
-@pytest.fixture(autouse=True, params=["dma", "reg"])
+@pytest.fixture(autouse=True, params=["dma", "dma3", "reg"])
 def _pass2(monkeypatch, request):
+    """dma: the default two-vector passes (k_p2d); dma3: the s-step schedule with
+    three-vector k_p3d passes at J = 2, 5 from m = 10 (NLS_PASS3=1); reg: the
+    register march (k_pass2r)."""
     monkeypatch.setenv("NLS_PASS2", "1")
     monkeypatch.setenv("NLS_P2_KZ", "8")  # several z chunks per column of tiles
-    monkeypatch.setenv("NLS_P2_IMPL", "2" if request.param == "dma" else "1")
+    monkeypatch.setenv("NLS_P2_IMPL", "1" if request.param == "reg" else "2")
+    monkeypatch.setenv("NLS_PASS3", "1" if request.param == "dma3" else "0")
     return request.param
 
 
@@ -34,10 +38,11 @@ def _eligible(form, nx, ny, m):
 
 
 def _ran_pass2(s, m):
-    """k_pass2 launches are timed at even J only; the plain path times every j."""
+    """s-step pass launches are timed at their start J (0, 2, then even J, or 5 after a
+    three-vector pass at 2); the plain path times every j."""
     t = s.timing()
     cnt = t["update_count"]
-    return cnt[0] > 0 and all(cnt[j] == 0 for j in range(1, m - 1, 2))
+    return cnt[0] > 0 and cnt[1] == 0  # s-step passes start at J = 0, 2, (5,) ... never at 1
 
 
 @pytest.mark.parametrize("nx,ny,nz,m", [(64, 16, 12, 16), (64, 32, 20, 10), (128, 16, 9, 15),
@@ -58,6 +63,9 @@ def test_pass2_trajectory_matches_oracle(_pass2, nx, ny, nz, m, eq):
         s.step(dt, nsteps)
         u = s.get_field()
         assert _ran_pass2(s, m) == _eligible(_pass2, nx, ny, m)
+        cnt = s.timing()["update_count"]
+        three = _pass2 == "dma3" and ny % 4 == 0 and 10 <= m <= 18
+        assert (cnt[5] > 0 and cnt[4] == 0) == three  # k_p3d at J = 2 and 5
     assert np.all(np.isfinite(u))
     assert rel_l2(u, ref) <= TOL_TRAJ
 

@@ -72,16 +72,21 @@ def test_g2_anisotropic_operator():
 def test_sstep_schedule():
     assert sm.sstep_schedule(15) == [(0, 2), (2, 3), (5, 3), (8, 2), (10, 2), (12, 2)]
     assert sm.sstep_schedule(9) == [(0, 2), (2, 3), (5, 3)]
+    assert sm.sstep_schedule(8) == [(0, 2), (2, 2), (4, 2), (6, 1)]
     assert sm.sstep_schedule(4) == [(0, 2), (2, 1)]
+    assert sm.sstep_schedule(9, "all") == [(0, 2), (2, 3), (5, 3)]
+    assert sm.sstep_schedule(8, "all") == [(0, 2), (2, 3), (5, 2)]
     assert sm.sstep_schedule(2) == [(0, 1)]
     for n in range(2, 33):  # every schedule stores exactly S_0..S_{n-1}
         s = sm.sstep_schedule(n)
         assert sum(ns for _, ns in s) == n - 1 and all(J + ns <= n - 1 for J, ns in s)
+        # device rule: three-vector passes at J = 2, 5 only, two-vector ones at even J
+        assert all((J in (2, 5)) if ns == 3 else J % 2 == 0 for J, ns in s)
 
 
-@pytest.mark.parametrize("n,dx,m,p3max", [(16, 20 / 511, 16, 5), (12, 20 / 511, 10, 5), (12, 0.5, 16, 5),
-                                          (12, 20 / 511, 25, 99), (12, 20 / 1023, 16, 99)])
-def test_three_vector_passes_match_oracle(n, dx, m, p3max):
+@pytest.mark.parametrize("n,dx,m,p3", [(16, 20 / 511, 16, (2, 5)), (12, 20 / 511, 10, (2, 5)), (12, 0.5, 16, (2, 5)),
+                                       (12, 20 / 511, 25, "all"), (12, 20 / 1023, 16, "all")])
+def test_three_vector_passes_match_oracle(n, dx, m, p3):
     """Three new vectors per pass (radius-3 stencil of S_J) at the headline stiffness:
     the fused-tail result equals the MGS oracle's Krylov action."""
     rng = np.random.default_rng(5)
@@ -90,5 +95,5 @@ def test_three_vector_passes_match_oracle(n, dx, m, p3max):
     Z, Y, X = np.meshgrid(x, x, x, indexing="ij")
     u = (np.exp(-4 * (X * X + Y * Y + Z * Z)) * (1 + 0.2j) + 1e-3 * rng.standard_normal(X.shape)).ravel()
     ref = np_ref.krylov(ap, u, -1e-3j, m, np_ref.F_EXP_ABS)
-    got, _ = sm.krylov_s_tail(ap, u, -1e-3j, m, np_ref.F_EXP_ABS, p3max=p3max)
+    got, _ = sm.krylov_s_tail(ap, u, -1e-3j, m, np_ref.F_EXP_ABS, p3=p3)
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) <= 1e-12

@@ -27,18 +27,15 @@ with nls_amd.Solver(3, n, n, n, dx, dx, m=m) as s:
     s.step(1e-3, steps)
     t = s.timing()
 tot = 0.0
-p2 = os.environ.get("NLS_PASS2", "1") != "0"
-for J in range(m):
-    c = t["update_count"][J]
-    if not c:
-        continue
+uc = t["update_count"]
+p2 = os.environ.get("NLS_PASS2", "1") != "0" and uc[1] == 0
+Js = [j for j in range(m - 1) if uc[j]]
+for i, J in enumerate(Js):
+    c = uc[J]
     ms = t["update_ms"][J] / c
     tot += t["update_ms"][J] / steps
-    if p2:
-        hz = J + 2 < m - 1
-        vec = J + 1 + (2 if hz else 1)
-    else:
-        vec = J + 2
+    ns = ((Js[i + 1] if i + 1 < len(Js) else m - 2) - J) if p2 else 1
+    vec = J + 1 + ns
     gbs = vec * 16 * cells / (ms * 1e-3) / 1e9
-    print(f"J={J:2d} {ms:7.3f} ms  {vec:2d} vectors  {gbs:7.0f} GB/s")
+    print(f"J={J:2d} ns={ns} {ms:7.3f} ms  {vec:2d} vectors  {gbs:7.0f} GB/s")
 print("update per step", round(tot, 3), "ms;", {k: round(v / steps, 3) for k, v in t["class_ms"].items()})
