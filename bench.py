@@ -453,8 +453,13 @@ def main():
     p2_ms = pass_ms.get(p2J, 0.0)
     tail_ms = tm["class_ms"]["final"] / fcnt if fcnt else 0.0
     own_bytes = None
-    if pass2:  # alpha_0 + sum over passes (J+1 reads + ns writes) + the tail's alpha + tail (m+1)
-        own_bytes = esz * (1 + sum(j + 1 + ns for j, ns in sched) + 1 + (m + 1))
+    # the NLSE tail writes u = N(y) only on the last step of an nls_step call (the
+    # others write just the next start vector): one call per run() for the G1 NLSE
+    multi = w["eq"] in (0, 1) and not w.get("sewi")
+    u_frac = (1.0 / args.steps) if multi else 1.0           # timed region
+    u_frac_prof = (1.0 / max(1, args.prof_steps)) if multi else 1.0  # timing pass
+    if pass2:  # alpha_0 + sum over passes (J+1 reads + ns writes) + the tail's alpha + tail (m + u)
+        own_bytes = esz * (1 + sum(j + 1 + ns for j, ns in sched) + 1 + (m + u_frac))
     if pass2 and p2_ms > tail_ms:
         J = p2J
         cnt = ucnt[J]
@@ -467,9 +472,9 @@ def main():
         J = m - 2
         cnt = fcnt
         avg_ms = tm["class_ms"]["final"] / fcnt
-        bytes_launch = ((m + 1) * esz + (8 if w["eq"] == 3 else 0)) * n_local
+        bytes_launch = ((m + u_frac_prof) * esz + (8 if w["eq"] == 3 else 0)) * n_local
         kname = f"k_tail<NLSE, M={m}> (fused tail: stencil + last Lanczos vector + combination " \
-                f"+ N(1/2) x2, {m - 1} reads + 2 writes)"
+                f"+ N(1/2) x2, {m - 1} reads + the next start vector + u on a call's last step)"
         kprefix = "k_tail<"
     else:  # the largest update pass that ran (m-3 where the basis ends in a fused tail)
         J = max([j for j, c in enumerate(tm["update_count"]) if c] or [0])

@@ -164,6 +164,7 @@ struct nls_handle {
   // hipGraph replay of steady-state steps (single-rank handles): one graph
   // launch per step instead of ~3m kernel launches; keyed by dt
   bool use_graph = false;
+  bool skip_u = false;         // the next NLSE tail may skip its u store (another step follows)
   hipGraphExec_t gexec = nullptr;
   double gdt = 0.0;
 };
@@ -1380,7 +1381,9 @@ void ss2_step(nls_handle *h, double dt) {
   int nl = h->nonlin;
   if (tail) {
     TailArgs ta = tail_args(h, 0);
-    ta.u = h->u;
+    // u = N(y) only where a caller can see it: a step followed by another step of
+    // the same nls_step call needs just the next start vector N(N(y)) (W_0)
+    ta.u = h->skip_u ? nullptr : h->u;
     ta.dt = dt;
     tail_launch(h, TAIL_NLSE, ta);
   } else {
@@ -1597,7 +1600,9 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
         finish_step_flags(h, dt);
         h->tacc.graph_steps += 1;
       } else {
+        h->skip_u = s + 1 < nsteps;
         issue_step(h, dt);
+        h->skip_u = false;
       }
       h->tacc.steps += 1;
       if (ra > 0) {

@@ -697,7 +697,7 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
       if constexpr (MODE == TAIL_NLSE) {
         const double mv = ta.nonlin >= 2 ? ta.mf[q] : 0.0;
         const cplx un = nl_half(to_c(y[0]), mv, ta.dt, ta.nonlin, ta.s1, ta.s2);
-        st_nt(static_cast<cplx *>(ta.u) + q, un);
+        if (ta.u) st_nt(static_cast<cplx *>(ta.u) + q, un);  // NULL: another step follows
         st_nt(reinterpret_cast<cplx *>(W) + q, nl_half(un, mv, ta.dt, ta.nonlin, ta.s1, ta.s2));
       } else if constexpr (MODE == TAIL_SG_MID) {
         double *__restrict__ up = static_cast<double *>(ta.up);

@@ -6,10 +6,12 @@ a wide coalesced streaming read on gfx950, so read bytes = 2 * FETCH_SIZE * 1024
 WRITE_SIZE is exact for 16-B-per-lane streaming stores.  FETCH_SIZE and WRITE_SIZE
 are collected in separate passes (tools/pmc_run.sh).
 
-usage: tools/pmc_summary.py <pmc_dir> <workload> <m> <cells> [out.json] [dominant-kernel-prefix]
+usage: tools/pmc_summary.py <pmc_dir> <workload> <m> <cells> [out.json] [dominant-kernel-prefix] [u_share]
 The dominant kernel is the one bench.py's roofline names (its "kernel" field):
 k_tail<..., m, ...> or, with the two-vector passes, k_p2d<J, ...>; pass its
-prefix (e.g. "k_p2d<12") to pick a pass, else the fused tail is taken.
+prefix (e.g. "k_p2d<12") to pick a pass, else the fused tail is taken.  u_share:
+the fraction of the NLSE tail launches that also wrote u (only the last step of an
+nls_step call does; tools/profile_round.sh's PMC runs: 2 of 7), default 1.
 """
 import collections
 import csv
@@ -50,7 +52,7 @@ def main():
         kernels[name] = e
     # dominant kernel: the fused final pass when the step has one, else k_update<m-2>;
     # a k_p2d<J> pass when asked for
-    want = sys.argv[6] if len(sys.argv) > 6 else None
+    want = sys.argv[6] if len(sys.argv) > 6 and sys.argv[6] not in ("", "-") else None
     dom, alg = None, None
     if want and want.startswith("k_p2d<"):
         J = int(re.search(r"k_p2d<(\d+)", want).group(1))
@@ -59,7 +61,7 @@ def main():
         alg = (J + 1 + (2 if hz else 1)) * esz * cells
     if dom is None:
         dom = next((k for k in kernels if re.fullmatch(rf"k_tail<(nls::)?cplx, [23], {m}, (true|false), 0>", k)), None)
-        alg = (m + 1) * esz * cells
+        alg = (m + (float(sys.argv[7]) if len(sys.argv) > 7 else 1.0)) * esz * cells
     if dom is None:
         dom = next((k for k in kernels if re.fullmatch(rf"k_update<[^,]*, [23], {J}(, (true|false))?>", k)), None)
         alg = (J + 2) * esz * cells
