@@ -115,6 +115,7 @@ struct nls_handle {
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
   int p2impl = 2;              // 2: LDS-DMA k_p2d; 1: register-march k_pass2r (NLS_P2_IMPL)
+  bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
   bool p3 = false;             // three-vector passes k_p3d at J = 2, 5 (single rank, k_p2d; NLS_PASS3=1)
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
@@ -626,8 +627,23 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
 // tiles of one two-vector launch over local planes [qa, qb) with tile depth kz:
 // k_p2d one workgroup per 64 x 4-row tile column chunk; k_pass2r one wave per
 // 60 x rb output column chunk, 4 waves per workgroup
+// The geometry k_p2d marches: the handle's, or for a 2D grid planes of 4 rows
+// (nyp = 4, npl = ny/4, P = 4 nx; single rank), whose row wrap is the 2D y neighbour
+Geo p2_geo(const nls_handle *h) {
+  Geo g = h->geo;
+  if (h->p2_d2) {
+    g.nyp = P2D_ROWS;
+    g.npl = h->geo.npl / P2D_ROWS;
+    g.P = P2D_ROWS * h->geo.nx;
+    g.nzl = g.npl;
+    g.z0 = 0;
+    g.qa = 0;
+    g.qb = (int32_t)g.npl;
+  }
+  return g;
+}
 int p2_tiles(const nls_handle *h, int J, int64_t qa, int64_t qb, int64_t kz) {
-  const Geo &g = h->geo;
+  const Geo g = p2_geo(h);
   const int64_t nzc = (qb - qa + kz - 1) / kz;
   if (h->p2impl == 2)
     return (int)(((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * (g.nyp / P2D_ROWS) * nzc);
@@ -640,7 +656,7 @@ int p2_tiles(const nls_handle *h, int J, int64_t qa, int64_t qb, int64_t kz) {
 // halo exchange of the new stencil vector) and the interior (compute stream).
 bool p2_split(const nls_handle *h) { return h->collective && h->geo.nzl >= 8 && h->p2impl == 2; }
 int p2_grid(const nls_handle *h, int J) {
-  const int64_t nzl = h->geo.nzl;
+  const int64_t nzl = p2_geo(h).nzl;
   if (!p2_split(h)) return p2_tiles(h, J, 0, nzl, h->p2kz);
   return 2 * p2_tiles(h, J, 0, 2, 2) + p2_tiles(h, J, 2, nzl - 2, h->p2kz);
 }
@@ -689,7 +705,7 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
   h->p2_warm = true;
   void *W = vec_ptr(h, 0, 0);
   int64_t vs = h->vs;
-  Geo g = h->geo;
+  Geo g = p2_geo(h);
   g.kz = h->p2kz;
   cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(h->p2) + p2state_sums_offset());
   const bool split = p2_split(h);
@@ -697,7 +713,7 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
     int J = sched[si].first, ns = sched[si].second;
     const int out = J + ns;  // the pass's last vector: the next stencil vector
     int nb = p2_grid(h, J);
-    const void *fn = ns == 3 ? kernel_pass3(J) : kernel_pass2(J, ns == 2, h->p2impl);
+    const void *fn = ns == 3 ? kernel_pass3(J) : kernel_pass2(J, ns == 2, h->p2impl, h->p2_d2);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
     if (!split) {
       int poff = 0;
@@ -842,34 +858,41 @@ void alloc_all(nls_handle *h) {
   const int dim = h->cfg.dim;
   const bool ani = h->ani;
   // two-vectors-per-pass Lanczos: stores S_0..S_{m-2}, ends in the fused tail.
-  // Default on for the 3D isotropic NLSE on one rank (k_p2d: 4-row tiles, m <= 18);
+  // Default on for the isotropic NLSE: 3D (k_p2d: 4-row tiles, m <= 18; also on
+  // slabs) and 2D on one rank (ny % 4 == 0, planes of 4 rows);
   // NLS_PASS2=0/1 forces it off / on where a pass form exists.
   h->pass2 = false;
   if (const char *e = std::getenv("NLS_P2_IMPL")) h->p2impl = std::atoi(e) == 1 ? 1 : 2;
   {
     const char *e = std::getenv("NLS_PASS2");
     const bool want = e ? std::atoi(e) != 0 : true;
+    // 2D (one rank): k_p2d on planes of 4 rows (p2_geo), ny % 4 == 0
+    const bool d2 = dim == 2 && !h->collective && g.npl % P2D_ROWS == 0 && g.npl >= 2 * P2D_ROWS;
     // multi-rank: slabs of >= 4 planes (two-plane halos)
-    const bool base = c && !ani && dim == 3 && (!h->collective || g.nzl >= 4) && h->nbasis == 1 &&
+    const bool base = c && !ani && (dim == 3 || d2) && (!h->collective || g.nzl >= 4) && h->nbasis == 1 &&
                       h->m >= 3 && g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
-    // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS; k_pass2r: 64-aligned x
-    const bool dma = g.nyp % P2D_ROWS == 0 && g.nyp >= 4 && h->m - 4 <= P2D_MAXJ;
-    if (h->p2impl == 2 && !dma) h->p2impl = e ? 1 : 0;  // the register march only on request
+    // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS; k_pass2r (3D): 64-aligned x
+    const bool dma = (dim == 3 ? g.nyp % P2D_ROWS == 0 && g.nyp >= 4 : d2) && h->m - 4 <= P2D_MAXJ;
+    if (h->p2impl == 2 && !dma) h->p2impl = (e && dim == 3) ? 1 : 0;  // the register march only on request
     h->pass2 = want && base &&
-               (h->p2impl == 2 || (h->p2impl == 1 && !h->collective && g.nx % 64 == 0 && g.nyp % 2 == 0));
+               (h->p2impl == 2 ||
+                (h->p2impl == 1 && dim == 3 && !h->collective && g.nx % 64 == 0 && g.nyp % 2 == 0));
+    h->p2_d2 = h->pass2 && dim == 2;
   }
   if (h->pass2) {
     // z depth of a k_p2d tile: deep (the prologue is not overlapped), but at least
     // ~2048 tiles so that every CU gets several (256 at 512^3, 32 at 256^3)
-    const int64_t cols = ((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * std::max<int64_t>(1, g.nyp / P2D_ROWS);
+    const Geo gm = p2_geo(h);
+    const int64_t cols = ((gm.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * std::max<int64_t>(1, gm.nyp / P2D_ROWS);
     const int64_t nzc = std::max<int64_t>(1, (2048 + cols - 1) / cols);
-    h->p2kz = (int)std::max<int64_t>(16, std::min<int64_t>(256, (g.npl + nzc - 1) / nzc));
+    h->p2kz = (int)std::max<int64_t>(16, std::min<int64_t>(256, (gm.npl + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("NLS_P2_BLIND")) h->p2_blind = std::atoi(e) != 0;
     // three-vector passes: parity-green but slower than the two-vector schedule at
     // 512^3 (k_p3d issue-bound at one wave per SIMD), so opt-in
     h->p3 = false;
-    if (const char *e = std::getenv("NLS_PASS3")) h->p3 = h->p2impl == 2 && !h->collective && std::atoi(e) != 0;
+    if (const char *e = std::getenv("NLS_PASS3"))
+      h->p3 = h->p2impl == 2 && !h->collective && !h->p2_d2 && std::atoi(e) != 0;
     h->p2grid = 0;
     for (int J = 0; J + 1 < h->m - 1; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
     hip_check(h, hipMalloc(&h->p2, p2state_bytes()), "hipMalloc(p2)");

@@ -821,17 +821,22 @@ const void *kernel_sg_end(int M) {
 }
 
 // two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp): even J only.
-// impl 2: LDS-DMA form k_p2d (J <= P2D_JMAX); 1: register-march k_pass2r
-const void *kernel_pass2(int J, bool hz, int impl) {
+// impl 2: LDS-DMA form k_p2d (J <= P2D_JMAX; d2: a 2D grid as planes of 4 rows);
+// 1: register-march k_pass2r (3D)
+const void *kernel_pass2(int J, bool hz, int impl, bool d2) {
   if (impl == 2) {
     switch (J) {
-#define X(J) \
-  case J: return hz ? reinterpret_cast<const void *>(&k_p2d<J, true>) : reinterpret_cast<const void *>(&k_p2d<J, false>);
+#define X(J)                                                                                       \
+  case J:                                                                                          \
+    return d2 ? (hz ? reinterpret_cast<const void *>(&k_p2d<J, true, true>)                        \
+                    : reinterpret_cast<const void *>(&k_p2d<J, false, true>))                      \
+              : (hz ? reinterpret_cast<const void *>(&k_p2d<J, true>) : reinterpret_cast<const void *>(&k_p2d<J, false>));
       X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14)
 #undef X
       default: return nullptr;
     }
   }
+  if (d2) return nullptr;
   switch (J) {
 #define X(J) \
   case J: return hz ? reinterpret_cast<const void *>(&k_pass2r<J, true>) : reinterpret_cast<const void *>(&k_pass2r<J, false>);

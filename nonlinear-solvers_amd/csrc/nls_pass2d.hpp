@@ -183,7 +183,10 @@ __device__ __forceinline__ void raw_barrier() {
 // Output planes [g.qa, g.qb) of the slab (multi-rank handles launch the two
 // boundary plane pairs apart from the interior, so the halo exchange overlaps);
 // partial sums at part[c * nb + poff + blockIdx.x].
-template <int J, bool HZ>
+// D2: a 2D [ny][nx] grid seen as planes of 4 rows (g: nyp = 4, npl = ny/4, P = 4 nx):
+// the row-wrap of the 3D march is then exactly the 2D y neighbour, the plane
+// neighbours (2D rows +-4) are dropped, and the boundary rows are 2D rows 0, ny-1.
+template <int J, bool HZ, bool D2 = false>
 __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
                                                               const P2State *__restrict__ ps,
                                                               cplx *__restrict__ part, int nb,
@@ -252,8 +255,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   // stack, and every scratch access is a VMEM op that breaks the vmcnt counting)
 #define P2D_PLANE(p, yy) (z0 + ((yy) < 0 ? (p) - 1 : ((yy) >= ny ? (p) + 1 : (p))))  // global
 #define P2D_ROW(yy) ((yy) < 0 ? (yy) + ny : ((yy) >= ny ? (yy) - ny : (yy)))
-#define P2D_DIAG(xx, j, kk) \
-  ((((xx) == 0) | ((xx) == nx - 1) | ((j) == 0) | ((j) == ny - 1) | ((kk) == 0) | ((kk) == nz - 1)) ? sdb : sdi)
+#define P2D_DIAG(xx, j, kk)                                                                \
+  (D2 ? ((((xx) == 0) | ((xx) == nx - 1) | (((kk) == 0) & ((j) == 0)) | (((kk) == nz - 1) & ((j) == ny - 1))) ? sdb : sdi) \
+      : ((((xx) == 0) | ((xx) == nx - 1) | ((j) == 0) | ((j) == ny - 1) | ((kk) == 0) | ((kk) == nz - 1)) ? sdb : sdi))
   // DMA this wave's two S_J rows of plane p into ring slot sl: the 64 aligned
   // cells and the 4 halo cells (the zero row outside the grid and past the
   // tile's last needed plane)
@@ -302,7 +306,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
     const cplx xm_ = xx_ > 0 ? Sc_[(mi_)] : cplx{0.0, 0.0};                             \
     const cplx xp_ = xx_ + 1 < nx ? Sc_[(pi_)] : cplx{0.0, 0.0};                        \
     const cplx ym_ = Sc_[(ci) - RW], yp_ = Sc_[(ci) + RW];                              \
-    const cplx zm_ = Sm_[(ci)], zp_ = Sp_[(ci)];                                        \
+    const cplx zm_ = D2 ? cplx{0.0, 0.0} : Sm_[(ci)], zp_ = D2 ? cplx{0.0, 0.0} : Sp_[(ci)]; \
     const double dg_ = P2D_DIAG(xx_, P2D_ROW(yy_), kk_);                                \
     const bool ok_ = xx_ >= 0 && xx_ < nx && kk_ >= 0 && kk_ < nz;                      \
     const cplx v_ = dg_ * c_ + s * (((zm_ + zp_) + (xm_ + xp_)) + (ym_ + yp_));         \
@@ -396,7 +400,8 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
       if (lane == 0) xm = le1;
       if (lane == 63) xp = er;
       const cplx ym = Lr[(lsl * P2D_LR + w) * 64 + lane], yp = Lr[(lsl * P2D_LR + w + 2) * 64 + lane];
-      const cplx l2 = P2D_DIAG(x, y, z0 + k) * l1 + s * (((lq0 + ln) + (xm + xp)) + (ym + yp));
+      const cplx zz = D2 ? cplx{0.0, 0.0} : lq0 + ln;
+      const cplx l2 = P2D_DIAG(x, y, z0 + k) * l1 + s * ((zz + (xm + xp)) + (ym + yp));
       cplx Za = cmul(bZ2, l2) + cmul(bZ1, l1), Zb = {0.0, 0.0};
 #pragma unroll
       for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, cZ[l], sv[l]);

@@ -180,3 +180,19 @@ def test_folded_alpha_nlse_matches_oracle(dim, nx, ny, nz):
                      lambda: _run(dim, nx, ny, nz, dx, u0, dt, steps, m, nls_amd.NLSE_CUBIC, True))
     ref = O.nlse_steps(O.grid(dim, nx, ny, nz, dx, dx), u0, dt, steps, m)
     assert rel_l2(a, ref) <= 1e-10
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz", [(2, 70, 67, 1), (3, 21, 19, 17)])
+def test_multi_step_call_equals_single_steps(dim, nx, ny, nz):
+    """One-vector path: the fused tail's u store only on a call's last step changes no
+    bit of the trajectory (5-step call vs 1-step calls)."""
+    dx = 0.4
+    u0 = _field(nx * ny * nz, 4)
+    out = []
+    for calls in ((5,), (1, 1, 1, 1, 1)):
+        with nls_amd.Solver(dim, nx, ny, nz, dx, dx, m=12) as s:
+            s.set_field(u0)
+            for k in calls:
+                s.step(1e-3, k)
+            out.append(s.get_field())
+    assert np.array_equal(out[0], out[1])

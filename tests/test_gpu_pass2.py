@@ -83,3 +83,72 @@ def test_pass2_one_step_matches_plain_path(monkeypatch, L):
             s.step(1e-3, 1)
             out[mode] = s.get_field()
     assert rel_l2(out["1"], out["0"]) <= 1e-12
+
+
+@pytest.mark.parametrize("eq", [0, 1])
+def test_multi_step_call_equals_single_steps(_pass2, eq):
+    """The NLSE tail writes u only on the last step of an nls_step call (the other steps
+    write just the next start vector): one 5-step call equals five 1-step calls bitwise."""
+    if _pass2 != "dma":
+        pytest.skip("one form is enough")
+    nx, ny, nz, m = 64, 16, 12, 16
+    dx = spacing(nx, 10.0)
+    u0 = soliton_field(3, nx, ny, nz, 10.0, seed=3)
+    out = []
+    for calls in ((5,), (1, 1, 1, 1, 1), (2, 3)):
+        with nls_amd.Solver(3, nx, ny, nz, dx, dx, equation=eq, m=m) as s:
+            s.set_field(u0)
+            for k in calls:
+                s.step(1e-3, k)
+            out.append(s.get_field())
+    assert np.array_equal(out[0], out[1]) and np.array_equal(out[0], out[2])
+
+
+# ---- 2D: k_p2d on planes of 4 rows (nls_api.cpp p2_geo; one rank, ny % 4 == 0) ----
+
+
+def _eligible2d(form, ny, m):
+    return form != "reg" and ny % 4 == 0 and ny >= 8 and m <= 18
+
+
+@pytest.mark.parametrize("nx,ny,m", [(64, 64, 16), (300, 20, 10), (50, 12, 16), (130, 8, 5), (70, 66, 16),
+                                     (64, 40, 3), (96, 36, 17)])
+@pytest.mark.parametrize("eq", [0, 1])
+def test_pass2_2d_trajectory_matches_oracle(_pass2, nx, ny, m, eq):
+    """The 2D row neighbours are the march's row wrap across planes of 4 rows; the plane
+    neighbours are dropped; boundary rows are 2D rows 0 and ny-1 (x edges as in 3D)."""
+    L = 10.0
+    dx = spacing(nx, L)
+    dy = spacing(ny, L)
+    u0 = soliton_field(2, nx, ny, 1, L, seed=12)
+    u0 = u0 / np.sqrt(np.sum(np.abs(u0) ** 2) * dx * dy)
+    g = O.grid(2, nx, ny, 1, dx, dy)
+    dt, nsteps = 1e-3, 10
+    ref = O.nlse_steps(g, u0, dt, nsteps, m, nonlin=eq)
+    with nls_amd.Solver(2, nx, ny, 1, dx, dy, equation=eq, m=m) as s:
+        s.set_field(u0)
+        s.set_timing(True)
+        s.step(dt, nsteps)
+        u = s.get_field()
+        if m > 3:  # at m = 3 both paths launch one update at J = 0: not telling
+            assert _ran_pass2(s, m) == _eligible2d(_pass2, ny, m)
+    assert np.all(np.isfinite(u))
+    assert rel_l2(u, ref) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("n", [256, 512])
+def test_pass2_2d_stiff_matches_oracle(_pass2, n):
+    """C2's spacing (dx = 20/4095, ||L|| dt ~ 1.7e2) on a grid the oracle runs in seconds."""
+    if _pass2 == "reg":
+        pytest.skip("2D has the LDS-DMA form only")
+    dx = 20.0 / 4095
+    u0 = soliton_field(2, n, n, 1, n * dx / 2, seed=13)
+    g = O.grid(2, n, n, 1, dx, dx)
+    ref = O.nlse_steps(g, u0, 1e-3, 6, 16)
+    with nls_amd.Solver(2, n, n, 1, dx, dx, m=16) as s:
+        s.set_field(u0)
+        s.set_timing(True)
+        s.step(1e-3, 6)
+        u = s.get_field()
+        assert _ran_pass2(s, 16)
+    assert rel_l2(u, ref) <= TOL_TRAJ

@@ -1,0 +1,9 @@
+# 2D two-vector passes: parity tests, then the 2D 4096^2 bench (both paths)
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_gpu_pass2.py tests/test_gpu_fused.py -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/t_2d.log 2>&1; rc=$?
+tail -3 gpurun_out/t_2d.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --workload nlse2d_4096 --no-cpu-baseline > gpurun_out/b2d_p2.json 2>&1 || exit 1
+NLS_PASS2=0 timeout -k 10 300 python bench.py --workload nlse2d_4096 --no-cpu-baseline > gpurun_out/b2d_p1.json 2>&1 || exit 1
+for f in gpurun_out/b2d_p2.json gpurun_out/b2d_p1.json; do python3 -c "import json;d=json.load(open('$f'));print('$f',round(d['value'],1),round(d['ms_per_step'],3),d['roofline']['kernel'][:24],round(d['roofline']['avg_launch_ms'],3),round(d['roofline']['frac'],3),{k:round(v,3) for k,v in d['step_roofline']['gpu_kernel_ms_per_step'].items()})"; done
