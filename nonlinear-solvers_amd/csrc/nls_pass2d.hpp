@@ -61,6 +61,9 @@ constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
 // Workgroups per CU: two where the registers (<= 256 per lane) and the rings
 // (<= 80 KiB) allow, so the second workgroup's waves cover the first's barriers
 // and LDS latencies; one for the long passes.
+#ifndef NLS_P2D_DS2_MAXJ
+#define NLS_P2D_DS2_MAXJ 0  // two workgroups per CU: two planes of S look-ahead up to this J, then one (J = 2: NP 4, 2.10 vs 2.14 ms)
+#endif
 #ifndef NLS_P2D_DS3_MAXJ
 #define NLS_P2D_DS3_MAXJ 4  // one workgroup per CU: three planes of S look-ahead up to this J, then one (J = 6: 3.78 vs 3.90 ms, NP 4 vs 3)
 #endif
@@ -73,7 +76,7 @@ __host__ __device__ constexpr int p2d_occ(int J) { return J == 0 ? NLS_P2D_OCC0 
 // before its own wait and barrier
 __host__ __device__ constexpr int p2d_ds(int J) {
   return p2d_occ(J) >= 3 ? 1
-                          : (p2d_occ(J) == 2 ? (J == 0 ? 3 : (J <= 2 ? 2 : 1))
+                          : (p2d_occ(J) == 2 ? (J == 0 ? 3 : (J <= NLS_P2D_DS2_MAXJ ? 2 : 1))
                                              : (J == 0 ? 6 : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J <= 12 || !NLS_P2D_EARLY ? 1 : 0))));
 }
 // early issue only at one workgroup per CU (two: the other workgroup covers the wait,
