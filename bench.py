@@ -460,7 +460,9 @@ def main():
     u_frac_prof = (1.0 / max(1, args.prof_steps)) if multi else 1.0  # timing pass
     if pass2:  # alpha_0 + sum over passes (J+1 reads + ns writes) + the tail's alpha + tail (m + u)
         own_bytes = esz * (1 + sum(j + 1 + ns for j, ns in sched) + 1 + (m + u_frac))
-    if pass2 and p2_ms > tail_ms:
+    # (the real Gautschi tails are not modelled here: with two-vector passes the
+    # largest pass is reported for them)
+    if pass2 and (p2_ms > tail_ms or w["eq"] not in (0, 1, 3)):
         J = p2J
         cnt = ucnt[J]
         avg_ms = p2_ms

@@ -119,7 +119,8 @@ struct nls_handle {
   bool p3 = false;             // three-vector passes k_p3d at J = 2, 5 (single rank, k_p2d; NLS_PASS3=1)
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
-  bool p2_warm = false;        // the P2State holds a previous basis' alpha_0
+  bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
+  bool p2_pr = false;          // real field marched as cell pairs by k_p2d (p2_geo)
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
@@ -631,10 +632,14 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
 // (nyp = 4, npl = ny/4, P = 4 nx; single rank), whose row wrap is the 2D y neighbour
 Geo p2_geo(const nls_handle *h) {
   Geo g = h->geo;
+  if (h->p2_pr) {  // pairs of cells along x
+    g.nx = h->geo.nx / 2;
+    g.P = h->geo.P / 2;
+  }
   if (h->p2_d2) {
     g.nyp = P2D_ROWS;
     g.npl = h->geo.npl / P2D_ROWS;
-    g.P = P2D_ROWS * h->geo.nx;
+    g.P = P2D_ROWS * g.nx;
     g.nzl = g.npl;
     g.z0 = 0;
     g.qa = 0;
@@ -683,43 +688,44 @@ std::vector<std::pair<int, int>> p2_schedule(const nls_handle *h, int nstore) {
   return out;
 }
 
-void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
+void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
   const int m = h->m, nstore = m - 1;
-  KState *st = h->B[0].st;
-  void *ps = h->p2;
+  KState *st = h->B[b].st;
+  void *ps = static_cast<char *>(h->p2) + (size_t)b * p2state_bytes();
+  int real = h->p2_pr ? 1 : 0;
   const std::vector<std::pair<int, int>> sched = p2_schedule(h, nstore);
   // blind start once a previous basis left its alpha_0 (the shift of the J = 0
   // pass): no alpha pass over W_0, beta from the pass's own ||S_0||^2
-  const bool blind = h->p2_warm && h->p2_blind && h->p2impl == 2;  // k_p2d<0> reduces ||S_0||^2
+  const bool blind = h->p2_warm[b] && h->p2_blind && h->p2impl == 2;  // k_p2d<0> reduces ||S_0||^2
   if (!blind) {
     Geo ga = h->geo;
     ga.kz = h->kz_alpha;
-    alpha_pass(h, 0, 0, ga);
-    reduce_iter(h, 0, 0);
+    alpha_pass(h, b, 0, ga);
+    reduce_iter(h, b, 0);
   }
   {
     int J = 0, mode = blind ? 2 : 0, ns = 0, nsn = sched[0].second;
-    void *args[] = {&ps, &st, &J, &mode, &ns, &nsn};
+    void *args[] = {&ps, &st, &J, &mode, &ns, &nsn, &real};
     launch(h, 2, 0, kernel_p2coef(), 1, args);
   }
-  h->p2_warm = true;
-  void *W = vec_ptr(h, 0, 0);
-  int64_t vs = h->vs;
+  h->p2_warm[b] = true;
+  void *W = vec_ptr(h, b, 0);
+  int64_t vs = h->p2_pr ? h->vs / 2 : h->vs;  // in the kernel's 16-B cells
   Geo g = p2_geo(h);
   g.kz = h->p2kz;
-  cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(h->p2) + p2state_sums_offset());
+  cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(ps) + p2state_sums_offset());
   const bool split = p2_split(h);
   for (size_t si = 0; si < sched.size(); ++si) {
     int J = sched[si].first, ns = sched[si].second;
     const int out = J + ns;  // the pass's last vector: the next stencil vector
     int nb = p2_grid(h, J);
-    const void *fn = ns == 3 ? kernel_pass3(J) : kernel_pass2(J, ns == 2, h->p2impl, h->p2_d2);
+    const void *fn = ns == 3 ? kernel_pass3(J) : kernel_pass2(J, ns == 2, h->p2impl, h->p2_d2, h->p2_pr);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
     if (!split) {
       int poff = 0;
       void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb, &h->zbuf, &poff};
       launch(h, 1, J, fn, nb, args);
-      if (h->collective) halo_begin(h, 0, out);
+      if (h->collective) halo_begin(h, b, out);
     } else {
       const int64_t nzl = h->geo.nzl;
       const int tb = p2_tiles(h, J, 0, 2, 2);
@@ -735,7 +741,7 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
         launch(h, 1, J, fn, tb, args, h->cstream);
       }
       hip_check(h, hipEventRecord(h->ev_bdone, h->cstream), "hipEventRecord");
-      halo_planes(h, vec_ptr(h, 0, out), (int64_t)h->esize, h->cstream, 2);
+      halo_planes(h, vec_ptr(h, b, out), (int64_t)h->esize, h->cstream, 2);
       hip_check(h, hipEventRecord(h->ev_halo, h->cstream), "hipEventRecord");
       h->halo_pending = true;
       Geo gi = g;
@@ -751,25 +757,25 @@ void run_lanczos2(nls_handle *h, int nf, int f0, int f1, double tr, double ti) {
     int nbA = 0, ncA = 0, ncU = ns * (J + 1) + ns * (ns + 1) / 2 + (J == 0 ? 1 : 0);
     void *cargs[] = {(void *)&pA, &nbA, &ncA, &h->partP2, &nb, &sums};
     launch(h, 2, J, kernel_colsum(), ncU, cargs);
-    if (h->collective) allreduce_sums(h, 0, ncU, sums);
+    if (h->collective) allreduce_sums(h, b, ncU, sums);
     int mode = 1, nsn = si + 1 < sched.size() ? sched[si + 1].second : 0;
-    void *a2[] = {&ps, &st, &J, &mode, &ns, &nsn};
+    void *a2[] = {&ps, &st, &J, &mode, &ns, &nsn, &real};
     launch(h, 2, J, kernel_p2coef(), 1, a2);
   }
   halo_wait(h);
   // the tail's alpha pass over S_{m-2}: a = S^H L S, ||S||^2, ||L S||^2
-  alpha_l2_pass(h, 0, m - 2);
+  alpha_l2_pass(h, b, m - 2);
   {
     const cplx *pU = nullptr;
     int nbA = h->grid_alpha2, ncA = 3, nbU = 0;
     void *cargs[] = {(void *)&h->partA, &nbA, &ncA, (void *)&pU, &nbU, &sums};
     launch(h, 2, m - 2, kernel_colsum(), ncA, cargs);
-    if (h->collective) allreduce_sums(h, 0, ncA, sums);
+    if (h->collective) allreduce_sums(h, b, ncA, sums);
     int mm = m;
     void *a2[] = {&ps, &st, &sums, &mm};
     launch(h, 2, m - 2, kernel_p2tail(), 1, a2);
   }
-  reduce_final(h, 0, nf, f0, f1, tr, ti, 1);
+  reduce_final(h, b, nf, f0, f1, tr, ti, 1);
   int mm = m, nff = nf;
   void *fa[] = {&ps, &st, &mm, &nff};
   launch(h, 2, m, kernel_p2tfin(), 1, fa);
@@ -868,9 +874,13 @@ void alloc_all(nls_handle *h) {
     const bool want = e ? std::atoi(e) != 0 : true;
     // 2D (one rank): k_p2d on planes of 4 rows (p2_geo), ny % 4 == 0
     const bool d2 = dim == 2 && !h->collective && g.npl % P2D_ROWS == 0 && g.npl >= 2 * P2D_ROWS;
+    // real 2D Gautschi (sine-Gordon, G1 and the G2 family; not KG's anisotropic
+    // operator): the field as pairs of cells, nx even
+    const bool pr = !c && !h->kg && !ani && d2 && g.nx % 2 == 0 && g.nx >= 4;
     // multi-rank: slabs of >= 4 planes (two-plane halos)
-    const bool base = c && !ani && (dim == 3 || d2) && (!h->collective || g.nzl >= 4) && h->nbasis == 1 &&
-                      h->m >= 3 && g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
+    const bool base = (c || pr) && !ani && (dim == 3 || d2) && (!h->collective || g.nzl >= 4) &&
+                      (h->nbasis == 1 || pr) && h->m >= 3 &&
+                      g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
     // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS; k_pass2r (3D): 64-aligned x
     const bool dma = (dim == 3 ? g.nyp % P2D_ROWS == 0 && g.nyp >= 4 : d2) && h->m - 4 <= P2D_MAXJ;
     if (h->p2impl == 2 && !dma) h->p2impl = (e && dim == 3) ? 1 : 0;  // the register march only on request
@@ -878,6 +888,7 @@ void alloc_all(nls_handle *h) {
                (h->p2impl == 2 ||
                 (h->p2impl == 1 && dim == 3 && !h->collective && g.nx % 64 == 0 && g.nyp % 2 == 0));
     h->p2_d2 = h->pass2 && dim == 2;
+    h->p2_pr = h->pass2 && !c;
   }
   if (h->pass2) {
     // z depth of a k_p2d tile: deep (the prologue is not overlapped), but at least
@@ -895,8 +906,8 @@ void alloc_all(nls_handle *h) {
       h->p3 = h->p2impl == 2 && !h->collective && !h->p2_d2 && std::atoi(e) != 0;
     h->p2grid = 0;
     for (int J = 0; J + 1 < h->m - 1; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
-    hip_check(h, hipMalloc(&h->p2, p2state_bytes()), "hipMalloc(p2)");
-    hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes(), h->stream), "hipMemset");
+    hip_check(h, hipMalloc(&h->p2, p2state_bytes() * h->nbasis), "hipMalloc(p2)");  // one per basis
+    hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes() * h->nbasis, h->stream), "hipMemset");
     hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)),
               "hipMalloc(partP2)");
     const size_t zb = (size_t)std::max<int64_t>(g.nx, 64) * sizeof(cplx);
@@ -1265,7 +1276,7 @@ int nls_set_field(nls_handle *h, const double *u, uint64_t n) {
       hip_check(h, hipMemcpyAsync(h->u, u, (size_t)n * h->esize, hipMemcpyHostToDevice, h->stream),
                 "hipMemcpy H2D");
       h->w0_ready = false;
-      h->p2_warm = false;  // a new field: the next basis measures alpha_0 again
+      h->p2_warm[0] = h->p2_warm[1] = false;  // a new field: the next basis measures alpha_0 again
     } else {
       copy_in_vector(h, 0, 0, u);
       halo(h, 0, 0);
@@ -1397,7 +1408,7 @@ void ss2_step(nls_handle *h, double dt) {
   // t = -tau (nlse_cubic_quintic_dev.hpp:86)
   const int lf = (h->ani || h->nonlin == 3) ? NLS_F_EXP : NLS_F_EXP_ABS;
   const double ltr = h->ani ? 0.0 : -0.0, lti = h->ani ? dt : -dt;
-  if (h->pass2) run_lanczos2(h, 1, lf, 0, ltr, lti);
+  if (h->pass2) run_lanczos2(h, 0, 1, lf, 0, ltr, lti);
   else run_lanczos(h, 0, 1, lf, 0, ltr, lti, tail);
   void *W = vec_ptr(h, 0, 0);
   KState *st = h->B[0].st;
@@ -1531,8 +1542,9 @@ void issue_step(nls_handle *h, double dt) {
     // G2 Gautschi family (e.g. phi4_single.cuh:33-47): the same sequence with
     // g = -m F(id u) and sinc^2(t sqrt|lambda|) instead of the G1 half argument.
     const int mid = h->gfun >= 0 ? TAIL_GG_MID : TAIL_SG_MID;
-    bool tail = use_tail(h, mid);
-    run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0, tail);
+    bool tail = use_tail(h, mid) || h->pass2;  // the s-step passes always end in the tail
+    if (h->pass2) run_lanczos2(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0);
+    else run_lanczos(h, 0, 2, NLS_F_ID_SQRT, NLS_F_COS_SQRT, dt, 0.0, tail);
     if (tail) {
       TailArgs ta = tail_args(h, 0);
       ta.out = vec_ptr(h, 1, 0);
@@ -1548,8 +1560,9 @@ void issue_step(nls_handle *h, double dt) {
       pw_launch(h, 3, kernel_sg_mid(m), args);
     }
     halo(h, 1, 0);
-    tail = use_tail(h, TAIL_SG_END);
-    run_lanczos(h, 1, 1, h->gfun >= 0 ? NLS_F_SINC2_SQRT : NLS_F_SINC2_HALF, 0, dt, 0.0, tail);
+    tail = use_tail(h, TAIL_SG_END) || h->pass2;
+    if (h->pass2) run_lanczos2(h, 1, 1, h->gfun >= 0 ? NLS_F_SINC2_SQRT : NLS_F_SINC2_HALF, 0, dt, 0.0);
+    else run_lanczos(h, 1, 1, h->gfun >= 0 ? NLS_F_SINC2_SQRT : NLS_F_SINC2_HALF, 0, dt, 0.0, tail);
     if (tail) {
       TailArgs ta = tail_args(h, 1);
       ta.u = vec_ptr(h, 0, 0);

@@ -821,13 +821,17 @@ const void *kernel_sg_end(int M) {
 }
 
 // two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp): even J only.
-// impl 2: LDS-DMA form k_p2d (J <= P2D_JMAX; d2: a 2D grid as planes of 4 rows);
+// impl 2: LDS-DMA form k_p2d (J <= P2D_JMAX; d2: a 2D grid as planes of 4 rows; pr: a
+// real 2D field as pairs of cells);
 // 1: register-march k_pass2r (3D)
-const void *kernel_pass2(int J, bool hz, int impl, bool d2) {
+const void *kernel_pass2(int J, bool hz, int impl, bool d2, bool pr) {
   if (impl == 2) {
     switch (J) {
 #define X(J)                                                                                       \
   case J:                                                                                          \
+    if (pr)                                                                                        \
+      return hz ? reinterpret_cast<const void *>(&k_p2d<J, true, true, true>)                      \
+                : reinterpret_cast<const void *>(&k_p2d<J, false, true, true>);                    \
     return d2 ? (hz ? reinterpret_cast<const void *>(&k_p2d<J, true, true>)                        \
                     : reinterpret_cast<const void *>(&k_p2d<J, false, true>))                      \
               : (hz ? reinterpret_cast<const void *>(&k_p2d<J, true>) : reinterpret_cast<const void *>(&k_p2d<J, false>));
@@ -836,7 +840,7 @@ const void *kernel_pass2(int J, bool hz, int impl, bool d2) {
       default: return nullptr;
     }
   }
-  if (d2) return nullptr;
+  if (d2 || pr) return nullptr;
   switch (J) {
 #define X(J) \
   case J: return hz ? reinterpret_cast<const void *>(&k_pass2r<J, true>) : reinterpret_cast<const void *>(&k_pass2r<J, false>);

@@ -60,7 +60,7 @@ const void *kernel_reduce_final();
 const void *kernel_colsum();
 // two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp; 3D isotropic complex, single rank)
 //   pass2 : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb[, const cplx* zbuf])
-const void *kernel_pass2(int J, bool hz, int impl, bool d2 = false);  // hz: also Z; impl 2: LDS-DMA k_p2d, 1: k_pass2r
+const void *kernel_pass2(int J, bool hz, int impl, bool d2 = false, bool pr = false);  // hz: also Z; impl 2: LDS-DMA k_p2d, 1: k_pass2r
 constexpr int P2D_WAVE_XO = 64, P2D_ROWS = 4, P2D_MAXJ = 14;  // == P2D_XO, P2D_TR, P2D_JMAX
 //   p2tail: (P2State*, KState*, const cplx* sums, int m);  p2tfin: (const P2State*, KState*, int m, int nf)
 const void *kernel_p2tail();

@@ -205,9 +205,10 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2r(cplx *__restrict__ W, int64
 // columns, summed).  Computes the new columns of C, D, H (tests/sstep_model.py
 // coef_update) and, for a next pass of nsn > 0 vectors at J' = J + ns, its
 // coefficients (pass_coefficients); nsn = 0: T into the KState for k_reduce_final
-// (s[] = 1, so fin is in the W basis; k_p2fin converts it).
+// (s[] = 1, so fin is in the W basis; k_p2fin converts it).  real: the sums come
+// from a real field marched as cell pairs; their imaginary parts are dropped.
 __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, KState *__restrict__ st,
-                                                     int J, int mode, int ns, int nsn) {
+                                                     int J, int mode, int ns, int nsn, int real) {
   __shared__ cplx q[3][P2M], sv[P2M], lw[P2M], w[2][P2M];
   __shared__ cplx bb[2][4];
   __shared__ double nu[3];
@@ -245,6 +246,11 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
   } else {
     cplx *sw = ps->sums;
     const int ng = ns * (ns + 1) / 2, og = ns * (J + 1);  // Gram entries, their offset
+    if (real) {
+      // a real field marched as cell pairs (k_p2d PR): the real parts are the dots
+      for (int e = t; e <= og + ng; e += NTHREADS) sw[e].im = 0.0;
+      __syncthreads();
+    }
     // Gram entry (a, b), a <= b
     auto gidx = [ns, og](int a, int b) { return og + a * ns - a * (a - 1) / 2 + (b - a); };
     if (J == 0 && ps->blind) {

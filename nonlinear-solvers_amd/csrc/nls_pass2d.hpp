@@ -189,7 +189,16 @@ __device__ __forceinline__ void raw_barrier() {
 // D2: a 2D [ny][nx] grid seen as planes of 4 rows (g: nyp = 4, npl = ny/4, P = 4 nx):
 // the row-wrap of the 3D march is then exactly the 2D y neighbour, the plane
 // neighbours (2D rows +-4) are dropped, and the boundary rows are 2D rows 0, ny-1.
-template <int J, bool HZ, bool D2 = false>
+// PR: a real field seen as pairs of cells (nx = pairs, one cplx = cells 2x, 2x+1;
+// real coefficients, so every linear combination acts per component and the real
+// part of each complex dot is the real dot): only the x neighbours differ (cell
+// 2x-1 is pair x-1's second, cell 2x+2 pair x+1's first) and the x boundary
+// diagonal applies per cell.
+__device__ __forceinline__ cplx pr_lap(cplx c, cplx xm, cplx xp, cplx yz, double dga, double dgb, double s) {
+  return {dga * c.re + s * (yz.re + (xm.im + c.im)), dgb * c.im + s * (yz.im + (c.re + xp.re))};
+}
+
+template <int J, bool HZ, bool D2 = false, bool PR = false>
 __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
                                                               const P2State *__restrict__ ps,
                                                               cplx *__restrict__ part, int nb,
@@ -258,9 +267,14 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   // stack, and every scratch access is a VMEM op that breaks the vmcnt counting)
 #define P2D_PLANE(p, yy) (z0 + ((yy) < 0 ? (p) - 1 : ((yy) >= ny ? (p) + 1 : (p))))  // global
 #define P2D_ROW(yy) ((yy) < 0 ? (yy) + ny : ((yy) >= ny ? (yy) - ny : (yy)))
-#define P2D_DIAG(xx, j, kk)                                                                \
-  (D2 ? ((((xx) == 0) | ((xx) == nx - 1) | (((kk) == 0) & ((j) == 0)) | (((kk) == nz - 1) & ((j) == ny - 1))) ? sdb : sdi) \
-      : ((((xx) == 0) | ((xx) == nx - 1) | ((j) == 0) | ((j) == ny - 1) | ((kk) == 0) | ((kk) == nz - 1)) ? sdb : sdi))
+// boundary cell in y / z (D2: 2D rows 0 and ny - 1 of the 4-row planes)
+#define P2D_BYZ(j, kk)                                                                     \
+  (D2 ? ((((kk) == 0) & ((j) == 0)) | (((kk) == nz - 1) & ((j) == ny - 1)))                \
+      : (((j) == 0) | ((j) == ny - 1) | ((kk) == 0) | ((kk) == nz - 1)))
+#define P2D_DIAG(xx, j, kk) ((((xx) == 0) | ((xx) == nx - 1) | P2D_BYZ(j, kk)) ? sdb : sdi)
+// PR: the diagonals of the pair's first / second cell
+#define P2D_DIAGA(xx, j, kk) ((((xx) == 0) | P2D_BYZ(j, kk)) ? sdb : sdi)
+#define P2D_DIAGB(xx, j, kk) ((((xx) == nx - 1) | P2D_BYZ(j, kk)) ? sdb : sdi)
   // DMA this wave's two S_J rows of plane p into ring slot sl: the 64 aligned
   // cells and the 4 halo cells (the zero row outside the grid and past the
   // tile's last needed plane)
@@ -310,9 +324,16 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
     const cplx xp_ = xx_ + 1 < nx ? Sc_[(pi_)] : cplx{0.0, 0.0};                        \
     const cplx ym_ = Sc_[(ci) - RW], yp_ = Sc_[(ci) + RW];                              \
     const cplx zm_ = D2 ? cplx{0.0, 0.0} : Sm_[(ci)], zp_ = D2 ? cplx{0.0, 0.0} : Sp_[(ci)]; \
-    const double dg_ = P2D_DIAG(xx_, P2D_ROW(yy_), kk_);                                \
     const bool ok_ = xx_ >= 0 && xx_ < nx && kk_ >= 0 && kk_ < nz;                      \
-    const cplx v_ = dg_ * c_ + s * (((zm_ + zp_) + (xm_ + xp_)) + (ym_ + yp_));         \
+    cplx v_;                                                                            \
+    if constexpr (PR) {                                                                 \
+      const int jj_ = P2D_ROW(yy_);                                                     \
+      v_ = pr_lap(c_, xm_, xp_, (zm_ + zp_) + (ym_ + yp_), P2D_DIAGA(xx_, jj_, kk_),    \
+                  P2D_DIAGB(xx_, jj_, kk_), s);                                         \
+    } else {                                                                            \
+      const double dg_ = P2D_DIAG(xx_, P2D_ROW(yy_), kk_);                              \
+      v_ = dg_ * c_ + s * (((zm_ + zp_) + (xm_ + xp_)) + (ym_ + yp_));                  \
+    }                                                                                   \
     dst = ok_ ? v_ : cplx{0.0, 0.0};                                                    \
   } while (0)
   // per plane a wave computes L S_J of its own row (main lanes, kept in a
@@ -404,7 +425,11 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
       if (lane == 63) xp = er;
       const cplx ym = Lr[(lsl * P2D_LR + w) * 64 + lane], yp = Lr[(lsl * P2D_LR + w + 2) * 64 + lane];
       const cplx zz = D2 ? cplx{0.0, 0.0} : lq0 + ln;
-      const cplx l2 = P2D_DIAG(x, y, z0 + k) * l1 + s * ((zz + (xm + xp)) + (ym + yp));
+      cplx l2;
+      if constexpr (PR)
+        l2 = pr_lap(l1, xm, xp, zz + (ym + yp), P2D_DIAGA(x, y, z0 + k), P2D_DIAGB(x, y, z0 + k), s);
+      else
+        l2 = P2D_DIAG(x, y, z0 + k) * l1 + s * ((zz + (xm + xp)) + (ym + yp));
       cplx Za = cmul(bZ2, l2) + cmul(bZ1, l1), Zb = {0.0, 0.0};
 #pragma unroll
       for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, cZ[l], sv[l]);
@@ -447,6 +472,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
 #undef P2D_PLANE
 #undef P2D_ROW
 #undef P2D_DIAG
+#undef P2D_DIAGA
+#undef P2D_DIAGB
+#undef P2D_BYZ
 #undef P2D_ISSUE_S
 #undef P2D_ISSUE_J
 #undef P2D_LAP

@@ -152,3 +152,82 @@ def test_pass2_2d_stiff_matches_oracle(_pass2, n):
         u = s.get_field()
         assert _ran_pass2(s, 16)
     assert rel_l2(u, ref) <= TOL_TRAJ
+
+
+# ---- real 2D Gautschi (sine-Gordon G1 and the G2 family): k_p2d on cell pairs ----
+
+
+def _eligible_pr(form, nx, ny, m):
+    return form != "reg" and nx % 2 == 0 and nx >= 4 and ny % 4 == 0 and ny >= 8 and m <= 18
+
+
+@pytest.mark.parametrize("nx,ny,m", [(64, 64, 10), (50, 12, 10), (130, 16, 16), (66, 40, 5), (7, 8, 10),
+                                     (30, 22, 10), (96, 36, 3)])
+def test_pass2_sg_trajectory_matches_oracle(_pass2, nx, ny, m):
+    """sg_solver_dev.hpp:168-193: two bases per step (id/cos of u, sinc^2 of g(u)), both
+    by two-vector passes on cell pairs (the x neighbours cross the pair; real dots =
+    the real parts of the pair dots)."""
+    L = 3.0
+    dx, dy = spacing(nx, L), spacing(ny, L)
+    x = np.linspace(-L, L, nx)
+    y = np.linspace(-L, L, ny)
+    Y, X = np.meshgrid(y, x, indexing="ij")
+    rng = np.random.default_rng(21)
+    u0 = (2.0 * np.arctan(np.exp(3.0 - 5.0 * np.sqrt(X * X + Y * Y))) + 1e-3 * rng.standard_normal(X.shape)).ravel()
+    dt = 5.0 / 500
+    up0 = u0 - dt * 0.1 * np.sin(X).ravel()
+    mf = -np.ones(u0.size)
+    g = O.grid(2, nx, ny, 1, dx, dy)
+    ref_u, ref_up = O.sg_steps(g, u0, up0, mf, dt, 12, m)
+    with nls_amd.Solver(2, nx, ny, 1, dx, dy, equation=nls_amd.SG_GAUTSCHI, m=m) as s:
+        s.set_sg_state(u0, up0, mf)
+        s.set_timing(True)
+        s.step(dt, 12)
+        u = s.get_field()
+        if m > 3:
+            assert _ran_pass2(s, m) == _eligible_pr(_pass2, nx, ny, m)
+    assert rel_l2(u, ref_u) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("kind", sorted(O.GG_KINDS))
+def test_pass2_gautschi_g2_with_bc_matches_oracle(_pass2, kind):
+    """phi4 / sg_single / sg_double / sg_hyperbolic (G2, m(x), BC after every step)."""
+    eq = {"phi4": nls_amd.PHI4, "sg": nls_amd.SG_G2, "sg_double": nls_amd.SG_DOUBLE,
+          "sg_hyperbolic": nls_amd.SG_HYPERBOLIC}[kind]
+    n, L, m, dt, steps = 40, 4.0, 10, 1e-2, 8
+    dx = 2 * L / (n - 1)
+    x = np.linspace(-L, L, n)
+    Y, X = np.meshgrid(x, x, indexing="ij")
+    rng = np.random.default_rng(22)
+    u0 = (1.2 * np.exp(-(X ** 2 + Y ** 2) / 2) + 1e-3 * rng.standard_normal(X.shape)).ravel()
+    up = u0 - dt * (0.2 * np.sin(X) * np.exp(-(X ** 2 + Y ** 2) / 4)).ravel()
+    mf = (1.0 + 0.2 * np.cos(X + Y)).ravel()
+    ref, _ = O.gautschi_g2_steps(O.grid(2, n, n, 1, dx, dx), O.GG_KINDS[kind], u0, up, mf, dt, steps, m)
+    with nls_amd.Solver(2, n, n, 1, dx, dx, equation=eq, m=m) as s:
+        s.set_sg_state(u0, up, mf)
+        s.set_timing(True)
+        for _ in range(steps):
+            s.step(dt, 1)
+            s.apply_bc()
+        u = s.get_field()
+        assert _ran_pass2(s, m) == (_pass2 != "reg")
+    assert rel_l2(u, ref) <= TOL_TRAJ
+
+
+def test_pass2_sg_stiff_matches_oracle(_pass2):
+    """C4's spacing (dx = 6/8191) on 256^2."""
+    if _pass2 == "reg":
+        pytest.skip("2D has the LDS-DMA form only")
+    n, dx, m, dt = 256, 6.0 / 8191, 10, 5.0 / 500
+    x = (np.arange(n) - n / 2) * dx
+    Y, X = np.meshgrid(x, x, indexing="ij")
+    u0 = (2.0 * np.arctan(np.exp(3.0 - 5.0 * np.sqrt(X * X + Y * Y) / (n * dx / 6)))).ravel()
+    g = O.grid(2, n, n, 1, dx, dx)
+    ref_u, _ = O.sg_steps(g, u0, u0.copy(), -np.ones(u0.size), dt, 4, m)
+    with nls_amd.Solver(2, n, n, 1, dx, dx, equation=nls_amd.SG_GAUTSCHI, m=m) as s:
+        s.set_sg_state(u0, u0.copy(), -np.ones(u0.size))
+        s.set_timing(True)
+        s.step(dt, 4)
+        u = s.get_field()
+        assert _ran_pass2(s, m)
+    assert rel_l2(u, ref_u) <= TOL_TRAJ
