@@ -120,6 +120,10 @@ struct nls_handle {
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
+  // a new state was set (nls_set_*): the next step starts its bases cold, so it is
+  // issued eagerly, never replayed from a graph captured warm (run-to-run bitwise
+  // reproducibility of "set state; step" sequences)
+  bool p2_fresh = true;
   bool p2_pr = false;          // real field marched as cell pairs by k_p2d (p2_geo)
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
@@ -1268,6 +1272,13 @@ int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t 
   return NLS_OK;
 }
 
+// A new solver state: the s-step bases forget the previous alpha_0 (the blind
+// start's shift), so "set state; step" is bitwise reproducible run to run.
+void p2_cold(nls_handle *h) {
+  h->p2_warm[0] = h->p2_warm[1] = false;
+  h->p2_fresh = true;
+}
+
 int nls_set_field(nls_handle *h, const double *u, uint64_t n) {
   return guarded(h, [&] {
     if (!u) fail(h, NLS_ERR_ARG, "u is NULL");
@@ -1276,11 +1287,11 @@ int nls_set_field(nls_handle *h, const double *u, uint64_t n) {
       hip_check(h, hipMemcpyAsync(h->u, u, (size_t)n * h->esize, hipMemcpyHostToDevice, h->stream),
                 "hipMemcpy H2D");
       h->w0_ready = false;
-      h->p2_warm[0] = h->p2_warm[1] = false;  // a new field: the next basis measures alpha_0 again
     } else {
       copy_in_vector(h, 0, 0, u);
       halo(h, 0, 0);
     }
+    p2_cold(h);  // a new field: the next bases measure alpha_0 again
     h->field_set = true;
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
   });
@@ -1299,6 +1310,7 @@ int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past, const
     if (mfield)
       hip_check(h, hipMemcpyAsync(h->mf, mfield, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
     halo(h, 0, 0);
+    p2_cold(h);
     h->field_set = true;
     h->vel_valid = false;
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
@@ -1320,6 +1332,7 @@ int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfie
     }
     h->coef_set = true;
     h->w0_ready = false;  // the start vector depends on m
+    p2_cold(h);
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
   });
 }
@@ -1596,6 +1609,7 @@ void finish_step_flags(nls_handle *h, double dt) {
 // the step begins with k_nl_init).  The graph is captured on first use per dt.
 bool graph_ready(nls_handle *h, double dt) {
   if (!h->use_graph || h->collective || h->timing || h->runahead > 0) return false;
+  if (h->pass2 && h->p2_fresh) return false;  // the first step after nls_set_*: cold bases
   if (h->cplx_ && (!h->w0_ready || h->w0_dt != dt)) return false;
   if (h->gexec && h->gdt == dt) return true;
   if (h->gexec) {
@@ -1639,6 +1653,7 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
         h->skip_u = s + 1 < nsteps;
         issue_step(h, dt);
         h->skip_u = false;
+        h->p2_fresh = false;  // every basis of the step is warm now
       }
       h->tacc.steps += 1;
       if (ra > 0) {

@@ -1,0 +1,19 @@
+# Headline bench under tail-kernel launch knobs (tile depth NLS_KZ_FUSED, XCD-banded
+# tile order NLS_TILE_REMAP, grid multiplier NLS_GRID_MULT), same box, two rounds.
+# usage: bash tools/tail_sweep.sh
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/tail_sweep
+run() {  # tag, env assignments...
+  local tag=$1; shift
+  env "$@" timeout -k 10 120 python bench.py --steps 6 --warmup 2 --prof-steps 4 --no-cpu-baseline \
+    > gpurun_out/tail_sweep/$tag.json 2> gpurun_out/tail_sweep/$tag.err || exit 1
+  python3 -c "import json;d=json.load(open('gpurun_out/tail_sweep/$tag.json'));k=d['step_roofline']['gpu_kernel_ms_per_step'];print('$tag',round(d['ms_per_step'],3),'tail',round(k['final'],3),'upd',round(k['update'],3))"
+}
+for r in 1 2; do
+  run base$r NLS_DUMMY=0
+  run kz8_$r NLS_KZ_FUSED=8
+  run kz16_$r NLS_KZ_FUSED=16
+  run kz64_$r NLS_KZ_FUSED=64
+  run remap$r NLS_TILE_REMAP=1
+  run mult32_$r NLS_GRID_MULT=32
+done
