@@ -929,9 +929,14 @@ void alloc_all(nls_handle *h) {
     if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
     Geo gf = g;
     if (h->kz_fused) gf.kz = h->kz_fused;
+    const int64_t tt = stencil_tiles(gf, dim, fused_rows_per_thread());
+    // large slabs: one tile per workgroup (the tail reduces nothing, so the grid
+    // size only sets the dispatch balance): 512^3 m=16 tail 6.64 -> 6.38 ms against
+    // two tiles per workgroup (tools/tail_sweep.sh, same box, two rounds)
+    const bool one_tile = g.nloc > (int64_t(1) << 25) && !std::getenv("NLS_GRID_MULT");
     for (int mode = 0; mode < 8; ++mode) {
       const void *ft = kernel_tail(tail_is_cplx(h, mode), dim, mode, h->m, ani);
-      if (ft) h->tail_grid[mode] = occupancy_grid(h, ft, stencil_tiles(gf, dim, fused_rows_per_thread()));
+      if (ft) h->tail_grid[mode] = one_tile ? (int)tt : occupancy_grid(h, ft, tt);
     }
   }
   // vectors stored per basis: m - 1 where every Lanczos run on it ends in a fused
