@@ -9,10 +9,11 @@ HBM before the timed region.  With --gpus N (launched by torch.distributed.run)
 the 512^3 grid is z-slab decomposed over N ranks (strong scaling) with RCCL halo
 exchange + all-reduce of the Lanczos dot products.
 
-roofline: the dominant kernel is the fused tail k_tail<NLSE, m> (the last
-Lanczos vector + combination + both nonlinear half-steps; m-1 basis vectors
-read, u and the next start vector written): algorithmic bytes per launch =
-(m+1) * 16 B * cells, timed with HIP events on the
+roofline: the dominant kernel is the longer of the fused tail k_tail<NLSE, m>
+(the last Lanczos vector + combination + both nonlinear half-steps; m-1 stored
+vectors read, the next start vector written, u on a call's last step) and the
+largest two-vector basis pass k_p2d<J = m-4> (J+1 reads + 2 writes) -- the two
+take about the same time at 512^3, m = 16; timed with HIP events on the
 solver's own stream in a separate pass of --prof-steps steps right after the
 timed region (the timed region itself carries no per-launch events).
 --gpus N without torch.distributed.run: bench.py starts the N ranks itself.
@@ -271,17 +272,21 @@ def _cpu_sample(args, oracle_py):
 
 def load_traffic(workload, m, kernel_prefix):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary
-    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950 read-side x2 correction); None
-    unless the summary was taken on the same m and the same dominant kernel."""
+    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950 read-side x2 correction): the
+    summary's per-kernel entry whose name starts with kernel_prefix (a k_p2d<J, ...>
+    pass or the k_tail), taken on the same workload and m; None otherwise."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("m") != m or not str(d.get("dominant_kernel", "")).startswith(kernel_prefix):
+        if d.get("m") != m:
             return None
-        return d.get("bytes_per_launch")
+        for name, e in d.get("kernels", {}).items():
+            if name.startswith(kernel_prefix):
+                return e["read_bytes"] + e["write_bytes"]
+        return None
     except Exception:
         return None
 
@@ -471,7 +476,7 @@ def main():
         bytes_launch = (J + 1 + p2ns) * esz * n_local
         kname = f"k_p{max(p2ns, 2)}d<J={J}> ({p2ns}-vector Lanczos pass: radius-{p2ns} stencil + CGS " \
                 f"coefficients, {J + 1} reads + {p2ns} writes)"
-        kprefix = f"k_p{max(p2ns, 2)}d<"
+        kprefix = f"k_p{max(p2ns, 2)}d<{J}, "
     elif fcnt and w["eq"] in (0, 1, 3) and not w.get("sewi"):
         J = m - 2
         cnt = fcnt
@@ -486,9 +491,9 @@ def main():
         avg_ms = tm["update_ms"][J] / cnt if cnt else float("nan")
         bytes_launch = (J + 2) * esz * n_local
         kname = f"k_update<J={J}> (stencil + CGS + write, {J + 1} reads + 1 write)"
-        kprefix = "k_update<"
+        kprefix = None  # (no per-J PMC entry is matched for the one-vector passes)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if cnt else None
-    traffic = load_traffic(args.workload, m, kprefix) if world == 1 else None
+    traffic = load_traffic(args.workload, m, kprefix) if world == 1 and kprefix else None
     step_bytes = algorithmic_bytes_per_cell_step(m, w["eq"], w.get("sewi", False)) * n_local
     step_ms = el * 1e3 / args.steps
     result = {
