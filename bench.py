@@ -9,11 +9,12 @@ HBM before the timed region.  With --gpus N (launched by torch.distributed.run)
 the 512^3 grid is z-slab decomposed over N ranks (strong scaling) with RCCL halo
 exchange + all-reduce of the Lanczos dot products.
 
-roofline: the dominant kernel is the longer of the fused tail k_tail<NLSE, m>
+roofline: for the NLSE the dominant kernel is the fused tail k_tail<NLSE, m>
 (the last Lanczos vector + combination + both nonlinear half-steps; m-1 stored
-vectors read, the next start vector written, u on a call's last step) and the
-largest two-vector basis pass k_p2d<J = m-4> (J+1 reads + 2 writes) -- the two
-take about the same time at 512^3, m = 16; timed with HIP events on the
+vectors read, the next start vector written, u on a call's last step: the most
+bytes per launch; the largest two-vector pass k_p2d<m-4> takes about as long at
+512^3, m = 16), for the real Gautschi equations the largest
+two-vector pass; timed with HIP events on the
 solver's own stream in a separate pass of --prof-steps steps right after the
 timed region (the timed region itself carries no per-launch events).
 --gpus N without torch.distributed.run: bench.py starts the N ranks itself.
@@ -469,7 +470,11 @@ def main():
         own_bytes = esz * (1 + sum(j + 1 + ns for j, ns in sched) + 1 + (m + u_frac))
     # (the real Gautschi tails are not modelled here: with two-vector passes the
     # largest pass is reported for them)
-    if pass2 and (p2_ms > tail_ms or w["eq"] not in (0, 1, 3)):
+    # the NLSE's dominant kernel is the fused tail (the most bytes per launch: m-1 reads,
+    # the next start vector and u; the largest pass takes about as long, so a timing
+    # rule would flip between runs), else the largest two-vector pass
+    nlse_tail = bool(fcnt) and w["eq"] in (0, 1, 3) and not w.get("sewi")
+    if pass2 and not nlse_tail:
         J = p2J
         cnt = ucnt[J]
         avg_ms = p2_ms
