@@ -34,12 +34,17 @@ with nls_amd.Solver(3, n, n, nz, dx, dx, m=16) as s:
     s.set_timing(False)
 cls = {k: round(v / 3, 3) for k, v in tm["class_ms"].items() if v}
 upd = {j: round(tm["update_ms"][j] / 3, 3) for j in range(16) if tm["update_count"][j]}
-print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} {el * 1e3:8.3f} ms/step "
+print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} kz={os.environ.get('NLS_P2_KZ', 'auto')} {el * 1e3:8.3f} ms/step "
       f"{n * n * nz / el / 1e6:8.0f} Mcells*steps/s  per step {cls}  per step and J {upd}", flush=True)
 """
 
-for nz, force in [(64, 0), (64, 1), (128, 0), (128, 1)]:
+# (nz, collective, k_p2d tile depth): an N-rank handle sizes its tiles from the GLOBAL
+# plane count (256 at 512^3 for every N), a 512 x 512 x nz grid from nz -- the third
+# entry pins the former
+for nz, force, kz in [(64, 0, 0), (64, 1, 0), (64, 1, 256), (128, 0, 0), (128, 1, 256)]:
     env = dict(os.environ, NLS_FORCE_RCCL=str(force))
+    if kz:
+        env["NLS_P2_KZ"] = str(kz)
     r = subprocess.run([sys.executable, "-c", CHILD, ROOT, str(nz)], env=env, timeout=300)
     if r.returncode:
         sys.exit(r.returncode)
