@@ -383,6 +383,7 @@ def main():
         rid = obj[0]
     s = nls_amd.Solver(dim, n, n, n if dim == 3 else 1, dx, dx, equation=w["eq"], m=m,
                        device=local_rank, nranks=world, rank=rank, rccl_id=rid)
+    comm_ranks, comm_transport = s.comm_size()  # what the library's transport reports
     u = synthetic_ic(w, s.z0, s.nzl)
     if w["eq"] == 2:
         s.set_sg_state(u, u.copy(), -np.ones(u.size))
@@ -519,8 +520,8 @@ def main():
                    "equation": ["nlse_cubic", "nlse_cq", "sg_gautschi", "nlse_g2", "kg_gautschi"][w["eq"]]
                    + ("_sewi" if w.get("sewi") else ""),
                    "parallelism": f"z-slab x{world}" if world > 1 else "single GPU",
-                   "ranks": {"world": world, "transport": "rccl" if world > 1 else "none",
-                             "slab_planes_rank0": int(s.nzl)}},
+                   "ranks": {"world": world, "transport": comm_transport,
+                             "library_comm_ranks": comm_ranks, "slab_planes_rank0": int(s.nzl)}},
         "roofline": {
             "bound": "hbm",
             "kernel": kname,

@@ -144,6 +144,13 @@ const char *nls_last_error(const nls_handle *h); /* h == NULL: last nls_create e
  * (3D: z, 2D: y); n_local = nzl * plane size. */
 int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t *n_local);
 
+/* Ranks the handle exchanges with, as the transport itself reports them: the RCCL
+ * communicator's ncclCommCount (transport 1), the in-process group's size
+ * (transport 2), or 1 for a single-rank handle without a communicator
+ * (transport 0).  The multi-GPU counterpart of the reference's
+ * device/nlse_driver_omp.cpp:103-121 rank loop; bench.py reports it. */
+int nls_comm_size(const nls_handle *h, int32_t *nranks, int32_t *transport);
+
 /* The slab decomposition itself (pure function, no device needed): planes
  * [*z0, *z0 + *nzl) of npl planes owned by `rank` of `nranks` -- contiguous,
  * the first npl % nranks ranks one plane larger.  nls_local_planes() of a

@@ -1269,6 +1269,21 @@ int nls_slab_planes(uint32_t npl, int32_t nranks, int32_t rank, uint32_t *z0, ui
   return NLS_OK;
 }
 
+int nls_comm_size(const nls_handle *h, int32_t *nranks, int32_t *transport) {
+  if (!h || !nranks) return NLS_ERR_ARG;
+  int n = 1, tr = 0;
+  if (h->comm) {
+    if (ncclCommCount(h->comm, &n) != ncclSuccess) return NLS_ERR_RCCL;
+    tr = 1;
+  } else if (h->group) {
+    n = h->group->n;
+    tr = 2;
+  }
+  *nranks = n;
+  if (transport) *transport = tr;
+  return NLS_OK;
+}
+
 int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t *n_local) {
   if (!h) return NLS_ERR_ARG;
   if (z0) *z0 = (uint32_t)h->geo.z0;

@@ -32,7 +32,7 @@ MAX_KRYLOV = 32
 
 EXPORTED_SYMBOLS = (
     "nls_abi_version", "nls_config_default", "nls_create", "nls_destroy", "nls_last_error",
-    "nls_local_planes", "nls_set_field", "nls_set_sg_state", "nls_step", "nls_sync",
+    "nls_local_planes", "nls_comm_size", "nls_set_field", "nls_set_sg_state", "nls_step", "nls_sync",
     "nls_get_field", "nls_get_sg_velocity", "nls_krylov_apply", "nls_laplacian_apply",
     "nls_rccl_unique_id", "nls_group_create", "nls_group_destroy", "nls_set_timing",
     "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
@@ -97,6 +97,7 @@ def lib():
     L.nls_last_error.restype = C.c_char_p
     L.nls_local_planes.argtypes = [H, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint64)]
+    L.nls_comm_size.argtypes = [H, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     L.nls_slab_planes.argtypes = [C.c_uint32, C.c_int32, C.c_int32, C.POINTER(C.c_uint32),
                                   C.POINTER(C.c_uint32)]
     L.nls_set_field.argtypes = [H, dp, C.c_uint64]
@@ -211,6 +212,13 @@ class Solver:
         z0, nzl, nloc = C.c_uint32(), C.c_uint32(), C.c_uint64()
         self._call(L.nls_local_planes, C.byref(z0), C.byref(nzl), C.byref(nloc))
         self.z0, self.nzl, self.n_local = z0.value, nzl.value, nloc.value
+
+    def comm_size(self) -> tuple[int, str]:
+        """(ranks, transport) as the handle's transport reports them (nls_comm_size):
+        the RCCL communicator's count, the in-process group's size, or (1, "none")."""
+        n, tr = C.c_int32(), C.c_int32()
+        self._call(lib().nls_comm_size, C.byref(n), C.byref(tr))
+        return n.value, ("none", "rccl", "group")[tr.value]
 
     # -- plumbing ---------------------------------------------------------
     def _call(self, fn, *args):

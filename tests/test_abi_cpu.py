@@ -223,3 +223,13 @@ def test_abi_exports_cq_g2_equation():
     assert nls_amd.NLSE_CQ_G2 == 9
     with open(os.path.join(ROOT, "include", "nls.h")) as fh:
         assert "NLS_NLSE_CQ_G2 = 9" in fh.read()
+
+
+def test_comm_size_rejects_null_handle():
+    """nls_comm_size (the ranks bench.py reports) fails cleanly without a handle or
+    an output pointer -- no device needed."""
+    import ctypes as C
+    L = nls_amd.lib()
+    n, tr = C.c_int32(-7), C.c_int32(-7)
+    assert L.nls_comm_size(None, C.byref(n), C.byref(tr)) == -1
+    assert n.value == -7 and tr.value == -7
