@@ -191,4 +191,5 @@ def test_pass2_rccl_collective_path_single_rank(monkeypatch):
         s.step(1e-3, 4)
         got = s.get_field()
         assert _ran_pass2(s, m)
+        assert s.comm_size() == (1, "rccl")  # ncclCommCount of the forced communicator
     assert rel_l2(got, ref) <= 1e-10

@@ -59,12 +59,13 @@ def test_bench_slabs_match_single_rank(field_and_single, nr):
     grp = nls_amd.Group(nr)
     out = np.empty_like(u0)
     P = N * N
-    err, planes = [], []
+    err, planes, comm = [], [], []
 
     def work(r):
         try:
             with nls_amd.Solver(3, N, N, N, DX, DX, m=M, device=0, nranks=nr, rank=r, group=grp) as s:
                 planes.append(s.nzl)
+                comm.append(s.comm_size())
                 sl = slice(s.z0 * P, (s.z0 + s.nzl) * P)
                 s.set_field(u0[sl])
                 s.step(DT, STEPS)
@@ -78,6 +79,7 @@ def test_bench_slabs_match_single_rank(field_and_single, nr):
     grp.close()
     assert not err, err
     assert sorted(planes) == [N // nr] * nr
+    assert comm == [(nr, "group")] * nr  # the transport's own rank count (nls_comm_size)
     a3 = out.reshape(N, N, N)
     assert np.array_equal(a3, a3[:, :, ::-1]), f"{nr} slabs lost the exact x-mirror symmetry"
     assert abs(np.linalg.norm(out) / np.linalg.norm(u0) - 1.0) < 1e-12
