@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define NLS_ABI_VERSION 4
+#define NLS_ABI_VERSION 5
 #define NLS_MAX_KRYLOV 32
 
 enum nls_status {
@@ -170,7 +170,8 @@ int nls_set_sg_state(nls_handle *h, const double *u, const double *u_past,
  * operator div(c grad u) (face weights (c_a + c_b)/2, diagonal -sum of weights,
  * scale 1/(dx*dy) in 2D and 1/(dx*dx) in 3D), both real, local slab.  Must be
  * called before the first nls_step.  NLS_NLSE_CQ_G2: m(x) only (cfield NULL,
- * isotropic operator); optional, m = 1 until called. */
+ * isotropic operator); likewise required before the first nls_step /
+ * nls_krylov_apply / nls_laplacian_apply (NLS_ERR_STATE otherwise). */
 int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfield,
                          uint64_t n_local);
 /* Neumann "copy" boundary condition of the G2 drivers, applied after every step
@@ -249,6 +250,24 @@ typedef struct nls_timing {
 int nls_set_timing(nls_handle *h, int32_t enable);
 int nls_get_timing(nls_handle *h, nls_timing *out); /* synchronises */
 int nls_reset_timing(nls_handle *h);
+
+/* Debug: the transport operations of a collective handle in issue order, with
+ * the cross-stream dependencies between them.  Recorded only when the
+ * environment has NLS_OPLOG=1 at nls_create.  Entries are 4 int32 each:
+ * {kind, stream (0 compute, 1 halo), count (doubles), peer rank (-1: none)}.
+ * Sets *n to the number recorded; with out != NULL also copies at most cap
+ * entries into out and clears the log (out == NULL: size query only).  The invariant the tests check: an operation
+ * on one stream is ordered after every earlier operation on the other stream
+ * by a NLS_OP_WAIT_* entry in between (RCCL never sees one communicator's
+ * operations in flight on two streams at once). */
+enum nls_op_kind {
+  NLS_OP_ALLREDUCE = 1,      /* ncclAllReduce / local fixed-order sum of the Lanczos sums */
+  NLS_OP_SEND = 2,           /* halo planes to peer */
+  NLS_OP_RECV = 3,           /* halo planes from peer */
+  NLS_OP_WAIT_HALO = 4,      /* compute stream waits for the halo stream */
+  NLS_OP_WAIT_COMPUTE = 5    /* halo stream waits for the compute stream */
+};
+int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n);
 
 #ifdef __cplusplus
 }

@@ -82,7 +82,9 @@ struct nls_handle {
   bool cplx_ = true;
   size_t esize = 16;
   Geo geo{};
-  int64_t vs = 0;  // elements per stored vector (incl. 2 x GHOST ghost planes)
+  int ghost = 1;   // ghost planes per side of a stored vector: 2 on two-vector handles
+  int64_t vpad = 4096;  // stride pad of a stored vector (elements)
+  int64_t vs = 0;  // elements per stored vector (incl. 2 x ghost planes and the pad)
   int m = 10;
   int nbasis = 1;
   Basis B[2];
@@ -114,10 +116,8 @@ struct nls_handle {
   void *p2 = nullptr;          // P2State
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
-  int p2impl = 2;              // 2: LDS-DMA k_p2d; 1: register-march k_pass2r (NLS_P2_IMPL)
   bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
-  bool p3 = false;             // three-vector passes k_p3d at J = 2, 5 (single rank, k_p2d; NLS_PASS3=1)
-  cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
+  cplx *zbuf = nullptr;       // one zero row (nx cells): the DMA source of out-of-grid rows
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
   // a new state was set (nls_set_*): the next step starts its bases cold, so it is
@@ -157,6 +157,12 @@ struct nls_handle {
   hipEvent_t ev_bnd = nullptr, ev_halo = nullptr, ev_bdone = nullptr;
   bool halo_pending = false;
   bool bnd_side = true;  // boundary-plane launches on cstream (NLS_BND_SIDE=0: in order on the compute stream)
+  // debug (NLS_OPLOG=1 at nls_create): the transport operations in issue order, with
+  // the cross-stream waits between them (nls_debug_oplog; tests/test_gpu_oplog.py)
+  bool oplog_on = false;
+  std::vector<int32_t> oplog;  // [kind, stream, count, peer] per entry (nls.h NLS_OP_*)
+  // debug switches read once at nls_create (never on the per-reduction path)
+  bool dbg_sums = false, dbg_alpha = false;
   // asynchronous snapshots: staging copy on the compute stream, D2H on xstream
   hipStream_t xstream = nullptr;
   hipEvent_t ev_snap = nullptr, ev_snap_done = nullptr;
@@ -213,12 +219,26 @@ void fail(nls_handle *h, int code, const std::string &msg) {
   throw Fail{code};
 }
 
-// Basis vectors carry GHOST ghost planes below and above the slab: one for the
-// radius-1 stencil of the one-vector passes, two for the radius-2 march of the
-// two-vector passes (k_p2d) on multi-rank handles.
-constexpr int GHOST = 2;  // == P2D_GHOST (nls_pass2d.hpp)
+// Basis vectors carry h->ghost ghost planes below and above the slab: one for the
+// radius-1 stencils of the one-vector passes, two (P2D_GHOST) for the radius-2
+// march of the two-vector passes (k_p2d).  The 32-bit index check at nls_create
+// assumes the larger (GHOST_MAX).
+constexpr int GHOST_MAX = 2;  // == P2D_GHOST (nls_pass2d.hpp)
 char *vec_ptr(nls_handle *h, int b, int k) {  // local plane 0 of vector k of basis b
-  return static_cast<char *>(h->B[b].W) + ((int64_t)k * h->vs + GHOST * h->geo.P) * (int64_t)h->esize;
+  return static_cast<char *>(h->B[b].W) + ((int64_t)k * h->vs + h->ghost * h->geo.P) * (int64_t)h->esize;
+}
+
+// debug op log (NLS_OPLOG=1): transport operations and cross-stream waits in issue order
+void oplog(nls_handle *h, int kind, int stream, int64_t count, int peer) {
+  if (!h->oplog_on) return;
+  h->oplog.insert(h->oplog.end(), {(int32_t)kind, (int32_t)stream, (int32_t)count, (int32_t)peer});
+}
+int stream_id(const nls_handle *h, hipStream_t st) { return st && st == h->cstream ? 1 : 0; }
+// the halo stream (cstream) waits for the work enqueued so far on the compute stream
+void halo_after_compute(nls_handle *h) {
+  hip_check(h, hipEventRecord(h->ev_bnd, h->stream), "hipEventRecord");
+  hip_check(h, hipStreamWaitEvent(h->cstream, h->ev_bnd, 0), "hipStreamWaitEvent");
+  oplog(h, NLS_OP_WAIT_COMPUTE, 1, 0, -1);
 }
 
 hipEvent_t get_event(nls_handle *h) {
@@ -333,6 +353,15 @@ void halo_planes(nls_handle *h, char *v, int64_t es, hipStream_t st = nullptr, i
     rec.b = get_event(h);
     hip_check(h, hipEventRecord(rec.a, st), "hipEventRecord");
   }
+  const int sid = stream_id(h, st);
+  if (h->rank > 0) {
+    oplog(h, NLS_OP_SEND, sid, (int64_t)cnt, h->rank - 1);
+    oplog(h, NLS_OP_RECV, sid, (int64_t)cnt, h->rank - 1);
+  }
+  if (h->rank < h->nranks - 1) {
+    oplog(h, NLS_OP_SEND, sid, (int64_t)cnt, h->rank + 1);
+    oplog(h, NLS_OP_RECV, sid, (int64_t)cnt, h->rank + 1);
+  }
   if (h->group) {
     halo_local(h, st, first, last, gbelow, gabove, (size_t)P * es * np);
     if (h->timing) {
@@ -367,8 +396,7 @@ void halo(nls_handle *h, int b, int k) {
 // the compute stream; the exchange runs on cstream while the interior planes
 // are computed.  halo_wait() orders the compute stream after it.
 void halo_begin(nls_handle *h, int b, int k) {
-  hip_check(h, hipEventRecord(h->ev_bnd, h->stream), "hipEventRecord");
-  hip_check(h, hipStreamWaitEvent(h->cstream, h->ev_bnd, 0), "hipStreamWaitEvent");
+  halo_after_compute(h);
   halo_planes(h, vec_ptr(h, b, k), (int64_t)h->esize, h->cstream, h->pass2 ? 2 : 1);
   hip_check(h, hipEventRecord(h->ev_halo, h->cstream), "hipEventRecord");
   h->halo_pending = true;
@@ -376,11 +404,19 @@ void halo_begin(nls_handle *h, int b, int k) {
 void halo_wait(nls_handle *h) {
   if (!h->halo_pending) return;
   hip_check(h, hipStreamWaitEvent(h->stream, h->ev_halo, 0), "hipStreamWaitEvent");
+  oplog(h, NLS_OP_WAIT_HALO, 0, 0, -1);
   h->halo_pending = false;
 }
 
+// On the compute stream, after any halo exchange still in flight on the halo
+// stream (halo_wait): the communicator never has operations of two streams in
+// flight at once, so nothing relies on RCCL ordering one communicator's work
+// across streams.  The exchange has overlapped the pass's interior
+// launch by then, which is all the overlap there is to gain.
 void allreduce_sums(nls_handle *h, int b, int ncplx, void *where = nullptr) {
   void *p = where ? where : static_cast<void *>(&h->B[b].st->sums[0]);
+  halo_wait(h);
+  oplog(h, NLS_OP_ALLREDUCE, 0, 2 * (int64_t)ncplx, -1);
   if (h->group) {
     // publish my partial sums, rendezvous, then every rank sums all ranks'
     // publications in rank order (identical result on every rank)
@@ -400,7 +436,7 @@ void allreduce_sums(nls_handle *h, int b, int ncplx, void *where = nullptr) {
     int nr = h->nranks, par = parity, cnt = ncplx, stride = NSUM;
     void *args[] = {&dst, &g->pub, &nr, &par, &cnt, &stride};
     launch(h, 2, -1, kernel_sum_ranks(), 1, args);
-    if (std::getenv("NLS_DEBUG_SUMS")) {
+    if (h->dbg_sums) {
       std::vector<cplx> hv(ncplx), hp(ncplx);
       hip_check(h, hipStreamSynchronize(h->stream), "sync");
       hip_check(h, hipMemcpy(hv.data(), p, ncplx * sizeof(cplx), hipMemcpyDeviceToHost), "d2h");
@@ -557,7 +593,7 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
       }
       if (prev_qa) {
         reduce_qa(h, b, j, ga);
-        if (std::getenv("NLS_DEBUG_ALPHA")) {  // debug: folded vs directly reduced alpha_j
+        if (h->dbg_alpha) {  // debug: folded vs directly reduced alpha_j
           KState hs;
           hip_check(h, hipStreamSynchronize(h->stream), "sync");
           hip_check(h, hipMemcpy(&hs, st, sizeof(KState), hipMemcpyDeviceToHost), "d2h");
@@ -600,10 +636,7 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
     // the compute stream (disjoint output planes and partial columns); the next
     // pass waits on the halo event.
     const bool side = need_halo && pl.nbnd > 0 && h->bnd_side;
-    if (side) {
-      hip_check(h, hipEventRecord(h->ev_bnd, h->stream), "hipEventRecord");
-      hip_check(h, hipStreamWaitEvent(h->cstream, h->ev_bnd, 0), "hipStreamWaitEvent");
-    }
+    if (side) halo_after_compute(h);
     for (int i = 0; i < pl.n; ++i) {
       Geo gi = g;
       gi.qa = pl.qa[i];
@@ -629,9 +662,6 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   reduce_final(h, b, nf, f0, f1, tr, ti);
 }
 
-// tiles of one two-vector launch over local planes [qa, qb) with tile depth kz:
-// k_p2d one workgroup per 64 x 4-row tile column chunk; k_pass2r one wave per
-// 60 x rb output column chunk, 4 waves per workgroup
 // The geometry k_p2d marches: the handle's, or for a 2D grid planes of 4 rows
 // (nyp = 4, npl = ny/4, P = 4 nx; single rank), whose row wrap is the 2D y neighbour
 Geo p2_geo(const nls_handle *h) {
@@ -651,23 +681,23 @@ Geo p2_geo(const nls_handle *h) {
   }
   return g;
 }
-int p2_tiles(const nls_handle *h, int J, int64_t qa, int64_t qb, int64_t kz) {
+// tiles of one k_p2d launch over local planes [qa, qb) with tile depth kz: one
+// workgroup per 64 x 4-row tile column chunk
+int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz) {
   const Geo g = p2_geo(h);
   const int64_t nzc = (qb - qa + kz - 1) / kz;
-  if (h->p2impl == 2)
-    return (int)(((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * (g.nyp / P2D_ROWS) * nzc);
-  const int rb = P2R_ROWS(J);
-  const int64_t waves = ((g.nx + P2R_WAVE_XO - 1) / P2R_WAVE_XO) * (g.nyp / rb) * nzc;
-  return (int)((waves + NTHREADS / 64 - 1) / (NTHREADS / 64));
+  return (int)(((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * (g.nyp / P2D_ROWS) * nzc);
 }
-// Multi-rank handles (slabs of >= 8 planes) launch each pass as the two boundary
-// plane pairs (tile depth 2, on the halo stream, followed there by the two-plane
-// halo exchange of the new stencil vector) and the interior (compute stream).
-bool p2_split(const nls_handle *h) { return h->collective && h->geo.nzl >= 8 && h->p2impl == 2; }
-int p2_grid(const nls_handle *h, int J) {
+// Multi-rank handles (slabs of >= 8 planes) launch each pass as ONE launch over both
+// boundary plane pairs (tile depth 2, Geo::q2; on the halo stream, followed there
+// by the two-plane halo exchange of the new stencil vector) and the interior
+// (compute stream).
+bool p2_split(const nls_handle *h) { return h->collective && h->geo.nzl >= 8; }
+int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
+int p2_grid(const nls_handle *h) {
   const int64_t nzl = p2_geo(h).nzl;
-  if (!p2_split(h)) return p2_tiles(h, J, 0, nzl, h->p2kz);
-  return 2 * p2_tiles(h, J, 0, 2, 2) + p2_tiles(h, J, 2, nzl - 2, h->p2kz);
+  if (!p2_split(h)) return p2_tiles(h, 0, nzl, h->p2kz);
+  return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, h->p2kz);
 }
 
 // Two new vectors per pass (nls_pass2.hpp): the alpha pass + reduction of W_0
@@ -677,15 +707,14 @@ int p2_grid(const nls_handle *h, int J) {
 // eigensolve; k_p2tfin maps fin to the coefficients of the caller's k_tail
 // (S_0..S_{m-2} and L S_{m-2}: the last Lanczos vector is never stored).
 // The s-step schedule (tests/sstep_model.py sstep_schedule): [(J, ns)] of the
-// passes storing S_0..S_{nstore-1}, two new vectors per pass, three (k_p3d) at
-// J = 2 and 5 when the basis reaches S_8 (so the two-vector passes stay at even J),
-// the last pass one or two.
-std::vector<std::pair<int, int>> p2_schedule(const nls_handle *h, int nstore) {
+// passes storing S_0..S_{nstore-1}, two new vectors per pass at even J, the last
+// pass one or two.  (Three-vector passes at J = 2, 5 move 6 % fewer bytes at
+// m = 16 but were issue-bound on MI355X, 29.5 vs 26.4 ms of passes at 512^3;
+// measured in round 2 and removed)
+std::vector<std::pair<int, int>> p2_schedule(const nls_handle *, int nstore) {
   std::vector<std::pair<int, int>> out;
-  const bool use3 = h->p3 && nstore - 1 >= 8;
   for (int J = 0; J + 1 < nstore;) {
-    const int left = nstore - 1 - J;
-    const int ns = (use3 && (J == 2 || J == 5) && left >= 3) ? 3 : std::min(2, left);
+    const int ns = std::min(2, nstore - 1 - J);
     out.emplace_back(J, ns);
     J += ns;
   }
@@ -700,7 +729,7 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
   const std::vector<std::pair<int, int>> sched = p2_schedule(h, nstore);
   // blind start once a previous basis left its alpha_0 (the shift of the J = 0
   // pass): no alpha pass over W_0, beta from the pass's own ||S_0||^2
-  const bool blind = h->p2_warm[b] && h->p2_blind && h->p2impl == 2;  // k_p2d<0> reduces ||S_0||^2
+  const bool blind = h->p2_warm[b] && h->p2_blind;  // k_p2d<0> reduces ||S_0||^2
   if (!blind) {
     Geo ga = h->geo;
     ga.kz = h->kz_alpha;
@@ -722,8 +751,8 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
   for (size_t si = 0; si < sched.size(); ++si) {
     int J = sched[si].first, ns = sched[si].second;
     const int out = J + ns;  // the pass's last vector: the next stencil vector
-    int nb = p2_grid(h, J);
-    const void *fn = ns == 3 ? kernel_pass3(J) : kernel_pass2(J, ns == 2, h->p2impl, h->p2_d2, h->p2_pr);
+    int nb = p2_grid(h);
+    const void *fn = kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
     if (!split) {
       int poff = 0;
@@ -731,16 +760,19 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
       launch(h, 1, J, fn, nb, args);
       if (h->collective) halo_begin(h, b, out);
     } else {
+      // one launch over both boundary plane pairs [0, 2) and [nzl-2, nzl) on the halo
+      // stream, then the exchange of the new stencil vector's two boundary planes
+      // there, while the interior runs on the compute stream
       const int64_t nzl = h->geo.nzl;
-      const int tb = p2_tiles(h, J, 0, 2, 2);
-      hip_check(h, hipEventRecord(h->ev_bnd, h->stream), "hipEventRecord");
-      hip_check(h, hipStreamWaitEvent(h->cstream, h->ev_bnd, 0), "hipStreamWaitEvent");
+      const int tb = p2_bnd_tiles(h);
+      halo_after_compute(h);
       Geo gb = g;
       gb.kz = 2;
-      for (int side = 0; side < 2; ++side) {
-        gb.qa = side == 0 ? 0 : (int32_t)(nzl - 2);
-        gb.qb = gb.qa + 2;
-        int poff = side * tb;
+      gb.qa = 0;
+      gb.qb = 2;
+      gb.q2 = (int32_t)(nzl - 2);
+      {
+        int poff = 0;
         void *args[] = {&W, &vs, &gb, &ps, &h->partP2, &nb, &h->zbuf, &poff};
         launch(h, 1, J, fn, tb, args, h->cstream);
       }
@@ -751,9 +783,11 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
       Geo gi = g;
       gi.qa = 2;
       gi.qb = (int32_t)(nzl - 2);
-      int poff = 2 * tb;
+      int poff = tb;
       void *args[] = {&W, &vs, &gi, &ps, &h->partP2, &nb, &h->zbuf, &poff};
-      launch(h, 1, J, fn, nb - 2 * tb, args);
+      launch(h, 1, J, fn, nb - tb, args);
+      // (the partials of the boundary launch; the exchange itself is awaited by
+      // the all-reduce / the next pass)
       hip_check(h, hipStreamWaitEvent(h->stream, h->ev_bdone, 0), "hipStreamWaitEvent");
     }
     // columns: S-dots per new vector, the Gram's upper triangle, J = 0: ||S_0||^2
@@ -844,9 +878,9 @@ void setup_geometry(nls_handle *h) {
   // 4096 elements (64 KiB of complex<double>): same-box A/B sweeps (tools/exp_pad3.sh,
   // exp_pad4.sh) gave 512^3 update passes -5 % (two boxes), 4096^2 +6 % vs the former
   // 4 KiB pad, within 1 % elsewhere; no pad at all is ~15 % slower (tools/bw_probe.hip)
-  int64_t pad = 4096;
-  if (const char *e = std::getenv("NLS_VEC_PAD")) pad = std::max<int64_t>(0, std::atoll(e));
-  h->vs = (g.nzl + 2 * GHOST) * g.P + pad;
+  h->vpad = 4096;
+  if (const char *e = std::getenv("NLS_VEC_PAD")) h->vpad = std::max<int64_t>(0, std::atoll(e));
+  // (the vector stride h->vs follows in alloc_all, once the ghost depth is known)
 }
 
 // scalar type of a tail kernel on this handle: the NLSE and sEWI epilogues are
@@ -872,7 +906,6 @@ void alloc_all(nls_handle *h) {
   // slabs) and 2D on one rank (ny % 4 == 0, planes of 4 rows);
   // NLS_PASS2=0/1 forces it off / on where a pass form exists.
   h->pass2 = false;
-  if (const char *e = std::getenv("NLS_P2_IMPL")) h->p2impl = std::atoi(e) == 1 ? 1 : 2;
   {
     const char *e = std::getenv("NLS_PASS2");
     const bool want = e ? std::atoi(e) != 0 : true;
@@ -885,31 +918,29 @@ void alloc_all(nls_handle *h) {
     const bool base = (c || pr) && !ani && (dim == 3 || d2) && (!h->collective || g.nzl >= 4) &&
                       (h->nbasis == 1 || pr) && h->m >= 3 &&
                       g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
-    // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS; k_pass2r (3D): 64-aligned x
+    // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS
     const bool dma = (dim == 3 ? g.nyp % P2D_ROWS == 0 && g.nyp >= 4 : d2) && h->m - 4 <= P2D_MAXJ;
-    if (h->p2impl == 2 && !dma) h->p2impl = (e && dim == 3) ? 1 : 0;  // the register march only on request
-    h->pass2 = want && base &&
-               (h->p2impl == 2 ||
-                (h->p2impl == 1 && dim == 3 && !h->collective && g.nx % 64 == 0 && g.nyp % 2 == 0));
+    h->pass2 = want && base && dma;
     h->p2_d2 = h->pass2 && dim == 2;
     h->p2_pr = h->pass2 && !c;
   }
+  // stored vectors: slab + ghost planes (two for the two-vector passes' radius-2
+  // march) + the stride pad
+  h->ghost = h->pass2 ? GHOST_MAX : 1;
+  h->vs = (g.nzl + 2 * h->ghost) * g.P + h->vpad;
   if (h->pass2) {
     // z depth of a k_p2d tile: deep (the prologue is not overlapped), but at least
-    // ~2048 tiles so that every CU gets several (256 at 512^3, 32 at 256^3)
+    // ~2048 tiles so that every CU gets several (256 at 512^3, 32 at 256^3), from the
+    // planes this launch covers: the slab's (not the global count), its
+    // interior on split multi-rank handles (64-plane slabs of 512^3: 2 x 30 planes)
     const Geo gm = p2_geo(h);
     const int64_t cols = ((gm.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * std::max<int64_t>(1, gm.nyp / P2D_ROWS);
     const int64_t nzc = std::max<int64_t>(1, (2048 + cols - 1) / cols);
-    h->p2kz = (int)std::max<int64_t>(16, std::min<int64_t>(256, (gm.npl + nzc - 1) / nzc));
+    const int64_t span = p2_split(h) ? gm.nzl - 4 : gm.nzl;
+    h->p2kz = (int)std::max<int64_t>(std::min<int64_t>(16, span), std::min<int64_t>(256, (span + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("NLS_P2_BLIND")) h->p2_blind = std::atoi(e) != 0;
-    // three-vector passes: parity-green but slower than the two-vector schedule at
-    // 512^3 (k_p3d issue-bound at one wave per SIMD), so opt-in
-    h->p3 = false;
-    if (const char *e = std::getenv("NLS_PASS3"))
-      h->p3 = h->p2impl == 2 && !h->collective && !h->p2_d2 && std::atoi(e) != 0;
-    h->p2grid = 0;
-    for (int J = 0; J + 1 < h->m - 1; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
+    h->p2grid = p2_grid(h);
     hip_check(h, hipMalloc(&h->p2, p2state_bytes() * h->nbasis), "hipMalloc(p2)");  // one per basis
     hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes() * h->nbasis, h->stream), "hipMemset");
     hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)),
@@ -1089,7 +1120,7 @@ bool slab_index_limit_exceeded(const nls_config &c) {
   const uint64_t P = c.dim == 3 ? (uint64_t)c.nx * c.ny : (uint64_t)c.nx;
   uint32_t z0 = 0, nzl = 0;
   if (nls_slab_planes((uint32_t)npl, c.nranks, 0, &z0, &nzl) != NLS_OK) return true;
-  return ((uint64_t)nzl + 2 * GHOST) * P + 4096 >= (uint64_t(1) << 31);
+  return ((uint64_t)nzl + 2 * GHOST_MAX) * P + 4096 >= (uint64_t(1) << 31);
 }
 
 }  // namespace
@@ -1142,8 +1173,8 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
            (uint32_t)(2 * c.nranks) > (c.dim == 3 ? c.nz : c.ny))
     why = "G2 NLSE / KG need >= 2 planes per rank";
   else if (slab_index_limit_exceeded(c))
-    why = "slab too large for 32-bit cell indices: (planes per rank + 2) * plane size + 4096 must be "
-          "< 2^31 (use more ranks)";
+    why = "slab too large for 32-bit cell indices: (planes per rank + 4) * plane size + 4096 must be "
+          "< 2^31 (two ghost planes per side; use more ranks)";
   if (!why.empty()) {
     g_create_error = why;
     return NLS_ERR_ARG;
@@ -1169,6 +1200,9 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   if (const char *e = std::getenv("NLS_RUNAHEAD"))
     h->runahead = std::min(nls_handle::RA_MAX, std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("NLS_GRAPH")) h->use_graph = std::atoi(e) != 0;
+  if (const char *e = std::getenv("NLS_OPLOG")) h->oplog_on = std::atoi(e) != 0;
+  h->dbg_sums = std::getenv("NLS_DEBUG_SUMS") != nullptr;
+  h->dbg_alpha = std::getenv("NLS_DEBUG_ALPHA") != nullptr;
   if (c.device >= 0) {
     h->dev = c.device;
   } else if (hipGetDevice(&h->dev) != hipSuccess) {
@@ -1469,6 +1503,7 @@ int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number) {
     if (!h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");
     if (step_number == 0) fail(h, NLS_ERR_ARG, "step numbers start at 1 (nlse_dev.hpp:206)");
+    h->skip_u = false;  // step 1's SS2 step writes u
     const int m = h->m;
     int64_t n = h->geo.nloc, vs = h->vs;
     const size_t bytes = (size_t)n * sizeof(cplx);
@@ -1637,6 +1672,7 @@ bool graph_ready(nls_handle *h, double dt) {
     h->gexec = nullptr;
   }
   hipGraph_t g = nullptr;
+  h->skip_u = false;  // a captured step always writes u
   hip_check(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
   try {
     issue_step(h, dt);
@@ -1670,9 +1706,14 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
         finish_step_flags(h, dt);
         h->tacc.graph_steps += 1;
       } else {
+        // u = N(y) is skipped only inside this call (another step follows); the
+        // guard clears the flag however issue_step leaves
+        struct SkipU {
+          nls_handle *h;
+          ~SkipU() { h->skip_u = false; }
+        } guard{h};
         h->skip_u = s + 1 < nsteps;
         issue_step(h, dt);
-        h->skip_u = false;
         h->p2_fresh = false;  // every basis of the step is warm now
       }
       h->tacc.steps += 1;
@@ -1874,6 +1915,16 @@ int nls_get_timing(nls_handle *h, nls_timing *out) {
     harvest_timing(h);
     *out = h->tacc;
   });
+}
+
+int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n) {
+  if (!h || !n) return NLS_ERR_ARG;
+  const uint64_t cnt = h->oplog.size() / 4;
+  *n = cnt;
+  if (!out) return NLS_OK;  // size query: the log is kept
+  std::memcpy(out, h->oplog.data(), (size_t)std::min(cnt, cap) * 4 * sizeof(int32_t));
+  h->oplog.clear();
+  return NLS_OK;
 }
 
 int nls_reset_timing(nls_handle *h) {

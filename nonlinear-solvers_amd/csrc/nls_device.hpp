@@ -62,6 +62,8 @@ struct Geo {
   int32_t kz;     // planes (3D) / rows per wave (2D) per tile of the stencil kernels
   int32_t remap;  // 1: XCD-banded tile order (speed only)
   int32_t qa, qb; // local planes [qa, qb) covered by a stencil launch (default 0, nzl)
+  int32_t q2;     // k_p2d only: > 0 adds the range [q2, q2 + qb - qa) to the launch (the two
+                  // boundary plane pairs of a split multi-rank pass in one grid); 0: none
   const double *cf;  // G2 anisotropic operator: c field at local plane 0 (ghost planes at
                      // -P and nzl*P, like a basis vector); unused by the isotropic operator
 };

@@ -27,7 +27,6 @@
 #include "nls_stencil.hpp"
 #include "nls_pass2.hpp"
 #include "nls_pass2d.hpp"
-#include "nls_pass3d.hpp"
 
 namespace nls {
 
@@ -820,13 +819,11 @@ const void *kernel_sg_end(int M) {
   }
 }
 
-// two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp): even J only.
-// impl 2: LDS-DMA form k_p2d (J <= P2D_JMAX; d2: a 2D grid as planes of 4 rows; pr: a
-// real 2D field as pairs of cells);
-// 1: register-march k_pass2r (3D)
-const void *kernel_pass2(int J, bool hz, int impl, bool d2, bool pr) {
-  if (impl == 2) {
-    switch (J) {
+// two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp): the LDS-DMA pass
+// k_p2d at even J <= P2D_JMAX; d2: a 2D grid as planes of 4 rows; pr: a real 2D
+// field as pairs of cells
+const void *kernel_pass2(int J, bool hz, bool d2, bool pr) {
+  switch (J) {
 #define X(J)                                                                                       \
   case J:                                                                                          \
     if (pr)                                                                                        \
@@ -835,25 +832,8 @@ const void *kernel_pass2(int J, bool hz, int impl, bool d2, bool pr) {
     return d2 ? (hz ? reinterpret_cast<const void *>(&k_p2d<J, true, true>)                        \
                     : reinterpret_cast<const void *>(&k_p2d<J, false, true>))                      \
               : (hz ? reinterpret_cast<const void *>(&k_p2d<J, true>) : reinterpret_cast<const void *>(&k_p2d<J, false>));
-      X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14)
+    X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14)
 #undef X
-      default: return nullptr;
-    }
-  }
-  if (d2 || pr) return nullptr;
-  switch (J) {
-#define X(J) \
-  case J: return hz ? reinterpret_cast<const void *>(&k_pass2r<J, true>) : reinterpret_cast<const void *>(&k_pass2r<J, false>);
-    X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30)
-#undef X
-    default: return nullptr;
-  }
-}
-// three-vector passes (nls_pass3d.hpp): the s-step schedule's J = 2 and 5
-const void *kernel_pass3(int J) {
-  switch (J) {
-    case 2: return reinterpret_cast<const void *>(&k_p3d<2>);
-    case 5: return reinterpret_cast<const void *>(&k_p3d<5>);
     default: return nullptr;
   }
 }
@@ -864,7 +844,6 @@ static_assert(offsetof(P2State, bZ2) == offsetof(P2State, bZ1) + sizeof(cplx) &&
 const void *kernel_p2tail() { return reinterpret_cast<const void *>(&k_p2tail); }
 const void *kernel_p2tfin() { return reinterpret_cast<const void *>(&k_p2tfin); }
 const void *kernel_p2coef() { return reinterpret_cast<const void *>(&k_p2coef); }
-const void *kernel_p2fin() { return reinterpret_cast<const void *>(&k_p2fin); }
 size_t p2state_bytes() { return sizeof(P2State); }
 size_t p2state_sums_offset() { return offsetof(P2State, sums); }
 

@@ -59,20 +59,13 @@ const void *kernel_reduce_final();
 //                  grid = ncA + ncU columns; dst = KState::sums (the do_sum phase, parallel)
 const void *kernel_colsum();
 // two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp; 3D isotropic complex, single rank)
-//   pass2 : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb[, const cplx* zbuf])
-const void *kernel_pass2(int J, bool hz, int impl, bool d2 = false, bool pr = false);  // hz: also Z; impl 2: LDS-DMA k_p2d, 1: k_pass2r
+//   pass2 : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* zbuf, int poff)
+const void *kernel_pass2(int J, bool hz, bool d2 = false, bool pr = false);  // hz: also Z (k_p2d)
 constexpr int P2D_WAVE_XO = 64, P2D_ROWS = 4, P2D_MAXJ = 14;  // == P2D_XO, P2D_TR, P2D_JMAX
 //   p2tail: (P2State*, KState*, const cplx* sums, int m);  p2tfin: (const P2State*, KState*, int m, int nf)
 const void *kernel_p2tail();
 const void *kernel_p2tfin();
-constexpr int P2R_WAVE_XO = 60;  // == P2R_XO
-#ifndef NLS_P2R_RB1
-#define NLS_P2R_RB1 12  // k_pass2r: one row per wave from this J (registers)
-#endif
-#define P2R_ROWS(J) (((J) == 4 || (J) >= NLS_P2R_RB1) ? 1 : 2)  // 512^3: J=4 3.92 vs 4.90 ms with one row
 const void *kernel_p2coef();  // (P2State*, KState*, int J, int mode, int ns, int nsn)
-const void *kernel_pass3(int J);  // k_p3d<J>, J = 2, 5 (same arguments as kernel_pass2's impl 2)
-const void *kernel_p2fin();
 size_t p2state_bytes();
 size_t p2state_sums_offset();
 

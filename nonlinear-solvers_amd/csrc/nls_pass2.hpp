@@ -31,171 +31,9 @@ struct P2State {
   int32_t blind;  // the J = 0 pass ran on the raw start vector (mode 2), beta from its sums
 };
 
-// Register-march form of the same pass (the LDS-DMA form k_p2d, nls_pass2d.hpp, is the default).  Each
-// wave owns a column of 64 lanes x P2R_RB rows and marches z on its own, no LDS,
-// no barriers: lanes hold x = 60 xt - 2 + lane, of which lanes 2..61 are outputs
-// and lanes 0,1,62,63 the x halo (x neighbours by lane shuffles; L S_J is valid
-// on lanes 1..62, L^2 S_J on 2..61).  Register queues: S_J on rows -2..RB+1 for
-// planes k-1..k+1, L S_J on rows -1..RB for planes k-2..k.  Step k loads
-// S_J(k+1) and the J other streams of plane k-1, forms L S_J(k), then
-// L^2 S_J(k-1) and the outputs of plane k-1.
-constexpr int p2r_rb(int J) { return P2R_ROWS(J); }  // rows per wave (registers; measured per J)
-constexpr int P2R_XO = 60;  // output x per wave
-template <int J, bool HZ>
-__global__ __launch_bounds__(NTHREADS) void k_pass2r(cplx *__restrict__ W, int64_t vs, Geo g,
-                                                     const P2State *__restrict__ ps,
-                                                     cplx *__restrict__ part, int nb) {
-  constexpr int RB = p2r_rb(J), SR = RB + 4, LR = RB + 2;
-  // columns: gX[0..J], then HZ: gZ[0..J], X^H X, X^H Z, Z^H Z; else X^H X.  (Deriving
-  // S_l^H Z, l < J, from gX through the Arnoldi relation instead loses ~1e-7 absolute
-  // at ||L|| ~ 1e2 -- the relation's rounding times ||L|| ||X|| -- measured, not kept.)
-  constexpr int NC = HZ ? 2 * (J + 1) + 3 : J + 2;
-  __shared__ cplx red[NTHREADS / 64][NC];
-  __shared__ cplx cX[J + 1], cZ[J + 1];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int nx = (int)g.nx, ny = (int)g.nyp, P = (int)g.P, nz = (int)g.npl;
-  const int ntx = (nx + P2R_XO - 1) / P2R_XO, nry = ny / RB;
-  const int nzc = (nz + g.kz - 1) / g.kz;
-  for (int l = t; l <= J; l += NTHREADS) {
-    cX[l] = ps->aX[l];
-    cZ[l] = ps->aZ[l];
-  }
-  __syncthreads();
-  const cplx bX1 = ps->bX1, bZ1 = ps->bZ1, bZ2 = ps->bZ2;
-  const double s = g.s, sdi = g.sd_in, sdb = g.sd_bd;
-  const cplx *__restrict__ SJ = W + (int64_t)J * vs;
-  cplx *__restrict__ Xo = W + (int64_t)(J + 1) * vs;
-  cplx *__restrict__ Zo = W + (int64_t)(J + 2) * vs;
-  const volatile cplx *vX = cX, *vZ = cZ;
-  auto ldc = [](const volatile cplx *p) { return cplx{p->re, p->im}; };
-  cplx acc[NC];
-#pragma unroll
-  for (int i = 0; i < NC; ++i) acc[i] = {0.0, 0.0};
-  const int wid = blockIdx.x * (NTHREADS / 64) + w;
-  if (wid < ntx * nry * nzc) {  // uniform per wave
-    const int xt = wid % ntx, yt = (wid / ntx) % nry, zc = wid / (ntx * nry);
-    const int x = xt * P2R_XO - 2 + lane, y0 = yt * RB;
-    const int k0 = zc * g.kz, k1 = min(k0 + g.kz, nz);
-    const bool xin = x >= 0 && x < nx;
-    const bool out = lane >= 2 && lane < 62 && x < nx;
-    // true plane / row of row yy (-2..ny+1) of plane k; diagonal of a cell
-    auto plane_of = [&](int k, int yy) { return yy < 0 ? k - 1 : (yy >= ny ? k + 1 : k); };
-    auto row_of = [&](int yy) { return yy < 0 ? yy + ny : (yy >= ny ? yy - ny : yy); };
-    auto dg = [&](int j, int kk) {
-      const bool bd = x == 0 || x == nx - 1 || j == 0 || j == ny - 1 || kk == 0 || kk == nz - 1;
-      return bd ? sdb : sdi;
-    };
-    auto ldS = [&](int k, int yy) {
-      const int kk = plane_of(k, yy);
-      cplx v = {0.0, 0.0};
-      if (xin && kk >= 0 && kk < nz) v = SJ[k * P + yy * nx + x];
-      return v;
-    };
-    cplx sq[3][SR], lq[3][LR];
-#pragma unroll
-    for (int r = 0; r < SR; ++r) {
-      sq[0][r] = ldS(k0 - 2, y0 - 2 + r);
-      sq[1][r] = ldS(k0 - 1, y0 - 2 + r);
-      sq[2][r] = {0.0, 0.0};
-    }
-#pragma unroll
-    for (int r = 0; r < LR; ++r) lq[0][r] = lq[1][r] = lq[2][r] = {0.0, 0.0};
-    // step k: sq[0] = plane k-1, sq[1] = plane k, load sq[2] = plane k+1;
-    //         lq[1..2] = L1 planes k-2, k-1 -> shifted, lq[2] = L1(k); outputs at plane k-1
-#pragma unroll 1
-    for (int k = k0 - 1; k <= k1; ++k) {
-#pragma unroll
-      for (int r = 0; r < SR; ++r) sq[2][r] = ldS(k + 1, y0 - 2 + r);
-      const bool emit = k - 1 >= k0;
-      // the J other streams of the first output row, in flight during the L1 step
-      cplx sv[J + 1];
-      {
-        const int flat = (k - 1) * P + y0 * nx + x;
-#pragma unroll
-        for (int l = 0; l < J; ++l) sv[l] = (emit && out) ? ld_nt(W + l * vs + flat) : cplx{0.0, 0.0};
-      }
-      // L1 at plane k, rows y0-1 .. y0+RB (S rows 1 .. RB+2)
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const cplx c = sq[1][r + 1];
-        cplx xm = shfl_up1(c), xp = shfl_dn1(c);
-        if (x == 0) xm = {0.0, 0.0};
-        if (x == nx - 1) xp = {0.0, 0.0};
-        const int yy = y0 - 1 + r, kk = plane_of(k, yy);
-        cplx v = {0.0, 0.0};
-        if (xin && kk >= 0 && kk < nz) {
-          const cplx nbs = xm + xp + sq[1][r] + sq[1][r + 2] + sq[0][r + 1] + sq[2][r + 1];
-          v = dg(row_of(yy), kk) * c + s * nbs;
-        }
-        lq[0][r] = lq[1][r];
-        lq[1][r] = lq[2][r];
-        lq[2][r] = v;
-      }
-      // lq[0] = L1(k-2), lq[1] = L1(k-1), lq[2] = L1(k): outputs at plane k-1
-      if (emit) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const int flat = (k - 1) * P + (y0 + r) * nx + x;
-          if (r > 0) {
-#pragma unroll
-            for (int l = 0; l < J; ++l) sv[l] = out ? ld_nt(W + l * vs + flat) : cplx{0.0, 0.0};
-          }
-          sv[J] = sq[0][r + 2];
-          const cplx l1 = lq[1][r + 1];
-          cplx X = cmul(bX1, l1);
-#pragma unroll
-          for (int l = 0; l <= J; ++l) X += cmul(ldc(vX + l), sv[l]);
-          cplx Z = {0.0, 0.0};
-          if constexpr (HZ) {
-            cplx xm = shfl_up1(l1), xp = shfl_dn1(l1);
-            if (x == 0) xm = {0.0, 0.0};
-            if (x == nx - 1) xp = {0.0, 0.0};
-            const cplx nbs = xm + xp + lq[1][r] + lq[1][r + 2] + lq[0][r + 1] + lq[2][r + 1];
-            const cplx l2 = dg(y0 + r, k - 1) * l1 + s * nbs;
-            Z = cmul(bZ2, l2) + cmul(bZ1, l1);
-#pragma unroll
-            for (int l = 0; l <= J; ++l) Z += cmul(ldc(vZ + l), sv[l]);
-          }
-          if (out) {
-#pragma unroll
-            for (int l = 0; l <= J; ++l) acc[l] += cj_mul(sv[l], X);
-            st_nt(Xo + flat, X);
-            if constexpr (HZ) {
-#pragma unroll
-              for (int l = 0; l <= J; ++l) acc[J + 1 + l] += cj_mul(sv[l], Z);
-              acc[2 * J + 2].re += abs2(X);
-              acc[2 * J + 3] += cj_mul(X, Z);
-              acc[2 * J + 4].re += abs2(Z);
-              st_nt(Zo + flat, Z);
-            } else {
-              acc[J + 1].re += abs2(X);
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < SR; ++r) {
-        sq[0][r] = sq[1][r];
-        sq[1][r] = sq[2][r];
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const double a = wave_sum(acc[i].re), b = wave_sum(acc[i].im);
-    if (lane == 0) red[w][i] = {a, b};
-  }
-  __syncthreads();
-  for (int i = t; i < NC; i += NTHREADS) {
-    cplx v = red[0][i];
-    for (int q = 1; q < NTHREADS / 64; ++q) v += red[q][i];
-    part[(int64_t)i * nb + blockIdx.x] = v;
-  }
-}
-
 // Coefficient kernel (one workgroup).  A pass at J writes ns = 1, 2 or 3 new
 // vectors V_1 = L W_J - sigma W_J - sum_{k<J} conj(H[J][k]) W_k, V_{i+1} = (L - sigma) V_i
-// (k_p2d: ns <= 2, k_p3d: ns = 3) and reduces, in this order, S_l^H V_i (l <= J, per i)
+// (k_p2d: ns <= 2; the recurrences also hold for ns = 3, tests/sstep_model.py) and reduces, in this order, S_l^H V_i (l <= J, per i)
 // and the Gram V_a^H V_b (a <= b, row by row); J = 0 of a blind start also ||S_0||^2.
 // mode 0: start (after the alpha pass and reduction of W_0: s[0] = beta, H[0][0] =
 // alpha_0); mode 2: blind start, no alpha pass: the J = 0 pass runs on the raw start
@@ -205,7 +43,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pass2r(cplx *__restrict__ W, int64
 // columns, summed).  Computes the new columns of C, D, H (tests/sstep_model.py
 // coef_update) and, for a next pass of nsn > 0 vectors at J' = J + ns, its
 // coefficients (pass_coefficients); nsn = 0: T into the KState for k_reduce_final
-// (s[] = 1, so fin is in the W basis; k_p2fin converts it).  real: the sums come
+// (s[] = 1, so fin is in the W basis; k_p2tfin converts it).  real: the sums come
 // from a real field marched as cell pairs; their imaginary parts are dropped.
 __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, KState *__restrict__ st,
                                                      int J, int mode, int ns, int nsn, int real) {
@@ -393,21 +231,6 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       st->To[t] = ps->H[t + 1][t].re;
     }
     st->s[t] = 1.0;
-  }
-}
-
-// fin (W basis, from k_reduce_final) -> S basis: fin_S = beta C fin_W
-__global__ __launch_bounds__(NTHREADS) void k_p2fin(const P2State *__restrict__ ps,
-                                                    KState *__restrict__ st, int m, int nf) {
-  __shared__ cplx fw[2][MMAX];
-  const int t = threadIdx.x;
-  for (int e = t; e < nf * m; e += NTHREADS) fw[e / m][e % m] = st->fin[e / m][e % m];
-  __syncthreads();
-  for (int e = t; e < nf * m; e += NTHREADS) {
-    const int f = e / m, l = e % m;
-    cplx v = {0.0, 0.0};
-    for (int i = l; i < m; ++i) v += cmul(ps->C[l][i], fw[f][i]);
-    st->fin[f][l] = ps->beta * v;
   }
 }
 

@@ -4,8 +4,8 @@
 //
 // Why a new form: the pass holds 2(J+1)+3 complex accumulators per lane, so
 // with the streamed S_l in VGPRs it runs at one wave per SIMD with too few
-// bytes in flight (the register-march k_pass2r streamed at ~55 % of the
-// pattern's rate).  Here every byte the pass reads moves HBM -> LDS by
+// bytes in flight (a register-march form streamed at ~55 % of the pattern's
+// rate; measured in round 2 and removed).  Here every byte the pass reads moves HBM -> LDS by
 // global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR destination),
 // issued ahead of its use, so the in-flight bytes no longer compete
 // with the accumulators for registers:
@@ -183,8 +183,9 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// Output planes [g.qa, g.qb) of the slab (multi-rank handles launch the two
-// boundary plane pairs apart from the interior, so the halo exchange overlaps);
+// Output planes [g.qa, g.qb) of the slab, plus [g.q2, g.q2 + qb - qa) when g.q2 > 0
+// (multi-rank handles launch the two boundary plane pairs as one grid apart from
+// the interior, so the halo exchange overlaps);
 // partial sums at part[c * nb + poff + blockIdx.x].
 // D2: a 2D [ny][nx] grid seen as planes of 4 rows (g: nyp = 4, npl = ny/4, P = 4 nx):
 // the row-wrap of the 3D march is then exactly the 2D y neighbour, the plane
@@ -225,7 +226,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   const int nzl = (int)g.nzl, z0 = (int)g.z0;
   const int ntx = (nx + P2D_XO - 1) / P2D_XO, nty = ny / P2D_TR;
   const int qa = g.qa, qb = g.qb;
-  const int nzc = (qb - qa + g.kz - 1) / g.kz;
+  // z chunks of [qa, qb), and with g.q2 > 0 as many again of [q2, q2 + qb - qa)
+  const int nz1 = (qb - qa + g.kz - 1) / g.kz;
+  const int nzc = g.q2 > 0 ? 2 * nz1 : nz1;
   const int ntiles = ntx * nty * nzc;
   // XCD-banded order: the 8 XCDs take contiguous tile ranges, so the y-adjacent
   // tiles sharing S_J halo rows run on one XCD (its L2) at the same time
@@ -233,7 +236,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   const int tile = b < 8 * T8 ? (b % 8) * T8 + b / 8 : b;
   const int yt = tile % nty, rest = tile / nty, xt = rest % ntx, zc = rest / ntx;
   const int x0 = xt * P2D_XO, y0 = yt * P2D_TR;
-  const int k0 = qa + zc * g.kz, k1 = min(k0 + g.kz, qb);
+  const bool hi = g.q2 > 0 && zc >= nz1;  // uniform
+  const int za = hi ? g.q2 : qa, zb = hi ? g.q2 + (qb - qa) : qb;
+  const int k0 = za + (hi ? zc - nz1 : zc) * g.kz, k1 = min(k0 + g.kz, zb);
   const int x = x0 + lane;
   const bool xin = x < nx;
   const bool full = x0 + P2D_XO <= nx;                    // uniform

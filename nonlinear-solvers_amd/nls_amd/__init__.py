@@ -37,8 +37,10 @@ EXPORTED_SYMBOLS = (
     "nls_rccl_unique_id", "nls_group_create", "nls_group_destroy", "nls_set_timing",
     "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
     "nls_get_field_async", "nls_wait_field", "nls_host_alloc", "nls_host_free", "nls_slab_planes",
-    "nls_step_sewi",
+    "nls_step_sewi", "nls_debug_oplog",
 )
+# nls_debug_oplog entry kinds (include/nls.h enum nls_op_kind)
+OP_ALLREDUCE, OP_SEND, OP_RECV, OP_WAIT_HALO, OP_WAIT_COMPUTE = 1, 2, 3, 4, 5
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
@@ -121,7 +123,8 @@ def lib():
     L.nls_set_timing.argtypes = [H, C.c_int32]
     L.nls_get_timing.argtypes = [H, C.POINTER(Timing)]
     L.nls_reset_timing.argtypes = [H]
-    if L.nls_abi_version() != 4:
+    L.nls_debug_oplog.argtypes = [H, C.POINTER(C.c_int32), C.c_uint64, C.POINTER(C.c_uint64)]
+    if L.nls_abi_version() != 5:
         raise RuntimeError("libnls_amd ABI mismatch")
     _LIB = L
     return L
@@ -329,6 +332,16 @@ class Solver:
 
     def reset_timing(self):
         self._call(lib().nls_reset_timing)
+
+    def oplog(self) -> list[tuple[int, int, int, int]]:
+        """Transport operations since the last call, in issue order, as
+        (kind, stream, count, peer) (nls_debug_oplog; recorded with NLS_OPLOG=1 at
+        creation)."""
+        n = C.c_uint64()
+        self._call(lib().nls_debug_oplog, None, 0, C.byref(n))  # size only
+        buf = (C.c_int32 * (4 * max(1, n.value)))()
+        self._call(lib().nls_debug_oplog, buf, n.value, C.byref(n))  # copies and clears
+        return [tuple(buf[4 * i:4 * i + 4]) for i in range(n.value)]
 
     def timing(self) -> dict:
         t = Timing()

@@ -32,13 +32,58 @@ def rel():
 # "parity floor"): on smooth data over fine grids, or at ||L|| dt >> m, the
 # Lanczos basis amplifies rounding noise in the high modes by roughly
 # prod_j ||L|| / beta_j per action, and the SS2 map carries that growth from
-# step to step.  Two faithful CPU restatements of the reference (the C oracle,
-# MGS + cyclic Jacobi, and the numpy twin, MGS + LAPACK eigh) then drift apart
-# exponentially although each is "exact".  A GPU trajectory is held to the
-# north_star tolerance where that floor is below it, and to FLOOR_FACTOR times
-# the floor where the reference algorithm itself cannot resolve 1e-10.
+# step to step.  The floor is measured on the ORACLE ITSELF: the same oracle
+# trajectory from an initial field perturbed by one ulp per component
+# (perturb_ulp, two seeds; self_floor).  Where it exceeds the north_star
+# tolerance the reference algorithm cannot resolve 1e-10 on that problem, and a
+# GPU trajectory is held to FLOOR_FACTOR x that floor instead.
 FLOOR_FACTOR = 10.0
 
 
 def parity_bound(tol, floor):
     return max(tol, FLOOR_FACTOR * floor)
+
+
+def perturb_ulp(u, seed):
+    """u with every real and imaginary component moved by about one ulp
+    (relative 2^-52 Gaussian noise): the size of one rounding error."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    u = np.asarray(u)
+    e = 2.0 ** -52
+    if np.iscomplexobj(u):
+        return (u.real * (1 + e * rng.standard_normal(u.shape))
+                + 1j * u.imag * (1 + e * rng.standard_normal(u.shape)))
+    return u * (1 + e * rng.standard_normal(u.shape))
+
+
+def self_floor(run, u0, seeds=(101, 202)):
+    """Per checkpoint, the largest distance between the oracle run `run(u0)` and
+    the oracle runs from one-ulp perturbations of u0.  run returns a dict
+    {checkpoint: field} (or a list of snapshots); so does self_floor."""
+    # the runs are independent oracle calls (ctypes releases the GIL): in parallel
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=1 + len(seeds)) as ex:
+        futs = [ex.submit(run, u0)] + [ex.submit(run, perturb_ulp(u0, sd)) for sd in seeds]
+        base, others = futs[0].result(), [f.result() for f in futs[1:]]
+    keys = list(base.keys()) if isinstance(base, dict) else list(range(len(base)))
+    fl = {k: 0.0 for k in keys}
+    for other in others:
+        for k in keys:
+            fl[k] = max(fl[k], rel_l2(other[k], base[k]))
+    return base, fl
+
+
+def record_parity(case, rows):
+    """Append one case's per-checkpoint parity record to $NLS_PARITY_LOG (JSON
+    lines; tools/parity_floor.py formats profiles/<round>/parity_floor.txt).
+    rows: [(checkpoint, gpu_err, self_floor, twin_floor or None)]."""
+    path = os.environ.get("NLS_PARITY_LOG")
+    if not path:
+        return
+    import json
+    with open(path, "a") as f:
+        f.write(json.dumps({"case": case, "rows": [
+            {"checkpoint": k, "gpu_err": e, "self_floor": sf, "twin_floor": tf,
+             "bound": parity_bound(1e-10, sf), "ratio_gpu_self": (e / sf) if sf > 0 else None}
+            for k, e, sf, tf in rows]}) + "\n")

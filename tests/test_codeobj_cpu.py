@@ -1,0 +1,56 @@
+"""CPU: the hand-counted vmcnt schedule of k_p2d holds in the compiled gfx950 code
+object (tests/codeobj.py; nls_pass2d.hpp:30-38, p2d_after / wait_step).  For every
+k_p2d<J, HZ, D2, PR> instantiation: no scratch / buffer / flat access, no private
+segment, no VGPR spill; the march loop issues exactly the source's DMA loads and
+stores; and its s_waitcnt vmcnt values are exactly the source's p2d_after values."""
+import os
+
+import pytest
+
+import codeobj as C
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "nonlinear-solvers_amd", "lib", "libnls_amd.so")
+HDR = os.path.join(ROOT, "nonlinear-solvers_amd", "csrc", "nls_pass2d.hpp")
+
+pytestmark = pytest.mark.skipif(not (C.available() and os.path.exists(LIB)),
+                                reason="ROCm llvm tools or the built library missing")
+
+
+@pytest.fixture(scope="module")
+def p2d_results(tmp_path_factory):
+    sched = C.P2dSchedule(HDR)
+    out = []
+    for co in C.gfx950_objects(LIB, str(tmp_path_factory.mktemp("co"))):
+        funcs = C.disassemble(co)
+        if any(C.p2d_params(n) for n in funcs):
+            out += C.check_p2d(funcs, C.metadata(co), sched)
+    return out
+
+
+def test_every_p2d_instantiation_found(p2d_results):
+    got = {(r["J"], r["HZ"], r["D2"], r["PR"]) for _n, _p, r in p2d_results}
+    want = {(J, hz, d2, pr) for J in range(0, 16, 2) for hz in (0, 1) for d2, pr in ((0, 0), (1, 0), (1, 1))}
+    assert got == want
+
+
+def test_p2d_vmcnt_contract_holds(p2d_results):
+    bad = [(r["J"], r["HZ"], r["D2"], r["PR"], p) for _n, p, r in p2d_results if p]
+    assert not bad, bad
+
+
+def test_checker_flags_an_extra_vmem_op():
+    """The loop check is not vacuous: one more load in a synthetic loop body fails it."""
+    sched = C.P2dSchedule(HDR)
+    name = "_ZN3nls5k_p2dILi2ELb1ELb0ELb0EEEv"
+    body = [(0x100, "s_waitcnt", "vmcnt(4)")] + \
+        [(0x104 + 4 * i, "global_load_lds_dwordx4", "v[2:3], off") for i in range(4)] + \
+        [(0x120, "global_load_lds_dword", ""), (0x124, "global_load_lds_dword", ""),
+         (0x128, "global_store_dwordx4", ""), (0x12c, "global_store_dwordx4", ""),
+         (0x130, "s_cbranch_scc1", f"<{name}+0x100>")]
+    ins = [(0x0, "s_load_dwordx2", "")] + body
+    md = {name: {"private_segment_fixed_size": "0", "vgpr_spill_count": "0"}}
+    assert C.check_p2d({name: ins}, md, sched)[0][1] == []
+    extra = ins[:-1] + [(0x12e, "scratch_load_dword", "v1, off"), ins[-1]]
+    probs = C.check_p2d({name: extra}, md, sched)[0][1]
+    assert probs and any("scratch" in p for p in probs)

@@ -1,9 +1,9 @@
 """GPU parity of the two-vectors-per-pass Lanczos (NLS_PASS2=1, nls_pass2.hpp,
 nls_pass2d.hpp): 3D isotropic NLSE trajectories against the CPU oracle, with the
-same tolerances as tests/test_gpu_parity.py, for both forms of the pass (LDS-DMA
-k_p2d, register march k_pass2r).  Every run ends each basis in the fused tail
-(k_alpha_l2 over S_{m-2}, k_p2tail, k_tail).  k_p2d takes 4-row tiles (ny % 4 == 0)
-and m <= 18; k_pass2r 64-aligned x; other shapes fall back to the other form."""
+same tolerances as tests/test_gpu_parity.py, for the LDS-DMA pass k_p2d.  Every
+run ends each basis in the fused tail (k_alpha_l2 over S_{m-2}, k_p2tail, k_tail).
+k_p2d takes 4-row tiles (ny % 4 == 0) and m <= 18; other shapes run the one-vector
+passes."""
 import numpy as np
 import pytest
 
@@ -18,28 +18,21 @@ nls_amd = pytest.importorskip("nls_amd")
 TOL_KRYLOV, TOL_TRAJ = 1e-12, 1e-10
 
 
-@pytest.fixture(autouse=True, params=["dma", "dma3", "reg"])
-def _pass2(monkeypatch, request):
-    """dma: the default two-vector passes (k_p2d); dma3: the s-step schedule with
-    three-vector k_p3d passes at J = 2, 5 from m = 10 (NLS_PASS3=1); reg: the
-    register march (k_pass2r)."""
+@pytest.fixture(autouse=True)
+def _pass2(monkeypatch):
+    """The two-vector passes (k_p2d) with several z chunks per column of tiles."""
     monkeypatch.setenv("NLS_PASS2", "1")
-    monkeypatch.setenv("NLS_P2_KZ", "8")  # several z chunks per column of tiles
-    monkeypatch.setenv("NLS_P2_IMPL", "1" if request.param == "reg" else "2")
-    monkeypatch.setenv("NLS_PASS3", "1" if request.param == "dma3" else "0")
-    return request.param
+    monkeypatch.setenv("NLS_P2_KZ", "8")
 
 
-def _eligible(form, nx, ny, m):
-    """Does the handle run the two-vector pass (nls_api.cpp alloc_all)?  dma falls
-    back to the register march where its tiles do not fit, reg never falls back."""
-    reg = nx % 64 == 0 and ny % 2 == 0
-    return reg if form == "reg" else ((ny % 4 == 0 and m <= 18) or reg)
+def _eligible(nx, ny, m):
+    """Does the handle run the two-vector pass (nls_api.cpp alloc_all)?"""
+    return ny % 4 == 0 and m <= 18
 
 
 def _ran_pass2(s, m):
-    """s-step pass launches are timed at their start J (0, 2, then even J, or 5 after a
-    three-vector pass at 2); the plain path times every j."""
+    """s-step pass launches are timed at their start J (0, 2, 4, ...); the plain path
+    times every j."""
     t = s.timing()
     cnt = t["update_count"]
     return cnt[0] > 0 and cnt[1] == 0  # s-step passes start at J = 0, 2, (5,) ... never at 1
@@ -49,7 +42,7 @@ def _ran_pass2(s, m):
                                         (64, 16, 16, 25), (64, 16, 10, 3), (64, 48, 8, 4),
                                         (64, 20, 11, 18), (50, 12, 13, 16), (130, 8, 9, 5)])
 @pytest.mark.parametrize("eq", [0, 1])
-def test_pass2_trajectory_matches_oracle(_pass2, nx, ny, nz, m, eq):
+def test_pass2_trajectory_matches_oracle(nx, ny, nz, m, eq):
     L = 10.0
     dx = spacing(nx, L)
     u0 = soliton_field(3, nx, ny, nz, L, seed=11)
@@ -62,10 +55,7 @@ def test_pass2_trajectory_matches_oracle(_pass2, nx, ny, nz, m, eq):
         s.set_timing(True)
         s.step(dt, nsteps)
         u = s.get_field()
-        assert _ran_pass2(s, m) == _eligible(_pass2, nx, ny, m)
-        cnt = s.timing()["update_count"]
-        three = _pass2 == "dma3" and ny % 4 == 0 and 10 <= m <= 18
-        assert (cnt[5] > 0 and cnt[4] == 0) == three  # k_p3d at J = 2 and 5
+        assert _ran_pass2(s, m) == _eligible(nx, ny, m)
     assert np.all(np.isfinite(u))
     assert rel_l2(u, ref) <= TOL_TRAJ
 
@@ -86,11 +76,9 @@ def test_pass2_one_step_matches_plain_path(monkeypatch, L):
 
 
 @pytest.mark.parametrize("eq", [0, 1])
-def test_multi_step_call_equals_single_steps(_pass2, eq):
+def test_multi_step_call_equals_single_steps(eq):
     """The NLSE tail writes u only on the last step of an nls_step call (the other steps
     write just the next start vector): one 5-step call equals five 1-step calls bitwise."""
-    if _pass2 != "dma":
-        pytest.skip("one form is enough")
     nx, ny, nz, m = 64, 16, 12, 16
     dx = spacing(nx, 10.0)
     u0 = soliton_field(3, nx, ny, nz, 10.0, seed=3)
@@ -107,14 +95,14 @@ def test_multi_step_call_equals_single_steps(_pass2, eq):
 # ---- 2D: k_p2d on planes of 4 rows (nls_api.cpp p2_geo; one rank, ny % 4 == 0) ----
 
 
-def _eligible2d(form, ny, m):
-    return form != "reg" and ny % 4 == 0 and ny >= 8 and m <= 18
+def _eligible2d(ny, m):
+    return ny % 4 == 0 and ny >= 8 and m <= 18
 
 
 @pytest.mark.parametrize("nx,ny,m", [(64, 64, 16), (300, 20, 10), (50, 12, 16), (130, 8, 5), (70, 66, 16),
                                      (64, 40, 3), (96, 36, 17)])
 @pytest.mark.parametrize("eq", [0, 1])
-def test_pass2_2d_trajectory_matches_oracle(_pass2, nx, ny, m, eq):
+def test_pass2_2d_trajectory_matches_oracle(nx, ny, m, eq):
     """The 2D row neighbours are the march's row wrap across planes of 4 rows; the plane
     neighbours are dropped; boundary rows are 2D rows 0 and ny-1 (x edges as in 3D)."""
     L = 10.0
@@ -131,16 +119,14 @@ def test_pass2_2d_trajectory_matches_oracle(_pass2, nx, ny, m, eq):
         s.step(dt, nsteps)
         u = s.get_field()
         if m > 3:  # at m = 3 both paths launch one update at J = 0: not telling
-            assert _ran_pass2(s, m) == _eligible2d(_pass2, ny, m)
+            assert _ran_pass2(s, m) == _eligible2d(ny, m)
     assert np.all(np.isfinite(u))
     assert rel_l2(u, ref) <= TOL_TRAJ
 
 
 @pytest.mark.parametrize("n", [256, 512])
-def test_pass2_2d_stiff_matches_oracle(_pass2, n):
+def test_pass2_2d_stiff_matches_oracle(n):
     """C2's spacing (dx = 20/4095, ||L|| dt ~ 1.7e2) on a grid the oracle runs in seconds."""
-    if _pass2 == "reg":
-        pytest.skip("2D has the LDS-DMA form only")
     dx = 20.0 / 4095
     u0 = soliton_field(2, n, n, 1, n * dx / 2, seed=13)
     g = O.grid(2, n, n, 1, dx, dx)
@@ -157,13 +143,13 @@ def test_pass2_2d_stiff_matches_oracle(_pass2, n):
 # ---- real 2D Gautschi (sine-Gordon G1 and the G2 family): k_p2d on cell pairs ----
 
 
-def _eligible_pr(form, nx, ny, m):
-    return form != "reg" and nx % 2 == 0 and nx >= 4 and ny % 4 == 0 and ny >= 8 and m <= 18
+def _eligible_pr(nx, ny, m):
+    return nx % 2 == 0 and nx >= 4 and ny % 4 == 0 and ny >= 8 and m <= 18
 
 
 @pytest.mark.parametrize("nx,ny,m", [(64, 64, 10), (50, 12, 10), (130, 16, 16), (66, 40, 5), (7, 8, 10),
                                      (30, 22, 10), (96, 36, 3)])
-def test_pass2_sg_trajectory_matches_oracle(_pass2, nx, ny, m):
+def test_pass2_sg_trajectory_matches_oracle(nx, ny, m):
     """sg_solver_dev.hpp:168-193: two bases per step (id/cos of u, sinc^2 of g(u)), both
     by two-vector passes on cell pairs (the x neighbours cross the pair; real dots =
     the real parts of the pair dots)."""
@@ -185,12 +171,12 @@ def test_pass2_sg_trajectory_matches_oracle(_pass2, nx, ny, m):
         s.step(dt, 12)
         u = s.get_field()
         if m > 3:
-            assert _ran_pass2(s, m) == _eligible_pr(_pass2, nx, ny, m)
+            assert _ran_pass2(s, m) == _eligible_pr(nx, ny, m)
     assert rel_l2(u, ref_u) <= TOL_TRAJ
 
 
 @pytest.mark.parametrize("kind", sorted(O.GG_KINDS))
-def test_pass2_gautschi_g2_with_bc_matches_oracle(_pass2, kind):
+def test_pass2_gautschi_g2_with_bc_matches_oracle(kind):
     """phi4 / sg_single / sg_double / sg_hyperbolic (G2, m(x), BC after every step)."""
     eq = {"phi4": nls_amd.PHI4, "sg": nls_amd.SG_G2, "sg_double": nls_amd.SG_DOUBLE,
           "sg_hyperbolic": nls_amd.SG_HYPERBOLIC}[kind]
@@ -210,14 +196,12 @@ def test_pass2_gautschi_g2_with_bc_matches_oracle(_pass2, kind):
             s.step(dt, 1)
             s.apply_bc()
         u = s.get_field()
-        assert _ran_pass2(s, m) == (_pass2 != "reg")
+        assert _ran_pass2(s, m)
     assert rel_l2(u, ref) <= TOL_TRAJ
 
 
-def test_pass2_sg_stiff_matches_oracle(_pass2):
+def test_pass2_sg_stiff_matches_oracle():
     """C4's spacing (dx = 6/8191) on 256^2."""
-    if _pass2 == "reg":
-        pytest.skip("2D has the LDS-DMA form only")
     n, dx, m, dt = 256, 6.0 / 8191, 10, 5.0 / 500
     x = (np.arange(n) - n / 2) * dx
     Y, X = np.meshgrid(x, x, indexing="ij")

@@ -38,10 +38,10 @@ print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} kz={os.environ.g
       f"{n * n * nz / el / 1e6:8.0f} Mcells*steps/s  per step {cls}  per step and J {upd}", flush=True)
 """
 
-# (nz, collective, k_p2d tile depth): an N-rank handle sizes its tiles from the GLOBAL
-# plane count (256 at 512^3 for every N), a 512 x 512 x nz grid from nz -- the third
-# entry pins the former
-for nz, force, kz in [(64, 0, 0), (64, 1, 0), (64, 1, 256), (128, 0, 0), (128, 1, 256)]:
+# (nz, collective, k_p2d tile depth): the tile depth follows the slab's own plane count
+# (its interior on split collective handles: 2 x 30 planes at nz = 64), the same as an
+# N-rank handle of 512^3 computes it; the pinned depths probe the choice
+for nz, force, kz in [(64, 0, 0), (64, 1, 0), (64, 1, 60), (64, 1, 16), (128, 0, 0), (128, 1, 0)]:
     env = dict(os.environ, NLS_FORCE_RCCL=str(force))
     if kz:
         env["NLS_P2_KZ"] = str(kz)
