@@ -84,6 +84,36 @@ def algorithmic_bytes_per_cell_step(m: int, eq: int, sewi: bool = False) -> int:
     return ((m - 1) * (m + 2) // 2 + m + 3) * 16
 
 
+def moved_bytes_per_cell_step(w, m, sched, pass2, u_frac, tm, steps):
+    """Bytes per cell and step THIS implementation moves (DESIGN.md sections 3-4), by
+    the launch sequence of the step; None where no model is written (KG, sEWI).
+      two-vector NLSE: alpha_0 (blind start: first step only) + sum over passes
+        (J+1 reads + ns writes) + the tail's alpha + tail (m-1 reads, W_0 and u on a
+        call's last step);
+      two-vector Gautschi (SG, two bases of f64, cell pairs): per basis the passes +
+        alpha + tail; the mid tail reads S_0..S_{m-2}, m(x), u_past and writes u_past,
+        g_0 (m+3), the end tail reads S_0..S_{m-2}, u_past, u and writes u, u_past (m+3);
+      one-vector G2 NLSE (div(c grad), m(x)): alpha passes j = 0..m-3 (W_j + c), the
+        tail's alpha (W_{m-2} + c), updates J = 0..m-3 ((J+2) vectors + c), tail (m-1
+        reads + c + m(x), u and W_0 written)."""
+    eq = w["eq"]
+    if w.get("sewi") or eq == 4:
+        return None
+    if pass2 and eq in (0, 1):
+        a0 = tm["class_count"].get("alpha", 0) - tm["class_count"].get("final", 0)  # alpha_0 launches
+        a0 = max(0, a0) / max(1, tm["steps"])
+        return 16 * (a0 + sum(j + 1 + ns for j, ns in sched) + 1 + (m + u_frac))
+    if pass2 and eq == 2:
+        per_basis = sum(j + 1 + ns for j, ns in sched) + 1
+        return 8 * (2 * per_basis + 2 * (m + 3))
+    if not pass2 and eq == 3:
+        alpha = (m - 1) * (16 + 8)
+        upd = sum((J + 2) * 16 + 8 for J in range(m - 2))
+        tail = (m - 1) * 16 + 16 + 8 + 8 + 16
+        return alpha + upd + tail
+    return None
+
+
 def synthetic_ic(w, z0, nzl, seed=1234):
     """8 random Gaussian solitons with phases + 1e-3 complex white noise.
     Noise is drawn per global plane, so the field does not depend on the rank split."""
@@ -150,16 +180,33 @@ def max_over_ranks(x, dist=None):
     return x
 
 
-def cpu_baseline(args):
+def cpu_model():
+    """The host CPU's model name (BASELINE.md section 3 asks for it)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(args, u_full=None):
     """The oracle (C++ restatement of nlse_driver.cpp -> NLSESolver::step ->
-    expm_multiply) on a bounded sample of the workload, timed twice on the host:
-    all cores (OpenMP build, SURVEY 8(d) "all cores" mode; reported as `value`)
-    and single-threaded (the reference's own Eigen path is single-threaded)."""
+    expm_multiply) on a bounded sample of the workload, on the host: all cores
+    (OpenMP build, SURVEY 8(d) "all cores" mode) and single-threaded (the
+    reference's own Eigen path is single-threaded).  For the headline workload the
+    reported `value` is ONE SS2 step of the full 512^3 grid (BASELINE.md section 3:
+    "a few steps at GPU sizes"; a 34 GB basis in host RAM), all cores; the 128^3
+    sub-grid rows stay beside it.  BASELINE C1 is timed in full as well."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
 
     one = _cpu_sample(args, oracle_py)
     out = dict(one)
+    out["cpu_model"] = cpu_model()
     try:
         oracle_py.use_openmp(True)
         nthr = oracle_py.threads()
@@ -167,10 +214,17 @@ def cpu_baseline(args):
             allc = _cpu_sample(args, oracle_py)
             out = dict(allc)
             out["cores"] = nthr
+            out["cpu_model"] = cpu_model()
             out["sample"] = allc["sample"].replace("1 thread", f"OpenMP {nthr} threads")
-            out["single_thread"] = {"value": one["value"], "seconds": one["seconds"]}
+            out["single_thread"] = {"value": one["value"], "seconds": one["seconds"], "sample": one["sample"]}
         if args.workload == "nlse3d_512":
-            out["c1_full_run"] = _cpu_c1(oracle_py, nthr)
+            out["c1_full_run"] = _cpu_c1(oracle_py, nthr, T=0.5)
+            out["c1_nlse_driver_defaults"] = _cpu_c1(oracle_py, nthr, T=1.5)
+            if u_full is not None and nthr > 1 and not args.no_full_grid_cpu:
+                full = _cpu_full_grid(args, oracle_py, u_full, nthr)
+                sub = {k: out[k] for k in ("value", "seconds", "sample", "cores")}
+                out.update(full)
+                out["subgrid_128"] = sub
     except (OSError, FileNotFoundError):
         pass
     finally:
@@ -178,12 +232,29 @@ def cpu_baseline(args):
     return out
 
 
-def _cpu_c1(oracle_py, nthr):
-    """BASELINE C1 timed in full on the host: the reference's CPU driver
-    (nlse_driver.cpp:27-106: 256^2, L = 10, T = 1.5, nt = 500 -> 499 SS2 steps of
-    dt = 0.003, Krylov m = 10, the two-soliton collision IC normalised to unit
-    mass) through the oracle restatement, all cores."""
-    n, L, T, nt, m = 256, 10.0, 1.5, 500, 10
+def _cpu_full_grid(args, oracle_py, u, nthr, steps=1):
+    """One SS2 step of the headline workload at its full grid (512^3, m = 16) through
+    the oracle on all cores: the CPU baseline at GPU size."""
+    w = WORKLOADS[args.workload]
+    n = w["n"]
+    dx = 2 * w["L"] / (n - 1)
+    g = oracle_py.grid(3, n, n, n, dx, dx)
+    t0 = time.perf_counter()
+    oracle_py.nlse_steps(g, u, w["dt"], steps, w["m"], nonlin=w["eq"])
+    el = time.perf_counter() - t0
+    return {"value": n ** 3 * steps / el / 1e6, "unit": "Mcells*steps/s", "cores": nthr, "kind": "port",
+            "seconds": el,
+            "sample": f"3D cubic NLSE {n}^3 m={w['m']} (the full workload grid), {steps} SS2 step, "
+                      f"oracle/ C++ -O2 OpenMP {nthr} threads"}
+
+
+def _cpu_c1(oracle_py, nthr, T=0.5):
+    """BASELINE C1 timed in full on the host through the oracle restatement, all
+    cores: 256^2, L = 10, nt = 500 -> 499 SS2 steps, Krylov m = 10, the two-soliton
+    collision IC of nlse_driver.cpp:52-66 normalised to unit mass.  T = 0.5 (dt =
+    1e-3) is BASELINE.json C1 and the GPU C1 test; T = 1.5 (dt = 3e-3) is
+    nlse_driver.cpp:35-40's own default."""
+    n, L, nt, m = 256, 10.0, 500, 10
     dx = 2 * L / (n - 1)
     x = np.linspace(-L, L, n)
     Y, X = np.meshgrid(x, x, indexing="ij")
@@ -195,7 +266,8 @@ def _cpu_c1(oracle_py, nthr):
     t0 = time.perf_counter()
     oracle_py.nlse_steps(g, u, T / nt, nt - 1, m)
     el = time.perf_counter() - t0
-    return {"workload": "C1: 2D cubic NLSE 256^2, dt = 3e-3, 499 steps, m = 10 (nlse_driver.cpp)",
+    return {"workload": f"C1: 2D cubic NLSE 256^2, T = {T}, nt = 500 (dt = {T / nt:g}), 499 steps, m = 10"
+                        + (" (BASELINE.json C1)" if T == 0.5 else " (nlse_driver.cpp:35-40 defaults)"),
             "seconds": el, "value": n * n * (nt - 1) / el / 1e6, "unit": "Mcells*steps/s",
             "cores": nthr}
 
@@ -348,6 +420,8 @@ def main():
     ap.add_argument("--prof-steps", type=int, default=5,
                     help="steps of the separate per-kernel timing pass (after the timed region)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-full-grid-cpu", action="store_true",
+                    help="skip the one-step CPU oracle run at the full 512^3 grid")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -397,6 +471,9 @@ def main():
     else:
         u /= np.sqrt(global_mass(u, dx ** dim, dist))  # nlse_call.cpp:41-49
         s.set_field(u)
+    # the full-grid CPU baseline steps the same initial field (headline workload, 1 rank)
+    keep_u = world == 1 and not args.no_cpu_baseline and args.workload == "nlse3d_512" and not args.n
+    u_full = u if keep_u else None
     del u
     dt = w["dt"]
 
@@ -465,12 +542,7 @@ def main():
     multi = w["eq"] in (0, 1) and not w.get("sewi")
     u_frac = (1.0 / args.steps) if multi else 1.0           # timed region
     u_frac_prof = (1.0 / max(1, args.prof_steps)) if multi else 1.0  # timing pass
-    if pass2 and w["eq"] in (0, 1, 3) and not w.get("sewi"):
-        # one basis per step: alpha_0 + sum over passes (J+1 reads + ns writes) + the
-        # tail's alpha + tail (m + u); the real Gautschi steps (two bases) are not modelled
-        own_bytes = esz * (1 + sum(j + 1 + ns for j, ns in sched) + 1 + (m + u_frac))
-    # (the real Gautschi tails are not modelled here: with two-vector passes the
-    # largest pass is reported for them)
+    own_bytes = moved_bytes_per_cell_step(w, m, sched, pass2, u_frac, tm, args.steps)
     # the NLSE's dominant kernel is the fused tail (the most bytes per launch: m-1 reads,
     # the next start vector and u; the largest pass takes about as long, so a timing
     # rule would flip between runs), else the largest two-vector pass
@@ -549,11 +621,12 @@ def main():
             "gpu_kernel_ms_per_step": {k: v / max(tm["steps"], 1) for k, v in tm["class_ms"].items()},
             "lanczos": ("s-step passes " + " ".join(f"J{j}:{ns}" for j, ns in sched) + " + fused tail")
             if pass2 else "one-vector passes + fused tail",
+            "bases_per_step": 2 if w["eq"] in (2, 4) else (3 if w.get("sewi") else 1),
         },
     }
     s.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args)
+        result["cpu_baseline"] = cpu_baseline(args, u_full)
     if rank == 0:
         print(json.dumps(result), file=out, flush=True)
     if dist is not None:

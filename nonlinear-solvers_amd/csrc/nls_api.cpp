@@ -117,6 +117,7 @@ struct nls_handle {
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
   bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
+  bool p2_split_on = true;     // collective handles: boundary/interior split (NLS_P2_SPLIT=0: off)
   cplx *zbuf = nullptr;       // one zero row (nx cells): the DMA source of out-of-grid rows
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
@@ -692,7 +693,7 @@ int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz) {
 // boundary plane pairs (tile depth 2, Geo::q2; on the halo stream, followed there
 // by the two-plane halo exchange of the new stencil vector) and the interior
 // (compute stream).
-bool p2_split(const nls_handle *h) { return h->collective && h->geo.nzl >= 8; }
+bool p2_split(const nls_handle *h) { return h->collective && h->geo.nzl >= 8 && h->p2_split_on; }
 int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
 int p2_grid(const nls_handle *h) {
   const int64_t nzl = p2_geo(h).nzl;
@@ -906,6 +907,7 @@ void alloc_all(nls_handle *h) {
   // slabs) and 2D on one rank (ny % 4 == 0, planes of 4 rows);
   // NLS_PASS2=0/1 forces it off / on where a pass form exists.
   h->pass2 = false;
+  if (const char *e = std::getenv("NLS_P2_SPLIT")) h->p2_split_on = std::atoi(e) != 0;
   {
     const char *e = std::getenv("NLS_PASS2");
     const bool want = e ? std::atoi(e) != 0 : true;

@@ -35,7 +35,7 @@ import pytest
 
 import np_ref as R
 import oracle_py as O
-from conftest import parity_bound, record_parity, rel_l2, self_floor
+from conftest import PROPAGATED_FACTOR, parity_bound, record_parity, rel_l2, self_floor
 
 pytestmark = pytest.mark.gpu
 nls_amd = pytest.importorskip("nls_amd")
@@ -140,17 +140,24 @@ def _cpu_nlse(dim, n, dx, u0, dt, m, eq):
     return _CPU[key]
 
 
-def _check(case, gpu, ora, floor, twin, hard=(1, 5)):
+def _check(case, gpu, ora, floor, twin, hard=(1, 5), prop=None):
     """GPU vs oracle at every checkpoint: <= TOL at the `hard` checkpoints, else
-    <= parity_bound(TOL, self-floor)."""
+    <= parity_bound(TOL, self-floor).  prop[k] (optional): the oracle continued
+    from the GPU's step-1 field, vs the oracle -- the GPU's first-step deviation
+    (<= TOL) as the reference algorithm itself amplifies it; beyond TOL the GPU
+    must stay within PROPAGATED_FACTOR x that."""
     rows = []
     for k in CHECK:
         err = rel_l2(gpu[k], ora[k])
         bound = TOL if k in hard else parity_bound(TOL, floor[k])
-        rows.append((k, err, floor[k], rel_l2(twin[k], ora[k]) if twin else None, bound))
-    record_parity(case, [r[:4] for r in rows])
-    msg = "; ".join(f"step {k}: gpu {e:.2e} self-floor {f:.2e} bound {b:.1e}" for k, e, f, _, b in rows)
-    assert all(e <= b for _, e, _, _, b in rows), msg
+        pk = prop.get(k) if prop else None
+        if pk is not None and k not in hard:
+            bound = min(bound, max(TOL, PROPAGATED_FACTOR * pk))
+        rows.append((k, err, floor[k], rel_l2(twin[k], ora[k]) if twin else None, pk, bound))
+    record_parity(case, [r[:5] for r in rows])
+    msg = "; ".join(f"step {k}: gpu {e:.2e} self-floor {f:.2e} propagated {p if p is None else f'{p:.2e}'} "
+                    f"bound {b:.1e}" for k, e, f, _, p, b in rows)
+    assert all(e <= b for _, e, _, _, _, b in rows), msg
 
 
 # (dim, n, dx): the sub-grid keeps the BASELINE workload's spacing
@@ -184,7 +191,14 @@ def test_nlse_stiff_matches_oracle(dim, n, dx, eq, mode):
         assert floor[steps] <= 1e-12
         _check(case, gpu, ora, floor, twin, hard=CHECK)
     else:
-        _check(case, gpu, ora, floor, twin)
+        # the reference algorithm's amplification of the GPU's own first-step deviation
+        g = O.grid(dim, n, n, n, dx, dx)
+        prop, v, done = {}, gpu[1], 1
+        for k in CHECK[1:]:
+            v = O.nlse_steps(g, v, dt, k - done, m, nonlin=eq)
+            done = k
+            prop[k] = rel_l2(v, ora[k])
+        _check(case, gpu, ora, floor, twin, prop=prop)
 
 
 def test_large_slab_path_uses_colsum():

@@ -38,13 +38,20 @@ print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} kz={os.environ.g
       f"{n * n * nz / el / 1e6:8.0f} Mcells*steps/s  per step {cls}  per step and J {upd}", flush=True)
 """
 
-# (nz, collective, k_p2d tile depth): the tile depth follows the slab's own plane count
-# (its interior on split collective handles: 2 x 30 planes at nz = 64), the same as an
-# N-rank handle of 512^3 computes it; the pinned depths probe the choice
-for nz, force, kz in [(64, 0, 0), (64, 1, 0), (64, 1, 60), (64, 1, 16), (128, 0, 0), (128, 1, 0)]:
-    env = dict(os.environ, NLS_FORCE_RCCL=str(force))
-    if kz:
-        env["NLS_P2_KZ"] = str(kz)
+# (nz, extra environment): the tile depth follows the slab's own plane count (its
+# interior on split collective handles), the same as an N-rank handle of 512^3
+# computes it; NLS_P2_KZ pins it, NLS_P2_SPLIT=0 drops the boundary/interior split
+VARIANTS = [
+    (64, {}), (64, {"NLS_P2_KZ": "64"}),
+    (64, {"NLS_FORCE_RCCL": "1"}), (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "60"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "64", "NLS_P2_SPLIT": "0"}),
+    (128, {}), (128, {"NLS_FORCE_RCCL": "1"}),
+]
+if len(sys.argv) > 1:  # a subset: python tools/slab_probe.py 0 2 3
+    VARIANTS = [VARIANTS[int(i)] for i in sys.argv[1:]]
+for nz, extra in VARIANTS:
+    env = dict(os.environ, **extra)
+    print(f"# {extra}", flush=True)
     r = subprocess.run([sys.executable, "-c", CHILD, ROOT, str(nz)], env=env, timeout=300)
     if r.returncode:
         sys.exit(r.returncode)
