@@ -91,7 +91,7 @@ struct nls_handle {
   void *u = nullptr;        // NLSE state u (nloc complex)
   double *up = nullptr;     // SG u_past
   double *mf = nullptr;     // SG m(x), G2 NLSE focusing field m(x)
-  double *cfb = nullptr;    // G2 anisotropy c(x): (nzl + 2) planes, local plane 0 at +P
+  double *cfb = nullptr;    // G2 anisotropy c(x): nzl + 2 ghost planes, local plane 0 at +ghost P
   bool ani = false;         // G2 operator div(c grad) (laplacians.hpp:54-218)
   bool kg = false;          // G2 Klein-Gordon Gautschi (real, ani)
   int gfun = -1;            // G2 Gautschi family (NLS_SG_G2 .. NLS_PHI4): GautschiForce; -1 G1 sine-Gordon
@@ -118,7 +118,15 @@ struct nls_handle {
   int p2grid = 0, p2kz = 32;
   bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
   bool p2_split_on = true;     // collective handles: boundary/interior split (NLS_P2_SPLIT=0: off)
-  cplx *zbuf = nullptr;       // one zero row (nx cells): the DMA source of out-of-grid rows
+  cplx *zbuf = nullptr;
+  cplx *p2lbuf = nullptr;      // split passes: L S_J at the 8 planes around the slab's ends (k_p2b_lap)
+  int p2bgrid = 0;             // workgroups of the boundary-plane kernel k_p2b
+  bool p2b_dma = false;        // A/B (NLS_P2_BND=dma): boundary planes by k_p2d tiles of depth 2 instead
+  // register form of the two-vector pass (k_p2g_lap + k_p2g, nls_pass2g.hpp): the G2
+  // anisotropic NLSE and the isotropic shapes k_p2d does not take
+  bool p2reg = false;
+  cplx *p2gbuf = nullptr;      // L S_J at local planes [-1, nzl] (nzl + 2 planes)
+  int p2ggrid = 0;       // one zero row (nx cells): the DMA source of out-of-grid rows
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
   // a new state was set (nls_set_*): the next step starts its bases cold, so it is
@@ -663,10 +671,16 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   reduce_final(h, b, nf, f0, f1, tr, ti);
 }
 
+// The smallest slab of the decomposition (nls_slab_planes: npl / nranks planes).
+// Every choice that changes a step's sequence of transport operations is made from
+// it, never from this rank's own slab, so that all ranks issue the same sequence.
+int64_t min_slab_planes(const nls_handle *h) { return h->geo.npl / std::max(1, h->nranks); }
+
 // The geometry k_p2d marches: the handle's, or for a 2D grid planes of 4 rows
 // (nyp = 4, npl = ny/4, P = 4 nx; single rank), whose row wrap is the 2D y neighbour
 Geo p2_geo(const nls_handle *h) {
   Geo g = h->geo;
+  if (h->p2reg) return g;  // k_p2g works on the handle's own planes
   if (h->p2_pr) {  // pairs of cells along x
     g.nx = h->geo.nx / 2;
     g.P = h->geo.P / 2;
@@ -689,13 +703,17 @@ int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz) {
   const int64_t nzc = (qb - qa + kz - 1) / kz;
   return (int)(((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * (g.nyp / P2D_ROWS) * nzc);
 }
-// Multi-rank handles (slabs of >= 8 planes) launch each pass as ONE launch over both
-// boundary plane pairs (tile depth 2, Geo::q2; on the halo stream, followed there
-// by the two-plane halo exchange of the new stencil vector) and the interior
-// (compute stream).
-bool p2_split(const nls_handle *h) { return h->collective && h->geo.nzl >= 8 && h->p2_split_on; }
-int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
+// Multi-rank handles (3D slabs of >= 8 planes) compute each pass's first two and
+// last two planes with the register-only boundary kernels k_p2b_lap + k_p2b on the
+// halo stream, followed there by the two-plane halo exchange of the new stencil
+// vector, while the interior planes run as k_p2d on the compute stream
+// (nls_pass2b.hpp).
+bool p2_split(const nls_handle *h) {
+  return h->collective && min_slab_planes(h) >= 8 && h->p2_split_on && !h->p2_d2 && !h->p2_pr && !h->p2reg;
+}
+int p2_bnd_tiles(const nls_handle *h) { return h->p2b_dma ? 2 * p2_tiles(h, 0, 2, 2) : h->p2bgrid; }
 int p2_grid(const nls_handle *h) {
+  if (h->p2reg) return h->p2ggrid;
   const int64_t nzl = p2_geo(h).nzl;
   if (!p2_split(h)) return p2_tiles(h, 0, nzl, h->p2kz);
   return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, h->p2kz);
@@ -755,27 +773,48 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
     int nb = p2_grid(h);
     const void *fn = kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
-    if (!split) {
+    if (h->p2reg) {
+      // y = L S_J over the slab and its neighbour planes, then the per-cell pass
+      void *SJ = vec_ptr(h, b, J);
+      Geo gl = h->geo;
+      const int dim = (int)h->cfg.dim;
+      int lgrid = (int)std::min<int64_t>(4096, ((gl.nzl + 2) * gl.P + NTHREADS - 1) / NTHREADS);
+      void *la[] = {&SJ, &gl, &h->p2gbuf};
+      launch(h, 1, J, kernel_p2g_lap(dim, h->ani), lgrid, la);
+      int poff = 0;
+      void *args[] = {&W, &vs, &gl, &ps, &h->partP2, &nb, &h->p2gbuf, &poff};
+      launch(h, 1, J, kernel_p2g(dim, J, ns == 2, h->ani), nb, args);
+      if (h->collective) halo_begin(h, b, out);
+    } else if (!split) {
       int poff = 0;
       void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb, &h->zbuf, &poff};
       launch(h, 1, J, fn, nb, args);
       if (h->collective) halo_begin(h, b, out);
     } else {
-      // one launch over both boundary plane pairs [0, 2) and [nzl-2, nzl) on the halo
-      // stream, then the exchange of the new stencil vector's two boundary planes
-      // there, while the interior runs on the compute stream
+      // the boundary planes [0, 2) and [nzl-2, nzl) by the register-only kernels on
+      // the halo stream, then the exchange of the new stencil vector's two boundary
+      // planes there, while the interior runs on the compute stream
       const int64_t nzl = h->geo.nzl;
       const int tb = p2_bnd_tiles(h);
       halo_after_compute(h);
-      Geo gb = g;
-      gb.kz = 2;
-      gb.qa = 0;
-      gb.qb = 2;
-      gb.q2 = (int32_t)(nzl - 2);
-      {
+      if (h->p2b_dma) {  // A/B: k_p2d over both boundary plane pairs (Geo::q2)
+        Geo gb = g;
+        gb.kz = 2;
+        gb.qa = 0;
+        gb.qb = 2;
+        gb.q2 = (int32_t)(nzl - 2);
         int poff = 0;
         void *args[] = {&W, &vs, &gb, &ps, &h->partP2, &nb, &h->zbuf, &poff};
         launch(h, 1, J, fn, tb, args, h->cstream);
+      } else {
+        void *SJ = vec_ptr(h, b, J);
+        Geo gb = h->geo;
+        int lg = (int)std::min<int64_t>(2048, (P2B_LPLANES_H * gb.P + NTHREADS - 1) / NTHREADS);
+        void *la[] = {&SJ, &gb, &h->p2lbuf};
+        launch(h, 1, J, kernel_p2b_lap(), lg, la, h->cstream);
+        int poff = 0;
+        void *args[] = {&W, &vs, &gb, &ps, &h->partP2, &nb, &h->p2lbuf, &poff};
+        launch(h, 1, J, kernel_p2b(J, ns == 2), tb, args, h->cstream);
       }
       hip_check(h, hipEventRecord(h->ev_bdone, h->cstream), "hipEventRecord");
       halo_planes(h, vec_ptr(h, b, out), (int64_t)h->esize, h->cstream, 2);
@@ -908,6 +947,7 @@ void alloc_all(nls_handle *h) {
   // NLS_PASS2=0/1 forces it off / on where a pass form exists.
   h->pass2 = false;
   if (const char *e = std::getenv("NLS_P2_SPLIT")) h->p2_split_on = std::atoi(e) != 0;
+  if (const char *e = std::getenv("NLS_P2_BND")) h->p2b_dma = std::string(e) == "dma";
   {
     const char *e = std::getenv("NLS_PASS2");
     const bool want = e ? std::atoi(e) != 0 : true;
@@ -917,14 +957,20 @@ void alloc_all(nls_handle *h) {
     // operator): the field as pairs of cells, nx even
     const bool pr = !c && !h->kg && !ani && d2 && g.nx % 2 == 0 && g.nx >= 4;
     // multi-rank: slabs of >= 4 planes (two-plane halos)
-    const bool base = (c || pr) && !ani && (dim == 3 || d2) && (!h->collective || g.nzl >= 4) &&
+    const bool base = (c || pr) && !ani && (dim == 3 || d2) && (!h->collective || min_slab_planes(h) >= 4) &&
                       (h->nbasis == 1 || pr) && h->m >= 3 &&
                       g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
     // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS
     const bool dma = (dim == 3 ? g.nyp % P2D_ROWS == 0 && g.nyp >= 4 : d2) && h->m - 4 <= P2D_MAXJ;
-    h->pass2 = want && base && dma;
-    h->p2_d2 = h->pass2 && dim == 2;
-    h->p2_pr = h->pass2 && !c;
+    // the register form k_p2g (complex fields): the G2 anisotropic NLSE (div(c grad); not
+    // the real Klein-Gordon) and the isotropic grids k_p2d does not take (ny % 4 != 0,
+    // 2D slabs, m > 18); J <= 28
+    const bool reg = c && !h->kg && h->nbasis == 1 && h->m >= 3 && h->m <= MMAX - 2 &&
+                     (!h->collective || min_slab_planes(h) >= 4) && g.nloc + 2 * g.P < (int64_t(1) << 31);
+    h->pass2 = want && ((base && dma) || reg);
+    h->p2reg = h->pass2 && !(base && dma);
+    h->p2_d2 = h->pass2 && !h->p2reg && dim == 2;
+    h->p2_pr = h->pass2 && !h->p2reg && !c;
   }
   // stored vectors: slab + ghost planes (two for the two-vector passes' radius-2
   // march) + the stride pad
@@ -938,6 +984,16 @@ void alloc_all(nls_handle *h) {
     const Geo gm = p2_geo(h);
     const int64_t cols = ((gm.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * std::max<int64_t>(1, gm.nyp / P2D_ROWS);
     const int64_t nzc = std::max<int64_t>(1, (2048 + cols - 1) / cols);
+    if (h->p2reg) {
+      h->p2ggrid = (int)std::min<int64_t>(4096, (g.nloc + NTHREADS - 1) / NTHREADS);
+      hip_check(h, hipMalloc(&h->p2gbuf, (size_t)(g.nzl + 2) * g.P * sizeof(cplx)), "hipMalloc(p2gbuf)");
+    }
+    if (p2_split(h)) {
+      // the boundary kernel: one thread per cell of the 4 planes, grid-stride over at
+      // most 1024 workgroups (their partial sums share the pass's partial array)
+      h->p2bgrid = (int)std::min<int64_t>(1024, (4 * g.P + NTHREADS - 1) / NTHREADS);
+      hip_check(h, hipMalloc(&h->p2lbuf, (size_t)P2B_LPLANES_H * g.P * sizeof(cplx)), "hipMalloc(p2lbuf)");
+    }
     const int64_t span = p2_split(h) ? gm.nzl - 4 : gm.nzl;
     h->p2kz = (int)std::max<int64_t>(std::min<int64_t>(16, span), std::min<int64_t>(256, (span + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
@@ -1014,10 +1070,12 @@ void alloc_all(nls_handle *h) {
     if (h->kg) hip_check(h, hipMalloc(&h->vel, nbytes), "hipMalloc(v)");
   }
   if (h->ani) {
-    const size_t cbytes = (size_t)(g.nzl + 2) * g.P * sizeof(double);
+    // the same ghost depth as a stored vector (two for the two-vector passes' radius-2
+    // stencil of div(c grad))
+    const size_t cbytes = (size_t)(g.nzl + 2 * h->ghost) * g.P * sizeof(double);
     hip_check(h, hipMalloc(&h->cfb, cbytes), "hipMalloc(c)");
     hip_check(h, hipMemsetAsync(h->cfb, 0, cbytes, h->stream), "hipMemset");
-    h->geo.cf = h->cfb + g.P;
+    h->geo.cf = h->cfb + h->ghost * g.P;
   }
   // grid sizes from measured occupancy; partial buffers sized for the largest
   Geo ga = g;
@@ -1086,10 +1144,10 @@ void free_all(nls_handle *h) {
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
                   (void *)h->vel, h->xedge, (void *)h->partX, h->p2, (void *)h->partP2,
-                  (void *)h->zbuf, (void *)h->partA, (void *)h->partU})
+                  (void *)h->zbuf, (void *)h->p2lbuf, (void *)h->p2gbuf, (void *)h->partA, (void *)h->partU})
     if (p) (void)hipFree(p);
   h->p2 = nullptr;
-  h->partP2 = h->zbuf = nullptr;
+  h->partP2 = h->zbuf = h->p2lbuf = h->p2gbuf = nullptr;
   h->u = h->scratch = h->snap = h->uprev = nullptr;
   h->up = h->mf = h->cfb = h->vel = nullptr;
   h->xedge = nullptr;
@@ -1382,9 +1440,10 @@ int nls_set_coefficients(nls_handle *h, const double *mfield, const double *cfie
     const size_t bytes = (size_t)n * sizeof(double);
     hip_check(h, hipMemcpyAsync(h->mf, mfield, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
     if (!cq_g2) {
-      hip_check(h, hipMemcpyAsync(h->cfb + h->geo.P, cfield, bytes, hipMemcpyHostToDevice, h->stream),
+      hip_check(h, hipMemcpyAsync(h->cfb + h->ghost * h->geo.P, cfield, bytes, hipMemcpyHostToDevice, h->stream),
                 "H2D");
-      halo_planes(h, reinterpret_cast<char *>(h->cfb + h->geo.P), (int64_t)sizeof(double));
+      halo_planes(h, reinterpret_cast<char *>(h->cfb + h->ghost * h->geo.P), (int64_t)sizeof(double), nullptr,
+                  h->ghost);
     }
     h->coef_set = true;
     h->w0_ready = false;  // the start vector depends on m

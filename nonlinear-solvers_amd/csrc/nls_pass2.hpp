@@ -31,6 +31,7 @@ struct P2State {
   int32_t blind;  // the J = 0 pass ran on the raw start vector (mode 2), beta from its sums
 };
 
+#ifndef NLS_NO_P2_KERNELS  // (defined by translation units that only need the types)
 // Coefficient kernel (one workgroup).  A pass at J writes ns = 1, 2 or 3 new
 // vectors V_1 = L W_J - sigma W_J - sum_{k<J} conj(H[J][k]) W_k, V_{i+1} = (L - sigma) V_i
 // (k_p2d: ns <= 2; the recurrences also hold for ns = 3, tests/sstep_model.py) and reduces, in this order, S_l^H V_i (l <= J, per i)
@@ -233,5 +234,7 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
     st->s[t] = 1.0;
   }
 }
+
+#endif  // NLS_NO_P2_KERNELS
 
 }  // namespace nls

@@ -501,6 +501,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   }
 }
 
+#ifndef NLS_NO_P2_KERNELS
 // ---- fused tail of the two-vector scheme ----------------------------------
 // After the last basis pass the stored vectors are S_0..S_j (j = m-2) with
 // W = S C orthonormal and the H columns < j known.  One k_alpha_l2 pass over
@@ -578,5 +579,7 @@ __global__ __launch_bounds__(NTHREADS) void k_p2tfin(const P2State *__restrict__
   }
   for (int l = t; l <= j + 1; l += NTHREADS) st->coef[l] = {l == j + 1 ? 1.0 : 0.0, 0.0};
 }
+
+#endif  // NLS_NO_P2_KERNELS
 
 }  // namespace nls

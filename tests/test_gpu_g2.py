@@ -94,28 +94,62 @@ def test_neumann_bc_bit_exact(dim, nx, ny, nz):
         assert np.array_equal(s.get_field(), O.neumann_bc(g, u))
 
 
+@pytest.mark.parametrize("pass2", ["1", "0"], ids=["two_vector", "one_vector"])
 @pytest.mark.parametrize("dim,nx,ny,nz,m", [(2, 32, 32, 1, 20), (2, 300, 20, 1, 20), (3, 12, 12, 12, 25),
-                                            (3, 70, 9, 11, 25), (3, 16, 16, 16, 10)])
-def test_g2_trajectory_with_bc_matches_oracle(dim, nx, ny, nz, m):
-    """The driver loop (nlse_cubic_driver_3d.cpp:116-119): step, then apply_bc."""
+                                            (3, 70, 9, 11, 25), (3, 16, 16, 16, 10), (2, 7, 5, 1, 20)])
+def test_g2_trajectory_with_bc_matches_oracle(monkeypatch, pass2, dim, nx, ny, nz, m):
+    """The driver loop (nlse_cubic_driver_3d.cpp:116-119): step, then apply_bc.  With
+    the two-vector passes (the default: the register form k_p2g_lap + k_p2g for div(c
+    grad), nls_pass2g.hpp) and with the one-vector passes (NLS_PASS2=0)."""
+    monkeypatch.setenv("NLS_PASS2", pass2)
     L, dt, steps = 4.0, 1e-3, 12
     dx = 2 * L / (nx - 1)
     u, mf, c = fields(dim, nx, ny, nz, seed=4)
     g = O.grid(dim, nx, ny, nz, dx, dx)
+    m = min(m, nx * ny * nz)
     ref = O.nlse_g2_steps(g, c, mf, u, dt, steps, m, bc=True)
     ref_nobc = O.nlse_g2_steps(g, c, mf, u, dt, steps, m, bc=False)
     with solver(dim, nx, ny, nz, dx, m) as s:
         s.set_coefficients(mf, c)
         s.set_field(u)
+        s.set_timing(True)
         for _ in range(steps):
             s.step(dt, 1)
             s.apply_bc()
         out = s.get_field()
+        cnt = s.timing()["update_count"]
+        assert (cnt[0] > 0 and cnt[1] == 0) == (pass2 == "1")  # s-step passes start at even J only
+        s.set_timing(False)
         s.set_field(u)
         s.step(dt, steps)
         out_nobc = s.get_field()
     assert rel_l2(out, ref) <= TOL_TRAJ
     assert rel_l2(out_nobc, ref_nobc) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("eq", ["g2", "g2_2d"])
+def test_g2_stiff_two_vector_matches_oracle(eq):
+    """The G2 production workload's spacing (bench g2_3d_256: L = 10, dx = 20/255, m = 25;
+    nlse_cubic_driver_3d.cpp:112-114) on a 48^3 sub-grid, 2D at m = 20 on 256^2 with the
+    2D driver's spacing; two-vector passes (k_p2g), BC after every step, 10 steps."""
+    dim = 3 if eq == "g2" else 2
+    n, m = (48, 25) if dim == 3 else (256, 20)
+    dx, dt, steps = 20.0 / 255, 1e-3, 10
+    u, mf, c = fields(dim, n, n, n, seed=9, L=(n - 1) * dx / 2)
+    g = O.grid(dim, n, n, n, dx, dx)
+    ref = O.nlse_g2_steps(g, c, mf, u, dt, steps, m, bc=True)
+    with solver(dim, n, n, n, dx, m) as s:
+        s.set_coefficients(mf, c)
+        s.set_field(u)
+        s.set_timing(True)
+        for _ in range(steps):
+            s.step(dt, 1)
+            s.apply_bc()
+        out = s.get_field()
+        cnt = s.timing()["update_count"]
+        # two-vector passes at even J only, the last at J = m - 4 or m - 3
+        assert cnt[0] > 0 and cnt[1] == 0 and max(j for j in range(32) if cnt[j]) >= m - 4
+    assert rel_l2(out, ref) <= TOL_TRAJ
 
 
 def test_g2_snapshot_is_pre_bc():

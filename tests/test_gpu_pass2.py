@@ -26,8 +26,14 @@ def _pass2(monkeypatch):
 
 
 def _eligible(nx, ny, m):
-    """Does the handle run the two-vector pass (nls_api.cpp alloc_all)?"""
-    return ny % 4 == 0 and m <= 18
+    """Does the handle run the two-vector pass (nls_api.cpp alloc_all)?  k_p2d for
+    ny % 4 == 0 and m <= 18, the register form k_p2g (nls_pass2g.hpp) for the other
+    complex shapes up to m = 30."""
+    return 3 <= m <= 30
+
+
+def _form(nx, ny, m):
+    return "dma" if ny % 4 == 0 and m <= 18 else "reg"
 
 
 def _ran_pass2(s, m):
@@ -40,7 +46,8 @@ def _ran_pass2(s, m):
 
 @pytest.mark.parametrize("nx,ny,nz,m", [(64, 16, 12, 16), (64, 32, 20, 10), (128, 16, 9, 15),
                                         (64, 16, 16, 25), (64, 16, 10, 3), (64, 48, 8, 4),
-                                        (64, 20, 11, 18), (50, 12, 13, 16), (130, 8, 9, 5)])
+                                        (64, 20, 11, 18), (50, 12, 13, 16), (130, 8, 9, 5),
+                                        (40, 18, 10, 16), (33, 7, 9, 12), (24, 24, 24, 30)])
 @pytest.mark.parametrize("eq", [0, 1])
 def test_pass2_trajectory_matches_oracle(nx, ny, nz, m, eq):
     L = 10.0
@@ -96,7 +103,7 @@ def test_multi_step_call_equals_single_steps(eq):
 
 
 def _eligible2d(ny, m):
-    return ny % 4 == 0 and ny >= 8 and m <= 18
+    return 3 <= m <= 30  # k_p2d on planes of 4 rows (ny % 4 == 0, ny >= 8, m <= 18), else k_p2g
 
 
 @pytest.mark.parametrize("nx,ny,m", [(64, 64, 16), (300, 20, 10), (50, 12, 16), (130, 8, 5), (70, 66, 16),

@@ -44,6 +44,7 @@ print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} kz={os.environ.g
 VARIANTS = [
     (64, {}), (64, {"NLS_P2_KZ": "64"}),
     (64, {"NLS_FORCE_RCCL": "1"}), (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "60"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "60", "NLS_P2_BND": "dma"}),
     (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "64", "NLS_P2_SPLIT": "0"}),
     (128, {}), (128, {"NLS_FORCE_RCCL": "1"}),
 ]
