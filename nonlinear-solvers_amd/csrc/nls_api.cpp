@@ -118,15 +118,16 @@ struct nls_handle {
   int p2grid = 0, p2kz = 32;
   bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
   bool p2_split_on = true;     // collective handles: boundary/interior split (NLS_P2_SPLIT=0: off)
-  cplx *zbuf = nullptr;
+  cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
   cplx *p2lbuf = nullptr;      // split passes: L S_J at the 8 planes around the slab's ends (k_p2b_lap)
   int p2bgrid = 0;             // workgroups of the boundary-plane kernel k_p2b
   bool p2b_dma = false;        // A/B (NLS_P2_BND=dma): boundary planes by k_p2d tiles of depth 2 instead
-  // register form of the two-vector pass (k_p2g_lap + k_p2g, nls_pass2g.hpp): the G2
+  // register form of the two-vector pass (k_lap + k_p2m, nls_pass2g.hpp): the G2
   // anisotropic NLSE and the isotropic shapes k_p2d does not take
   bool p2reg = false;
   cplx *p2gbuf = nullptr;      // L S_J at local planes [-1, nzl] (nzl + 2 planes)
-  int p2ggrid = 0;       // one zero row (nx cells): the DMA source of out-of-grid rows
+  int p2mgrid[MMAX] = {};      // k_p2m grid per J
+  int p2lapgrid = 0;           // k_lap grid over planes [-1, nzl]
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
   // a new state was set (nls_set_*): the next step starts its bases cold, so it is
@@ -671,6 +672,27 @@ void run_lanczos(nls_handle *h, int b, int nf, int f0, int f1, double tr, double
   reduce_final(h, b, nf, f0, f1, tr, ti);
 }
 
+Geo p2m_lap_geo(const nls_handle *h);
+// y = L S_J of the register two-vector pass into lbuf (k_lap)
+void p2m_lap(nls_handle *h, int b, int J, hipStream_t st) {
+  void *SJ = vec_ptr(h, b, J);
+  Geo gl = p2m_lap_geo(h);
+  void *lb0 = h->p2gbuf + h->geo.P;  // local plane 0 of y
+  void *la[] = {&SJ, &gl, &lb0};
+  launch(h, 1, J, kernel_lap(true, (int)h->cfg.dim, h->ani), h->p2lapgrid, la, st);
+}
+
+// y = L S_J of the register two-vector pass: the slab's planes and, where they exist
+// in the grid, the neighbouring slabs' first plane on each side (ghost planes)
+Geo p2m_lap_geo(const nls_handle *h) {
+  Geo g = h->geo;
+  g.qa = g.z0 > 0 ? -1 : 0;
+  g.qb = (int32_t)(g.nzl + (g.z0 + g.nzl < g.npl ? 1 : 0));
+  return g;
+}
+
+constexpr int64_t P2D_MIN_TILES = 1024;
+
 // The smallest slab of the decomposition (nls_slab_planes: npl / nranks planes).
 // Every choice that changes a step's sequence of transport operations is made from
 // it, never from this rank's own slab, so that all ranks issue the same sequence.
@@ -712,8 +734,8 @@ bool p2_split(const nls_handle *h) {
   return h->collective && min_slab_planes(h) >= 8 && h->p2_split_on && !h->p2_d2 && !h->p2_pr && !h->p2reg;
 }
 int p2_bnd_tiles(const nls_handle *h) { return h->p2b_dma ? 2 * p2_tiles(h, 0, 2, 2) : h->p2bgrid; }
-int p2_grid(const nls_handle *h) {
-  if (h->p2reg) return h->p2ggrid;
+int p2_grid(const nls_handle *h, int J = 0) {
+  if (h->p2reg) return h->p2mgrid[J];
   const int64_t nzl = p2_geo(h).nzl;
   if (!p2_split(h)) return p2_tiles(h, 0, nzl, h->p2kz);
   return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, h->p2kz);
@@ -770,20 +792,19 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
   for (size_t si = 0; si < sched.size(); ++si) {
     int J = sched[si].first, ns = sched[si].second;
     const int out = J + ns;  // the pass's last vector: the next stencil vector
-    int nb = p2_grid(h);
-    const void *fn = kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
+    int nb = p2_grid(h, J);
+    const void *fn = h->p2reg ? nullptr : kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
     if (h->p2reg) {
-      // y = L S_J over the slab and its neighbour planes, then the per-cell pass
-      void *SJ = vec_ptr(h, b, J);
-      Geo gl = h->geo;
+      // y = L S_J over the slab and its neighbour planes, then the pass over y.  (Issuing
+      // the next pass's y on a second stream, to overlap the column sums and k_p2coef,
+      // measured no gain at G2 256^3: 13.76 vs 13.75 ms/step.)
       const int dim = (int)h->cfg.dim;
-      int lgrid = (int)std::min<int64_t>(4096, ((gl.nzl + 2) * gl.P + NTHREADS - 1) / NTHREADS);
-      void *la[] = {&SJ, &gl, &h->p2gbuf};
-      launch(h, 1, J, kernel_p2g_lap(dim, h->ani), lgrid, la);
+      p2m_lap(h, b, J, nullptr);
       int poff = 0;
-      void *args[] = {&W, &vs, &gl, &ps, &h->partP2, &nb, &h->p2gbuf, &poff};
-      launch(h, 1, J, kernel_p2g(dim, J, ns == 2, h->ani), nb, args);
+      Geo gp = h->geo;
+      void *args[] = {&W, &vs, &gp, &ps, &h->partP2, &nb, &h->p2gbuf, &poff};
+      launch(h, 1, J, kernel_p2m(dim, J, ns == 2, h->ani), nb, args);
       if (h->collective) halo_begin(h, b, out);
     } else if (!split) {
       int poff = 0;
@@ -977,16 +998,25 @@ void alloc_all(nls_handle *h) {
   h->ghost = h->pass2 ? GHOST_MAX : 1;
   h->vs = (g.nzl + 2 * h->ghost) * g.P + h->vpad;
   if (h->pass2) {
-    // z depth of a k_p2d tile: deep (the prologue is not overlapped), but at least
-    // ~2048 tiles so that every CU gets several (256 at 512^3, 32 at 256^3), from the
-    // planes this launch covers: the slab's (not the global count), its
-    // interior on split multi-rank handles (64-plane slabs of 512^3: 2 x 30 planes)
+    // z depth of a k_p2d tile: deep (each tile's prologue is a latency chain), but at
+    // least ~P2D_MIN_TILES tiles, from the planes this launch covers: the slab's (ADVICE
+    // r02: not the global count), its interior on split multi-rank handles.  512^3:
+    // 256 (2048 tiles, capped); the 8-rank slab 512^2 x 64: 64 / 60 (one tile per
+    // column) measured 4.40 / 4.77 ms/step against 4.57 / 4.98 at 32 / 30
+    // (tools/slab_probe.py, profiles/r03/slab_probe.txt)
     const Geo gm = p2_geo(h);
     const int64_t cols = ((gm.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * std::max<int64_t>(1, gm.nyp / P2D_ROWS);
-    const int64_t nzc = std::max<int64_t>(1, (2048 + cols - 1) / cols);
+    const int64_t nzc = std::max<int64_t>(1, (P2D_MIN_TILES + cols - 1) / cols);
     if (h->p2reg) {
-      h->p2ggrid = (int)std::min<int64_t>(4096, (g.nloc + NTHREADS - 1) / NTHREADS);
-      hip_check(h, hipMalloc(&h->p2gbuf, (size_t)(g.nzl + 2) * g.P * sizeof(cplx)), "hipMalloc(p2gbuf)");
+      const size_t lb = (size_t)(g.nzl + 2) * g.P * sizeof(cplx);
+      hip_check(h, hipMalloc(&h->p2gbuf, lb), "hipMalloc(p2gbuf)");
+      hip_check(h, hipMemsetAsync(h->p2gbuf, 0, lb, h->stream), "hipMemset");
+      const Geo gl = p2m_lap_geo(h);
+      h->p2lapgrid = occupancy_grid(h, kernel_lap(true, dim, ani), stencil_tiles(gl, dim, alpha_rows_per_thread()));
+      for (int J = 0; J + 1 < h->m - 1; J += 2) {
+        const void *fm = kernel_p2m(dim, J, true, ani);
+        h->p2mgrid[J] = fm ? occupancy_grid(h, fm, stencil_tiles(g, dim, p2m_rows_per_thread(J))) : 0;
+      }
     }
     if (p2_split(h)) {
       // the boundary kernel: one thread per cell of the 4 planes, grid-stride over at
@@ -999,6 +1029,8 @@ void alloc_all(nls_handle *h) {
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("NLS_P2_BLIND")) h->p2_blind = std::atoi(e) != 0;
     h->p2grid = p2_grid(h);
+    if (h->p2reg)
+      for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, h->p2mgrid[J]);
     hip_check(h, hipMalloc(&h->p2, p2state_bytes() * h->nbasis), "hipMalloc(p2)");  // one per basis
     hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes() * h->nbasis, h->stream), "hipMemset");
     hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)),

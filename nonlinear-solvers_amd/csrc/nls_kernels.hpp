@@ -66,11 +66,11 @@ constexpr int P2D_WAVE_XO = 64, P2D_ROWS = 4, P2D_MAXJ = 14;  // == P2D_XO, P2D_
 //   p2b    : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* lbuf, int poff)
 //            -- the slab's planes 0, 1, nzl-2, nzl-1 of k_p2d<J, hz> (nls_pass2b.hpp)
 const void *kernel_p2b(int J, bool hz);
-//   p2g_lap: (const cplx* S_J, Geo g, cplx* lbuf)  -- L S_J at local planes [-1, nzl] (nls_pass2g.hpp)
-//   p2g    : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* lbuf, int poff)
-//            -- the register two-vector pass over planes [g.qa, g.qb); J even <= 28
-const void *kernel_p2g(int dim, int J, bool hz, bool ani);
-const void *kernel_p2g_lap(int dim, bool ani);
+//   p2m    : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* lbuf, int poff)
+//            -- the register two-vector pass (nls_pass2g.hpp; lbuf = y = L S_J at local planes
+//            [-1, nzl], local plane 0 at lbuf + P, from k_lap); J even <= 28
+const void *kernel_p2m(int dim, int J, bool hz, bool ani);
+int p2m_rows_per_thread(int J);
 const void *kernel_p2b_lap();
 constexpr int P2B_LPLANES_H = 8;  // == P2B_LPLANES: planes of the lbuf scratch
 //   p2tail: (P2State*, KState*, const cplx* sums, int m);  p2tfin: (const P2State*, KState*, int m, int nf)

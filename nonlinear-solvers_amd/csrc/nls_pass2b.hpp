@@ -18,7 +18,7 @@
 //               sum_l aZ[l] S_l (nls_pass2.hpp), their stores and the pass's dot
 //               products, in k_p2d's column layout and evaluation order.
 #pragma once
-#include "nls_pass2d.hpp"
+#include "nls_pass2g.hpp"  // p2_split_store
 
 namespace nls {
 
@@ -143,31 +143,7 @@ __global__ __launch_bounds__(NTHREADS) void k_p2b(cplx *__restrict__ W, int64_t 
       if constexpr (J == 0) acc[NC - 1].re = fma(sv[0].re, sv[0].re, fma(sv[0].im, sv[0].im, acc[NC - 1].re));
     }
   }
-#pragma unroll
-  for (int c = 0; c < NH; ++c) {
-    const double a = wave_sum(acc[c].re), b = wave_sum(acc[c].im);
-    if (lane == 0) red[w][c] = {a, b};
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < NC; c += NTHREADS) {
-    cplx v;
-    if constexpr (HZ) {
-      // column c -> (wave parity, accumulator): X set on even waves, Z set on odd ones
-      int par, a;
-      if (c <= J) { par = 0; a = c; }                      // S_l^H X
-      else if (c <= 2 * J + 1) { par = 1; a = c - J - 1; }  // S_l^H Z
-      else if (c == 2 * J + 2) { par = 0; a = J + 1; }      // X^H X
-      else if (c == 2 * J + 3) { par = 1; a = J + 1; }      // X^H Z
-      else if (c == 2 * J + 4) { par = 1; a = J + 2; }      // Z^H Z
-      else { par = 0; a = J + 2; }                          // ||S_0||^2 (J = 0)
-      v = red[par][a] + red[par + 2][a];
-    } else {
-      v = red[0][c];
-#pragma unroll
-      for (int q = 1; q < NTHREADS / 64; ++q) v += red[q][c];
-    }
-    part[(int64_t)c * nb + poff + blockIdx.x] = v;
-  }
+  p2_split_store<J, HZ, NC, NH>(acc, red, part, nb, poff);
 }
 
 }  // namespace nls

@@ -1,143 +1,132 @@
-// nls_pass2g.hpp -- the two-vector basis pass without LDS staging: the form for
+// nls_pass2g.hpp -- the two-vector basis pass without LDS staging (k_p2m): the form for
 // the operators and shapes the LDS-DMA pass k_p2d does not take -- the G2
 // anisotropic operator div(c grad) (nlsolvers/common/include/laplacians.hpp:54-103,
 // 158-218) of the G2 NLSE drivers (m = 25 in 3D, nlse_cubic_driver_3d.cpp:112-114;
 // 20 in 2D), whose J ring would exceed the LDS, and isotropic grids with ny % 4 != 0
 // or m > 18.  The scheme, coefficients and per-cell formulas are k_p2d's
-// (nls_pass2.hpp); the pass is split in two launches:
+// (nls_pass2.hpp); the pass is two launches:
 //
-//   k_p2g_lap : y = L S_J at local planes [-1, nzl] into lbuf (nzl + 2 planes; the
-//               ghost planes from the two-plane halo, 0 outside the grid)
-//   k_p2g     : per cell of the slab: L^2 S_J = L y from lbuf, then
-//               X = bX1 y + sum_l aX[l] S_l, Z = bZ2 L y + bZ1 y + sum_l aZ[l] S_l,
-//               their stores and the pass's dots S_l^H X, S_l^H Z, X^H X, X^H Z,
-//               Z^H Z (+ ||S_0||^2 at J = 0) in k_p2d's column layout.
+//   k_lap  : y = L S_J at local planes [-1, nzl] (the neighbour slabs' first planes
+//            from the two-plane halo) into lbuf
+//   k_p2m  : the register-queue march over y, which gives every cell y and L y =
+//            L^2 S_J; X = bX1 y + sum_l aX[l] S_l, Z = bZ2 L y + bZ1 y + sum_l aZ[l]
+//            S_l, their stores and the pass's dots in k_p2d's column layout.
 //
-// Per pass that moves lbuf once more than k_p2d (written, then read with the
-// stencil) and, for div(c grad), c twice: at m = 25 a G2 step moves ~236 vectors
-// instead of the one-vector passes' ~374 (bench.py moved_bytes_per_cell_step).
+// Per pass that moves y once more than k_p2d (written, then marched) and, for
+// div(c grad), c twice: at m = 25 a G2 step moves ~236 vectors instead of the
+// one-vector passes' ~374 (bench.py moved_bytes_per_cell_step).  (A per-cell form
+// with the stencils of y through L1/L2 ran at ~3.5 TB/s, the march at ~5.3 TB/s;
+// measured in round 3 and removed.)
 #pragma once
 #include "nls_pass2d.hpp"
+#include "nls_stencil.hpp"
 
 namespace nls {
 
-struct LGeo {
-  int nx, ny, P, nz, z0;  // ny: rows per plane (3D), 1 (2D: "planes" are grid rows)
-  double s, sdi, sdb;
-};
-__device__ __forceinline__ LGeo lgeo(const Geo &g) {
-  return {(int)g.nx, (int)g.nyp, (int)g.P, (int)g.npl, (int)g.z0, g.s, g.sd_in, g.sd_bd};
-}
-
-// (L V) at local plane k, row y, column x (laplacians.hpp:10-105 isotropic, incl.
-// the 3D flat-index y-wrap; ANI: face weights (c_a + c_b)/2, diagonal -sum of the
-// weights, as nls_stencil.hpp march); 0 outside the grid.  V and C point at local
-// plane 0; their ghost planes hold the neighbouring slabs' planes.
-template <int DIM, bool ANI>
-__device__ __forceinline__ cplx lap_cell(const cplx *__restrict__ V, const double *__restrict__ C,
-                                         const LGeo &g, int k, int y, int x) {
-  const cplx zero = {0.0, 0.0};
-  const int kk = g.z0 + k;
-  if (x < 0 || x >= g.nx || kk < 0 || kk >= g.nz) return zero;
-  const int p = k * g.P + y * g.nx + x;
-  const bool exm = x > 0, exp_ = x + 1 < g.nx, ezm = kk > 0, ezp = kk + 1 < g.nz;
-  const cplx cur = V[p];
-  const cplx xm = exm ? V[p - 1] : zero, xp = exp_ ? V[p + 1] : zero;
-  const cplx prev = ezm ? V[p - g.P] : zero, next = ezp ? V[p + g.P] : zero;
-  if constexpr (DIM == 3) {
-    const bool eym = kk > 0 || y > 0, eyp = kk < g.nz - 1 || y < g.ny - 1;  // idx -/+ nx in range
-    const cplx ym = eym ? V[p - g.nx] : zero, yp = eyp ? V[p + g.nx] : zero;
-    if constexpr (ANI) {
-      const double cc = C[p];
-      const double wxm = exm ? 0.5 * (cc + C[p - 1]) : 0.0, wxp = exp_ ? 0.5 * (cc + C[p + 1]) : 0.0;
-      const double wym = eym ? 0.5 * (cc + C[p - g.nx]) : 0.0, wyp = eyp ? 0.5 * (cc + C[p + g.nx]) : 0.0;
-      const double wzm = ezm ? 0.5 * (cc + C[p - g.P]) : 0.0, wzp = ezp ? 0.5 * (cc + C[p + g.P]) : 0.0;
-      return g.s * ((((wzm * prev + wzp * next) + (wxm * xm + wxp * xp)) + (wym * ym + wyp * yp)) -
-                    (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * cur);
+// The per-workgroup partials of a pass whose accumulators are split over wave pairs
+// (HZ: X set on even waves, Z set on odd ones; k_p2g, k_p2b) in k_p2d's column order:
+// [S_l^H X (l <= J)] [S_l^H Z] [X^H X] [X^H Z] [Z^H Z] [||S_0||^2 (J = 0)], without Z
+// [S_l^H X] [X^H X] [||S_0||^2] summed over all four waves.
+template <int J, bool HZ, int NC, int NH>
+__device__ __forceinline__ void p2_split_store(cplx (&acc)[NH], cplx (&red)[NTHREADS / 64][NH],
+                                               cplx *__restrict__ part, int nb, int poff) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < NH; ++c) {
+    const double a = wave_sum(acc[c].re), b = wave_sum(acc[c].im);
+    if (lane == 0) red[w][c] = {a, b};
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < NC; c += NTHREADS) {
+    cplx v;
+    if constexpr (HZ) {
+      int par, a;
+      if (c <= J) { par = 0; a = c; }                      // S_l^H X
+      else if (c <= 2 * J + 1) { par = 1; a = c - J - 1; }  // S_l^H Z
+      else if (c == 2 * J + 2) { par = 0; a = J + 1; }      // X^H X
+      else if (c == 2 * J + 3) { par = 1; a = J + 1; }      // X^H Z
+      else if (c == 2 * J + 4) { par = 1; a = J + 2; }      // Z^H Z
+      else { par = 0; a = J + 2; }                          // ||S_0||^2 (J = 0)
+      v = red[par][a] + red[par + 2][a];
     } else {
-      const bool bd = !exm || !exp_ || y == 0 || y == g.ny - 1 || !ezm || !ezp;
-      return (bd ? g.sdb : g.sdi) * cur + g.s * (((prev + next) + (xm + xp)) + (ym + yp));
+      v = red[0][c];
+#pragma unroll
+      for (int q = 1; q < NTHREADS / 64; ++q) v += red[q][c];
     }
-  } else {
-    if constexpr (ANI) {
-      const double cc = C[p];
-      const double wxm = exm ? 0.5 * (cc + C[p - 1]) : 0.0, wxp = exp_ ? 0.5 * (cc + C[p + 1]) : 0.0;
-      const double wzm = ezm ? 0.5 * (cc + C[p - g.P]) : 0.0, wzp = ezp ? 0.5 * (cc + C[p + g.P]) : 0.0;
-      return g.s * (((wzm * prev + wzp * next) + (wxm * xm + wxp * xp)) - ((wzm + wzp) + (wxm + wxp)) * cur);
-    } else {
-      const bool bd = !exm || !exp_ || !ezm || !ezp;
-      return g.s * ((prev + next) + (xm + xp)) + (bd ? g.sdb : g.sdi) * cur;
-    }
+    part[(int64_t)c * nb + poff + blockIdx.x] = v;
   }
 }
 
-template <int DIM, bool ANI>
-__global__ __launch_bounds__(NTHREADS) void k_p2g_lap(const cplx *__restrict__ SJ, Geo g,
-                                                      cplx *__restrict__ lbuf) {
-  const LGeo lg = lgeo(g);
-  const double *C = g.cf;
-  const int P = lg.P, nx = lg.nx;
-  const int total = ((int)g.nzl + 2) * P;
-  for (int e = blockIdx.x * NTHREADS + threadIdx.x; e < total; e += gridDim.x * NTHREADS) {
-    const int k = e / P - 1, r = e - (k + 1) * P;
-    const int y = DIM == 3 ? r / nx : 0, x = DIM == 3 ? r - y * nx : r;
-    lbuf[e] = lap_cell<DIM, ANI>(SJ, C, lg, k, y, x);
-  }
-}
-
-// Cells of local planes [g.qa, g.qb); partials at part[c * nb + poff + blockIdx.x].
+// The pass marches y = L S_J (lbuf, written by k_lap over planes [-1, nzl] on the same
+// tiles) with nls_stencil.hpp's register-queue
+// tile march, which hands each cell y and L y (z neighbours from registers, x from
+// the neighbouring lane, y from the thread's rows; only tile-edge values through
+// L1/L2), then streams S_0..S_J as k_update does: every load of every row first,
+// then X, Z, their stores and the dots.  All NC accumulators per lane (one wave per
+// SIMD from J ~ 14); the coefficients are broadcast from LDS at every use.
+template <int J> struct P2mRB { static constexpr int v = J <= 4 ? 2 : 1; };
 template <int DIM, int J, bool HZ, bool ANI>
-__global__ __launch_bounds__(NTHREADS) void k_p2g(cplx *__restrict__ W, int64_t vs, Geo g,
+__global__ __launch_bounds__(NTHREADS) void k_p2m(cplx *__restrict__ W, int64_t vs, Geo g,
                                                   const P2State *__restrict__ ps, cplx *__restrict__ part,
                                                   int nb, const cplx *__restrict__ lbuf, int poff) {
   constexpr int NC = (HZ ? 2 * (J + 1) + 3 : J + 2) + (J == 0 ? 1 : 0);
-  // the combination coefficients by wave-uniform (scalar) loads at their use: staged in
-  // LDS, the compiler hoisted them into 8 (J + 1) VGPRs
-  const cplx *__restrict__ cX = ps->aX, *__restrict__ cZ = ps->aZ;
+  constexpr int RB = P2mRB<J>::v;
+  __shared__ cplx cX[J + 1], cZ[J + 1];
+  for (int l = threadIdx.x; l <= J; l += NTHREADS) {
+    cX[l] = ps->aX[l];
+    cZ[l] = ps->aZ[l];
+  }
+  __syncthreads();
   const cplx bX1 = ps->bX1, bZ1 = ps->bZ1, bZ2 = ps->bZ2;
-  const LGeo lg = lgeo(g);
-  const double *C = g.cf;
-  const int P = lg.P, nx = lg.nx;
-  const cplx *L0 = lbuf + P;  // y at local plane 0
   cplx *__restrict__ Xo = W + (int64_t)(J + 1) * vs;
   cplx *__restrict__ Zo = W + (int64_t)(J + 2) * vs;
   const cplx zero = {0.0, 0.0};
   cplx acc[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) acc[c] = zero;
-  const int e0 = g.qa * P, total = (g.qb - g.qa) * P;
-  for (int e = blockIdx.x * NTHREADS + threadIdx.x; e < total; e += gridDim.x * NTHREADS) {
-    const int flat = e0 + e, k = flat / P, r = flat - k * P;
-    const int y = DIM == 3 ? r / nx : 0, x = DIM == 3 ? r - y * nx : r;
-    const cplx l1 = L0[flat];
-    cplx sv[J + 1];
+  const cplx *L0 = lbuf + g.P;  // y at local plane 0 (planes -1 .. nzl)
+  auto body = [&](const int *p, const cplx *cur, const cplx *lap, const bool *ok) {
+    cplx sv[RB][J + 1];
 #pragma unroll
-    for (int l = 0; l < J; ++l) sv[l] = ld_nt(W + l * vs + flat);
-    sv[J] = W[J * vs + flat];
-    cplx Xa = cmul(bX1, l1), Xb = zero;
+    for (int r = 0; r < RB; ++r) {
+      const cplx *__restrict__ src = W + p[r];
 #pragma unroll
-    for (int l = 0; l <= J; ++l) cmac((l & 1) ? Xb : Xa, cX[l], sv[l]);
-    const cplx X = Xa + Xb;
-    st_nt(Xo + flat, X);
-#pragma unroll
-    for (int l = 0; l <= J; ++l) cjmac(acc[l], sv[l], X);
-    if constexpr (HZ) {
-      const cplx l2 = lap_cell<DIM, ANI>(L0, C, lg, k, y, x);
-      cplx Za = cmul(bZ2, l2) + cmul(bZ1, l1), Zb = zero;
-#pragma unroll
-      for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, cZ[l], sv[l]);
-      const cplx Z = Za + Zb;
-      st_nt(Zo + flat, Z);
-#pragma unroll
-      for (int l = 0; l <= J; ++l) cjmac(acc[J + 1 + l], sv[l], Z);
-      acc[2 * J + 2].re = fma(X.re, X.re, fma(X.im, X.im, acc[2 * J + 2].re));
-      cjmac(acc[2 * J + 3], X, Z);
-      acc[2 * J + 4].re = fma(Z.re, Z.re, fma(Z.im, Z.im, acc[2 * J + 4].re));
-    } else {
-      acc[J + 1].re = fma(X.re, X.re, fma(X.im, X.im, acc[J + 1].re));
+      for (int l = 0; l < J; ++l) {
+        sv[r][l] = ok[r] ? ld_nt(src) : zero;
+        src += vs;
+      }
+      sv[r][J] = ok[r] ? *src : zero;
     }
-    if constexpr (J == 0) acc[NC - 1].re = fma(sv[0].re, sv[0].re, fma(sv[0].im, sv[0].im, acc[NC - 1].re));
-  }
+    asm volatile("" ::: "memory");  // keep the coefficient LDS reads at their use
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (!ok[r]) continue;
+      cplx Xa = cmul(bX1, cur[r]), Xb = zero;
+#pragma unroll
+      for (int l = 0; l <= J; ++l) cmac((l & 1) ? Xb : Xa, cX[l], sv[r][l]);
+      const cplx X = Xa + Xb;
+      st_nt(Xo + p[r], X);
+#pragma unroll
+      for (int l = 0; l <= J; ++l) cjmac(acc[l], sv[r][l], X);
+      if constexpr (HZ) {
+        cplx Za = cmul(bZ2, lap[r]) + cmul(bZ1, cur[r]), Zb = zero;
+#pragma unroll
+        for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, cZ[l], sv[r][l]);
+        const cplx Z = Za + Zb;
+        st_nt(Zo + p[r], Z);
+#pragma unroll
+        for (int l = 0; l <= J; ++l) cjmac(acc[J + 1 + l], sv[r][l], Z);
+        acc[2 * J + 2].re = fma(X.re, X.re, fma(X.im, X.im, acc[2 * J + 2].re));
+        cjmac(acc[2 * J + 3], X, Z);
+        acc[2 * J + 4].re = fma(Z.re, Z.re, fma(Z.im, Z.im, acc[2 * J + 4].re));
+      } else {
+        acc[J + 1].re = fma(X.re, X.re, fma(X.im, X.im, acc[J + 1].re));
+      }
+      if constexpr (J == 0)
+        acc[NC - 1].re = fma(sv[r][0].re, sv[r][0].re, fma(sv[r][0].im, sv[r][0].im, acc[NC - 1].re));
+    }
+  };
+  march<cplx, DIM, RB, true, ANI>(L0, g, body);
   block_store<NC>(acc, part, nb, poff);
 }
 
