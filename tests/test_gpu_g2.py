@@ -286,10 +286,14 @@ def test_sinc_action_matches_oracle(dim, nx, ny, nz):
             assert rel_l2(s.krylov_apply(u, t, nls_amd.F_SINC), ref) <= TOL_KRYLOV
 
 
+@pytest.mark.parametrize("pass2", ["1", "0"], ids=["two_vector", "one_vector"])
 @pytest.mark.parametrize("dim,nx,ny,nz,m", [(3, 12, 12, 12, 15), (3, 70, 9, 11, 15), (2, 32, 32, 1, 25),
                                             (2, 300, 20, 1, 25)])
-def test_sewi_trajectory_matches_oracle(dim, nx, ny, nz, m):
-    """The sEWI driver loop (nlse_cubic_sewi_driver_3d.cpp:116-119): step_sewi(i), apply_bc."""
+def test_sewi_trajectory_matches_oracle(monkeypatch, pass2, dim, nx, ny, nz, m):
+    """The sEWI driver loop (nlse_cubic_sewi_driver_3d.cpp:116-119): step_sewi(i), apply_bc;
+    its three Krylov actions per step by the two-vector passes (default) or the
+    one-vector passes (NLS_PASS2=0)."""
+    monkeypatch.setenv("NLS_PASS2", pass2)
     L, dt, steps = 4.0, 1e-3, 8
     dx = 2 * L / (nx - 1)
     u, mf, c = fields(dim, nx, ny, nz, seed=9)
