@@ -135,7 +135,8 @@ struct nls_handle {
   // issued eagerly, never replayed from a graph captured warm (run-to-run bitwise
   // reproducibility of "set state; step" sequences)
   bool p2_fresh = true;
-  bool p2_pr = false;          // real field marched as cell pairs by k_p2d (p2_geo)
+  bool p2_pr = false;
+  bool p2_ani = false;         // k_p2d with the G2 operator (nls_pass2a.hip)          // real field marched as cell pairs by k_p2d (p2_geo)
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
@@ -733,7 +734,8 @@ int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz) {
 // vector, while the interior planes run as k_p2d on the compute stream
 // (nls_pass2b.hpp).
 bool p2_split(const nls_handle *h) {
-  return h->collective && min_slab_planes(h) >= 8 && h->p2_split_on && !h->p2_d2 && !h->p2_pr && !h->p2reg;
+  return h->collective && min_slab_planes(h) >= 8 && h->p2_split_on && !h->p2_d2 && !h->p2_pr && !h->p2reg &&
+         !h->p2_ani;
 }
 int p2_bnd_tiles(const nls_handle *h) { return h->p2b_dma ? 2 * p2_tiles(h, 0, 2, 2) : h->p2bgrid; }
 int p2_grid(const nls_handle *h, int J = 0) {
@@ -795,7 +797,9 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
     int J = sched[si].first, ns = sched[si].second;
     const int out = J + ns;  // the pass's last vector: the next stencil vector
     int nb = p2_grid(h, J);
-    const void *fn = h->p2reg ? nullptr : kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
+    const void *fn = h->p2reg ? nullptr
+                     : h->p2_ani ? kernel_pass2a(J, ns == 2)
+                                 : kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
     if (h->p2reg) {
       // y = L S_J over the slab and its neighbour planes, then the pass over y.  (Issuing
@@ -991,8 +995,17 @@ void alloc_all(nls_handle *h) {
     // 2D slabs, m > 18); J <= 28
     const bool reg = c && !h->kg && h->nbasis == 1 && h->m >= 3 && h->m <= MMAX - 2 &&
                      (!h->collective || min_slab_planes(h) >= 4) && g.nloc + 2 * g.P < (int64_t(1) << 31);
-    h->pass2 = want && ((base && dma) || reg);
-    h->p2reg = h->pass2 && !(base && dma);
+    // k_p2d with the G2 operator div(c grad) (the c field staged beside S_J): 3D
+    // complex, whole 4-row tiles, nx even (16-B pairs of c), J <= P2D_MAXJ_A (m <= 26);
+    // NLS_P2_REG=1 keeps the register form
+    const int maxj = ((h->m - 3) / 2) * 2;  // the schedule's last J
+    const bool adma = c && ani && !h->kg && dim == 3 && h->nbasis == 1 && h->m >= 3 && g.nyp % P2D_ROWS == 0 &&
+                      g.nyp >= P2D_ROWS && g.nx % 2 == 0 && g.nx >= 4 && maxj <= P2D_MAXJ_A &&
+                      (!h->collective || min_slab_planes(h) >= 4) && g.nloc + 2 * g.P < (int64_t(1) << 31) &&
+                      !(std::getenv("NLS_P2_REG") && std::atoi(std::getenv("NLS_P2_REG")));
+    h->pass2 = want && ((base && dma) || adma || reg);
+    h->p2reg = h->pass2 && !(base && dma) && !adma;
+    h->p2_ani = h->pass2 && !h->p2reg && ani;
     h->p2_d2 = h->pass2 && !h->p2reg && dim == 2;
     h->p2_pr = h->pass2 && !h->p2reg && !c;
   }

@@ -46,11 +46,26 @@ constexpr int P2D_TR = 4;             // rows per tile (one per wave)
 constexpr int P2D_SR = P2D_TR + 4;    // S_J rows staged per plane (y0-2 .. y0+5)
 constexpr int P2D_SRB = 1024 + 64;    // bytes per staged S_J row: x0..x0+63, then x0-2, x0-1, x0+64, x0+65
 constexpr int P2D_LR = P2D_TR + 2;    // L S_J rows shared per plane (y0-1 .. y0+4)
-constexpr int P2D_JMAX = 14;          // largest J whose rings fit 160 KiB of LDS
+constexpr int P2D_JMAX = 14;          // largest J of the isotropic passes (m <= 18)
+constexpr int P2D_JMAX_A = 22;        // largest J of the anisotropic passes (G2: m = 25 -> J <= 22)
 constexpr int P2D_GHOST = 2;          // ghost planes per side of a stored vector (radius-2 march)
 constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
+// A (the G2 operator div(c grad)): the c field staged beside S_J, same rows and
+// planes: 8 rows of x0..x0+63 (512 B of f64 each), then the 8 rows' 4 halo cells
+// (x0-2, x0-1, x0+64, x0+65; 32 B each)
+constexpr int P2D_CRB = 512;
+constexpr int P2D_CSB = P2D_SR * P2D_CRB + P2D_SR * 32;
 #ifndef NLS_P2D_OCC2_MAXJ
 #define NLS_P2D_OCC2_MAXJ 4   // two workgroups per CU up to this J
+#endif
+#ifndef NLS_P2A_OCC2_MAXJ
+#define NLS_P2A_OCC2_MAXJ 4   // anisotropic passes: two workgroups per CU up to this J (J = 4: late J ring, 0.655 -> 0.416 ms at G2 256^3)
+#endif
+#ifndef NLS_P2A_EARLY
+#define NLS_P2A_EARLY 1       // anisotropic passes at one workgroup per CU: early issue (J < 22)
+#endif
+#ifndef NLS_P2A_DS1
+#define NLS_P2A_DS1 1         // anisotropic passes at one workgroup per CU, J > NLS_P2D_DS3_MAXJ: S look-ahead
 #endif
 #ifndef NLS_P2D_EARLY
 #define NLS_P2D_EARLY 1  // one workgroup per CU: issue a step's DMAs before its wait (needs an extra S slot)
@@ -70,69 +85,124 @@ constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
 #ifndef NLS_P2D_OCC0
 #define NLS_P2D_OCC0 3  // workgroups per CU of the J = 0 pass (S look-ahead 1; 512^3: 1.40 vs 1.61 ms at 2)
 #endif
-__host__ __device__ constexpr int p2d_occ(int J) { return J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ ? 2 : 1); }
+__host__ __device__ constexpr int p2d_occ(int J, bool A = false) {
+  return A ? (J <= NLS_P2A_OCC2_MAXJ ? 2 : 1) : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ ? 2 : 1));
+}
 // S ring: the planes k .. k+2 being read, DS planes of look-ahead and the slot of
 // plane k-2 (free since the previous step's barrier), into which a step issues
 // before its own wait and barrier
-__host__ __device__ constexpr int p2d_ds(int J) {
-  return p2d_occ(J) >= 3 ? 1
-                          : (p2d_occ(J) == 2 ? (J == 0 ? 3 : (J <= NLS_P2D_DS2_MAXJ ? 2 : 1))
-                                             : (J == 0 ? 6 : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J <= 12 || !NLS_P2D_EARLY ? 1 : 0))));
+__host__ __device__ constexpr int p2d_ds(int J, bool A = false) {
+  return A ? (p2d_occ(J, A) == 2 ? (J == 0 ? 2 : 1) : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J >= 22 ? 1 : NLS_P2A_DS1)))
+           : (p2d_occ(J) >= 3 ? 1
+                                : (p2d_occ(J) == 2
+                                       ? (J == 0 ? 3 : (J <= NLS_P2D_DS2_MAXJ ? 2 : 1))
+                                       : (J == 0 ? 6 : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J <= 12 || !NLS_P2D_EARLY ? 1 : 0)))));
 }
 // early issue only at one workgroup per CU (two: the other workgroup covers the wait,
-// and the LDS is short)
-__host__ __device__ constexpr bool p2d_early(int J) { return NLS_P2D_EARLY && p2d_occ(J) == 1; }
-__host__ __device__ constexpr int p2d_nsl(int J) { return p2d_ds(J) + 3 + (p2d_early(J) ? 1 : 0); }
-__host__ __device__ constexpr int p2d_off_l(int J) { return p2d_nsl(J) * P2D_SR * P2D_SRB; }
-__host__ __device__ constexpr int p2d_off_j(int J) { return p2d_off_l(J) + 2 * P2D_LR * 1024; }
-__host__ __device__ constexpr int p2d_avail(int J) {
-  return P2D_LDS / p2d_occ(J) - p2d_off_j(J) - 2 * (J + 1) * 16;
+// and the LDS is short); not where the anisotropic rings leave no slot for it
+__host__ __device__ constexpr bool p2d_early(int J, bool A = false) {
+  return A ? NLS_P2A_EARLY && p2d_occ(J, A) == 1 && J < 22 : NLS_P2D_EARLY && p2d_occ(J) == 1;
+}
+__host__ __device__ constexpr int p2d_nsl(int J, bool A = false) { return p2d_ds(J, A) + 3 + (p2d_early(J, A) ? 1 : 0); }
+__host__ __device__ constexpr int p2d_off_c_ring(int J, bool A = false) { return p2d_nsl(J, A) * P2D_SR * P2D_SRB; }
+__host__ __device__ constexpr int p2d_off_l(int J, bool A = false) {
+  return p2d_off_c_ring(J, A) + (A ? p2d_nsl(J, A) * P2D_CSB : 0);
+}
+__host__ __device__ constexpr int p2d_off_j(int J, bool A = false) { return p2d_off_l(J, A) + 2 * P2D_LR * 1024; }
+__host__ __device__ constexpr int p2d_avail(int J, bool A = false) {
+  return P2D_LDS / p2d_occ(J, A) - p2d_off_j(J, A) - 2 * (J + 1) * 16;
 }
 // J ring: NP whole planes of the J stored vectors of the wave's row (1 KiB each),
-// the plane being read + NP-1 planes of look-ahead
-__host__ __device__ constexpr int p2d_np(int J) {
+// the plane being read + NP-1 planes of look-ahead.  NP = 1 ("late" J ring, the long
+// anisotropic passes): the wave reads its J rows of plane k into registers and then
+// DMAs plane k+1 into the same slot, so the look-ahead is one step
+__host__ __device__ constexpr int p2d_np(int J, bool A = false) {
   return J == 0 ? 0
-                : (p2d_avail(J) / (P2D_TR * 1024 * J) < NLS_P2D_NP_MAX ? p2d_avail(J) / (P2D_TR * 1024 * J)
-                                                                       : NLS_P2D_NP_MAX);
+                : (p2d_avail(J, A) / (P2D_TR * 1024 * J) < NLS_P2D_NP_MAX ? p2d_avail(J, A) / (P2D_TR * 1024 * J)
+                                                                          : NLS_P2D_NP_MAX);
 }
-__host__ __device__ constexpr int p2d_off_c(int J) { return p2d_off_j(J) + p2d_np(J) * J * P2D_TR * 1024; }
-__host__ __device__ constexpr int p2d_lds_bytes(int J) { return p2d_off_c(J) + 2 * (J + 1) * 16; }
-__host__ __device__ constexpr bool p2d_rings_ok(int J) {
-  return J == 0 || (J <= P2D_JMAX && p2d_np(J) >= 2 && p2d_lds_bytes(J) * p2d_occ(J) <= P2D_LDS);
+__host__ __device__ constexpr bool p2d_late(int J, bool A = false) { return J > 0 && p2d_np(J, A) == 1; }
+__host__ __device__ constexpr int p2d_off_c(int J, bool A = false) {
+  return p2d_off_j(J, A) + p2d_np(J, A) * J * P2D_TR * 1024;
+}
+__host__ __device__ constexpr int p2d_lds_bytes(int J, bool A = false) { return p2d_off_c(J, A) + 2 * (J + 1) * 16; }
+__host__ __device__ constexpr bool p2d_rings_ok(int J, bool A = false) {
+  return J == 0 ? p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS
+                : (J <= (A ? P2D_JMAX_A : P2D_JMAX) && p2d_np(J, A) >= (A ? 1 : 2) &&
+                   p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS);
 }
 static_assert(p2d_rings_ok(2) && p2d_rings_ok(4) && p2d_rings_ok(6) && p2d_rings_ok(8) && p2d_rings_ok(10) &&
               p2d_rings_ok(12) && p2d_rings_ok(14), "rings do not fit the LDS");
+static_assert(p2d_rings_ok(0, true) && p2d_rings_ok(2, true) && p2d_rings_ok(4, true) && p2d_rings_ok(6, true) &&
+              p2d_rings_ok(8, true) && p2d_rings_ok(10, true) && p2d_rings_ok(12, true) &&
+              p2d_rings_ok(14, true) && p2d_rings_ok(16, true) && p2d_rings_ok(18, true) &&
+              p2d_rings_ok(20, true) && p2d_rings_ok(22, true),
+              "anisotropic rings do not fit the LDS");
 
-// VMEM ops issued after the last one step i needs, up to its wait (see k_p2d):
-// per step the wave issues [4 S-row DMAs (2 rows: main + halo)][J J-row DMAs]
-// (then waits, with NLS_P2D_EARLY) ... [STW stores]; the prologue issues the S
-// groups of planes k0+2 .. k0+1+DS, then the J planes 0 .. NP-2.  Step i needs
-// S(k+2) and J plane k.
-constexpr int P2D_NSD = 4;  // S DMAs per wave and plane
-__host__ __device__ constexpr int p2d_after(int J, int STW, int i) {
-  const int DS = p2d_ds(J), NP = p2d_np(J), G = P2D_NSD + J + STW, own = p2d_early(J) ? P2D_NSD + J : 0;
-  // S(k+2): issued by step i-DS (first group; at i itself when DS = 0) or the prologue
-  const int nS = i >= DS ? (DS == 0 ? J : J + STW + (DS - 1) * G + own)
-                         : P2D_NSD * (DS - 1 - i) + (NP > 0 ? NP - 1 : 0) * J + i * G + own;
-  if (J == 0) return nS;
-  const int nJ = i >= NP - 1 ? STW + (NP - 2) * G + own : (NP - 2 - i) * J + i * G + own;
-  return nJ < nS ? nJ : nS;
+// VMEM ops issued after the last one step i needs, up to its wait (see k_p2d): a
+// replay of the wave's issue order.  After the prologue's full wait the wave issues
+// the S groups of planes k0+2 .. k0+1+DS (NSD DMAs each: 2 S rows, main + halo, and
+// with A the 2 c rows, main + halo) and the J groups of planes k0 .. k0+NP-2 (late:
+// plane k0); then per step: [S group k+DS+2 and J group k+NP-1] before the wait
+// (early) or after it, the late J group k+1 after the J rows are read, then the STW
+// stores.  Step i needs S(k+2) and J plane k.
+__host__ __device__ constexpr int p2d_nsd(bool A) { return A ? 6 : 4; }
+__host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = false) {
+  const int DS = p2d_ds(J, A), NP = p2d_np(J, A), NSD = p2d_nsd(A);
+  const bool early = p2d_early(J, A), late = p2d_late(J, A);
+  int n = 0, lastS = 0, lastJ = 0;
+  for (int d = 0; d < DS; ++d) {
+    n += NSD;
+    if (d == i) lastS = n;
+  }
+  if (J > 0) {
+    const int pj = late ? 1 : NP - 1;
+    for (int d = 0; d < pj; ++d) {
+      n += J;
+      if (d == i) lastJ = n;
+    }
+  }
+  for (int s = 0;; ++s) {
+    if (early) {
+      n += NSD;
+      if (s + DS == i) lastS = n;
+      if (J > 0 && !late) {
+        n += J;
+        if (s + NP - 1 == i) lastJ = n;
+      }
+    }
+    if (s == i) break;  // the wait of step i
+    if (!early) {
+      n += NSD;
+      if (s + DS == i) lastS = n;
+      if (J > 0 && !late) {
+        n += J;
+        if (s + NP - 1 == i) lastJ = n;
+      }
+    }
+    if (late) {
+      n += J;
+      if (s + 1 == i) lastJ = n;
+    }
+    n += STW;
+  }
+  const int aS = n - lastS, aJ = J > 0 ? n - lastJ : 1 << 20;
+  return aS < aJ ? aS : aJ;
 }
-__host__ __device__ constexpr int p2d_i0(int J) {
-  return J == 0 ? p2d_ds(J) : (p2d_np(J) - 1 > p2d_ds(J) ? p2d_np(J) - 1 : p2d_ds(J));
-}
+// from this step on every wait is the same (a safe bound of the replay's warm-up)
+__host__ __device__ constexpr int p2d_i0(int J, bool A = false) { return p2d_ds(J, A) + p2d_np(J, A) + 1; }
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 0 ? 0 : (N > 63 ? 63 : N)) : "memory");
 }
-template <int J, int STW, int I = 0> __device__ __forceinline__ void wait_step(int i) {
-  if constexpr (I >= p2d_i0(J)) {
-    wait_vm<p2d_after(J, STW, I)>();
+template <int J, int STW, bool A, int I = 0> __device__ __forceinline__ void wait_step(int i) {
+  if constexpr (I >= p2d_i0(J, A)) {
+    wait_vm<p2d_after(J, STW, I, A)>();
   } else {
     if (i == I) {
-      wait_vm<p2d_after(J, STW, I)>();
+      wait_vm<p2d_after(J, STW, I, A)>();
       return;
     }
-    wait_step<J, STW, I + 1>(i);
+    wait_step<J, STW, A, I + 1>(i);
   }
 }
 
@@ -147,6 +217,15 @@ __device__ __forceinline__ void dma16(const void *base, uint32_t voff, char *lds
   const void *g = static_cast<const char *>(base) + voff;
   if (aux) __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 2);
   else __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+// face weight of the G2 operator (nls_stencil.hpp face_w): (c_a + c_b)/2 where the face exists
+__device__ __forceinline__ double p2d_face(bool e, double ca, double cb) { return e ? 0.5 * (ca + cb) : 0.0; }
+// the same with a per-lane source address (the c rows: two rows per instruction)
+__device__ __forceinline__ void glds16(const char *g, char *lds) {
+  __builtin_amdgcn_global_load_lds(static_cast<const void *>(g), (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const char *g, char *lds) {
+  __builtin_amdgcn_global_load_lds(static_cast<const void *>(g), (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
 }
 // lane i <- lane i-1 / i+1 by DPP wave shifts (GFX9 wave_shr:1 / wave_shl:1; the
 // lane shifted in from outside the wave reads 0)
@@ -199,23 +278,26 @@ __device__ __forceinline__ cplx pr_lap(cplx c, cplx xm, cplx xp, cplx yz, double
   return {dga * c.re + s * (yz.re + (xm.im + c.im)), dgb * c.im + s * (yz.im + (c.re + xp.re))};
 }
 
-template <int J, bool HZ, bool D2 = false, bool PR = false>
-__global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
+template <int J, bool HZ, bool D2 = false, bool PR = false, bool A = false>
+__global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
                                                               const P2State *__restrict__ ps,
                                                               cplx *__restrict__ part, int nb,
                                                               const cplx *__restrict__ zbuf, int poff) {
-  static_assert(p2d_rings_ok(J), "rings exceed LDS");
-  constexpr int DS = p2d_ds(J), NSL = p2d_nsl(J), NP = p2d_np(J);
+  static_assert(p2d_rings_ok(J, A), "rings exceed LDS");
+  static_assert(!(A && (D2 || PR)), "the anisotropic pass is 3D complex");
+  constexpr int DS = p2d_ds(J, A), NSL = p2d_nsl(J, A), NP = p2d_np(J, A);
+  constexpr bool LATE = p2d_late(J, A);
   constexpr int STW = HZ ? 2 : 1;            // stores per step
   // columns: gX[0..J], (HZ: gZ[0..J], xx, xz, zz | xx); J = 0 also ||S_0||^2 (the
   // blind start, k_p2coef mode 2)
   constexpr int NC = (HZ ? 2 * (J + 1) + 3 : J + 2) + (J == 0 ? 1 : 0);
   constexpr int NPD = NP > 0 ? NP : 1;
   constexpr int RW = P2D_SRB / 16;           // cplx per staged S row (68)
-  __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J)];
+  __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J, A)];
   const cplx *Sr = reinterpret_cast<const cplx *>(smem);             // [NSL][P2D_SR][RW]
-  cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J));          // [2][P2D_LR][64]
-  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J));          // [J+1]
+  const double *Cr = reinterpret_cast<const double *>(smem + p2d_off_c_ring(J, A));  // A: [NSL][P2D_CSB/8]
+  cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J, A));       // [2][P2D_LR][64]
+  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J, A));       // [J+1]
   cplx *cZ = cX + (J + 1);                                           // [J+1]
   // w through readfirstlane: wave-uniform for the compiler too, so row and plane
   // logic stays scalar
@@ -262,6 +344,14 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   const uint32_t xoff = (uint32_t)clampx(x) * 16u;
   const int hc = (lane >> 2) & 3;
   const uint32_t hoff = (uint32_t)clampx(hc < 2 ? x0 - 2 + hc : x0 + 62 + hc) * 16u + (uint32_t)(lane & 3) * 4u;
+  // A: the c field (f64, nx even so that every pair of cells is one aligned 16 B):
+  // lane -> cells x0 + 2 (lane & 31) + {0, 1} (clamped into the row), halo lane
+  // (0..15) -> dword lane & 1 of cell x0-2, x0-1, x0+64, x0+65
+  const char *__restrict__ Cg = reinterpret_cast<const char *>(g.cf);
+  const int64_t P8 = (int64_t)P * 8;
+  const int64_t coff = (int64_t)min(x0 + 2 * (lane & 31), nx - 2) * 8;
+  const int hcc = (lane >> 1) & 3;
+  const int64_t choff = (int64_t)clampx(hcc < 2 ? x0 - 2 + hcc : x0 + 62 + hcc) * 8 + (lane & 1) * 4;
   // L S_J positions: main lane i -> x0 + i (row index i, x neighbours i-1 / i+1,
   // the halo cells 65 / 66 at the tile edges); extra pass lane 0 -> x0-1, lane 1
   // -> x0+64 (row indices 65 / 66, neighbours 64,0 / 63,67)
@@ -298,6 +388,23 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
       dma16(b_, xoff, dst_ + r_ * P2D_SRB, 0);                                          \
       if (lane < 16) dma4(b_, hoff, dst_ + r_ * P2D_SRB + 1024);                        \
     }                                                                                   \
+    if constexpr (A) {                                                                  \
+      /* the c rows of the same two S rows: lanes 0..31 / 32..63 two cells each of   \
+         row 2w / 2w+1, then their halo cells on lanes 0..15 (8 lanes x 4 B a row) */ \
+      char *cd_ = smem + p2d_off_c_ring(J, A) + (sl) * P2D_CSB;                         \
+      const int yc_ = y0 - 2 + 2 * w + (lane >> 5), kc_ = P2D_PLANE(p_, yc_), lc_ = kc_ - z0; \
+      const bool okc_ = kc_ >= 0 && kc_ < nz && lc_ >= -P2D_GHOST && lc_ < nzl + P2D_GHOST && \
+                        p_ <= k1 + 1;                                                   \
+      const char *cb_ = okc_ ? Cg + (p_ * P8 + (int64_t)yc_ * nx * 8)                   \
+                             : reinterpret_cast<const char *>(zbuf);                    \
+      glds16(cb_ + coff, cd_ + 2 * w * P2D_CRB);                                        \
+      const int yh_ = y0 - 2 + 2 * w + ((lane >> 3) & 1), kh_ = P2D_PLANE(p_, yh_), lh_ = kh_ - z0; \
+      const bool okh_ = kh_ >= 0 && kh_ < nz && lh_ >= -P2D_GHOST && lh_ < nzl + P2D_GHOST && \
+                        p_ <= k1 + 1;                                                   \
+      const char *hb_ = okh_ ? Cg + (p_ * P8 + (int64_t)yh_ * nx * 8)                   \
+                             : reinterpret_cast<const char *>(zbuf);                    \
+      if (lane < 16) glds4(hb_ + choff, cd_ + P2D_SR * P2D_CRB + 2 * w * 32);           \
+    }                                                                                   \
   } while (0)
   // DMA the J stored vectors of this wave's row of plane p into J-ring slot sl
   // (planes past the tile load the zero row)
@@ -308,12 +415,16 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   do {                                                                                  \
     const int p_ = (p);                                                                 \
     const int64_t po_ = p_ * P16;                                                       \
-    char *dst_ = smem + p2d_off_j(J) + (((sl) * J) * P2D_TR + w) * 1024;                \
+    char *dst_ = smem + p2d_off_j(J, A) + (((sl) * J) * P2D_TR + w) * 1024;             \
     _Pragma("unroll") for (int l_ = 0; l_ < J; ++l_) {                                  \
       const void *b_ = p_ < k1 ? (const void *)(sb[l_] + po_) : (const void *)zbuf;    \
       dma16(b_, xoff, dst_ + l_ * P2D_TR * 1024, 1);                                    \
     }                                                                                   \
   } while (0)
+  // A: c of ring slot sl, tile row tr, row index i (0..63: x0 + i; 64..67: the halo
+  // cells x0-2, x0-1, x0+64, x0+65)
+#define P2D_CV(sl, tr, i)                                                                \
+  Cr[(sl) * (P2D_CSB / 8) + ((i) < 64 ? (tr) * 64 + (i) : P2D_SR * 64 + (tr) * 4 + (i) - 64)]
   // L S_J at plane p, S tile row tr (yy = y0 - 2 + tr), x position xx with row
   // indices ci (centre), mi_ / pi_ (x - 1 / x + 1), from ring slots sm, sc, sp
   // (planes p-1, p, p+1)
@@ -331,7 +442,20 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
     const cplx zm_ = D2 ? cplx{0.0, 0.0} : Sm_[(ci)], zp_ = D2 ? cplx{0.0, 0.0} : Sp_[(ci)]; \
     const bool ok_ = xx_ >= 0 && xx_ < nx && kk_ >= 0 && kk_ < nz;                      \
     cplx v_;                                                                            \
-    if constexpr (PR) {                                                                 \
+    if constexpr (A) {                                                                  \
+      /* div(c grad) (laplacians.hpp:158-218): face weights (c_a + c_b)/2 where the  \
+         reference's flat-index neighbour exists, diagonal -sum of the weights */     \
+      const int jj_ = P2D_ROW(yy_);                                                     \
+      const double cc_ = P2D_CV(sc, tr_, ci);                                           \
+      const double wxm_ = p2d_face(xx_ > 0, cc_, P2D_CV(sc, tr_, mi_));                   \
+      const double wxp_ = p2d_face(xx_ + 1 < nx, cc_, P2D_CV(sc, tr_, pi_));              \
+      const double wym_ = p2d_face(kk_ > 0 || jj_ > 0, cc_, P2D_CV(sc, tr_ - 1, ci));     \
+      const double wyp_ = p2d_face(kk_ < nz - 1 || jj_ < ny - 1, cc_, P2D_CV(sc, tr_ + 1, ci)); \
+      const double wzm_ = p2d_face(kk_ > 0, cc_, P2D_CV(sm, tr_, ci));                    \
+      const double wzp_ = p2d_face(kk_ < nz - 1, cc_, P2D_CV(sp, tr_, ci));               \
+      v_ = s * ((((wzm_ * zm_ + wzp_ * zp_) + (wxm_ * xm_ + wxp_ * xp_)) + (wym_ * ym_ + wyp_ * yp_)) - \
+                (((wzm_ + wzp_) + (wxm_ + wxp_)) + (wym_ + wyp_)) * c_);                 \
+    } else if constexpr (PR) {                                                          \
       const int jj_ = P2D_ROW(yy_);                                                     \
       v_ = pr_lap(c_, xm_, xp_, (zm_ + zp_) + (ym_ + yp_), P2D_DIAGA(xx_, jj_, kk_),    \
                   P2D_DIAGB(xx_, jj_, kk_), s);                                         \
@@ -370,11 +494,16 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
   raw_barrier();
   cplx lq0, lq1, le1;  // L S_J of planes k-1 and k (own row), halo values of plane k
   P2D_LAP(lq0, k0 - 1, w + 2, 0, 1, 2, x, lane, mi, pi);
+  // A: c of the own cell at plane k-1 (its slot is reused before L^2 S_J of plane k needs it)
+  double cq0 = 0.0;
+  if constexpr (A && HZ) cq0 = P2D_CV(1, w + 2, lane);
   P2D_LROWS(k0, 1, 2, 3, 0, lq1, le1);
   raw_barrier();  // L ring slot 0 published; every wave is done with S slot 0 (plane k0-2)
 #pragma unroll
   for (int d = 0; d < DS; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
-  if constexpr (J > 0) {
+  if constexpr (LATE) {
+    P2D_ISSUE_J(k0, 0);
+  } else if constexpr (J > 0) {
 #pragma unroll
     for (int d = 0; d + 1 < NP; ++d) P2D_ISSUE_J(k0 + d, d);
   }
@@ -389,15 +518,15 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
     const int i = k - k0;
     // NLS_P2D_EARLY: issue first (the slots are free: S plane k-2 since the last
     // barrier, the wave's own J plane k-1 since its last step), then wait
-    if constexpr (p2d_early(J)) {
+    if constexpr (p2d_early(J, A)) {
       P2D_ISSUE_S(k + DS + 2, sis);
-      if constexpr (J > 0) P2D_ISSUE_J(k + NP - 1, jis);
+      if constexpr (J > 0 && !LATE) P2D_ISSUE_J(k + NP - 1, jis);
     }
-    wait_step<J, STW>(i);
+    wait_step<J, STW, A>(i);
     raw_barrier();
-    if constexpr (!p2d_early(J)) {
+    if constexpr (!p2d_early(J, A)) {
       P2D_ISSUE_S(k + DS + 2, sis);
-      if constexpr (J > 0) P2D_ISSUE_J(k + NP - 1, jis);
+      if constexpr (J > 0 && !LATE) P2D_ISSUE_J(k + NP - 1, jis);
     }
     const int s1 = sk + 1 == NSL ? 0 : sk + 1, s2 = s1 + 1 == NSL ? 0 : s1 + 1;
     // L S_J of plane k+1: own row (register) + halo values, shared rows into L slot lsl^1
@@ -406,9 +535,14 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
     // the J stored vectors of this cell and S_J itself
     cplx sv[J + 1];
     if constexpr (J > 0) {
-      const cplx *jv = reinterpret_cast<const cplx *>(smem + p2d_off_j(J) + ((jr * J) * P2D_TR + w) * 1024);
+      const cplx *jv = reinterpret_cast<const cplx *>(smem + p2d_off_j(J, A) + ((jr * J) * P2D_TR + w) * 1024);
 #pragma unroll
       for (int l = 0; l < J; ++l) sv[l] = jv[l * P2D_TR * 64 + lane];
+      if constexpr (LATE) {
+        // the rows are in registers: the slot takes plane k+1 (one step of look-ahead)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        P2D_ISSUE_J(k + 1, 0);
+      }
     }
     sv[J] = Sr[(sk * P2D_SR + w + 2) * RW + lane];
     const cplx l1 = lq1;
@@ -431,7 +565,21 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
       const cplx ym = Lr[(lsl * P2D_LR + w) * 64 + lane], yp = Lr[(lsl * P2D_LR + w + 2) * 64 + lane];
       const cplx zz = D2 ? cplx{0.0, 0.0} : lq0 + ln;
       cplx l2;
-      if constexpr (PR)
+      if constexpr (A) {
+        // the same operator at the same cell: c of the own row at planes k-1 (register),
+        // k (x, y neighbours from the ring) and k+1
+        const int gk = z0 + k;
+        const double cc = P2D_CV(sk, w + 2, lane);
+        const double wxm = p2d_face(x > 0, cc, P2D_CV(sk, w + 2, mi));
+        const double wxp = p2d_face(x + 1 < nx, cc, P2D_CV(sk, w + 2, pi));
+        const double wym = p2d_face(gk > 0 || y > 0, cc, P2D_CV(sk, w + 1, lane));
+        const double wyp = p2d_face(gk < nz - 1 || y < ny - 1, cc, P2D_CV(sk, w + 3, lane));
+        const double wzm = p2d_face(gk > 0, cc, cq0);
+        const double wzp = p2d_face(gk < nz - 1, cc, P2D_CV(s1, w + 2, lane));
+        l2 = s * ((((wzm * lq0 + wzp * ln) + (wxm * xm + wxp * xp)) + (wym * ym + wyp * yp)) -
+                  (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * l1);
+        cq0 = cc;
+      } else if constexpr (PR)
         l2 = pr_lap(l1, xm, xp, zz + (ym + yp), P2D_DIAGA(x, y, z0 + k), P2D_DIAGB(x, y, z0 + k), s);
       else
         l2 = P2D_DIAG(x, y, z0 + k) * l1 + s * ((zz + (xm + xp)) + (ym + yp));
@@ -483,6 +631,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J)) void k_p2d(cplx *__restrict__
 #undef P2D_ISSUE_S
 #undef P2D_ISSUE_J
 #undef P2D_LAP
+#undef P2D_CV
 #undef P2D_LROWS
   wait_vm<0>();  // the look-ahead DMAs land before the LDS is reused
   raw_barrier();

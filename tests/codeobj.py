@@ -112,11 +112,11 @@ def main_loop(ins: list[tuple[int, str, str]], fname: str) -> list[tuple[int, st
     return [i for i in ins if lo <= i[0] <= hi]
 
 
-_P2D = re.compile(r"k_p2dILi(\d+)ELb([01])ELb([01])ELb([01])E")
+_P2D = re.compile(r"k_p2dILi(\d+)ELb([01])ELb([01])ELb([01])ELb([01])E")
 
 
 def p2d_params(name: str):
-    """(J, HZ, D2, PR) of a mangled k_p2d<J, HZ, D2, PR> symbol, else None."""
+    """(J, HZ, D2, PR, A) of a mangled k_p2d<J, HZ, D2, PR, A> symbol, else None."""
     m = _P2D.search(name)
     return tuple(int(g) for g in m.groups()) if m else None
 
@@ -129,16 +129,17 @@ def vmem_counts(ins) -> dict[str, int]:
     return c
 
 
-def p2d_loop_loads(J: int) -> dict[str, int]:
+def p2d_loop_loads(J: int, A: int = 0) -> dict[str, int]:
     """VMEM loads of one march step as the source issues them: 2 S rows (1 KiB each
-    + a 4-byte halo piece on 16 lanes) and the J J-ring rows."""
-    return {"global_load_lds_dwordx4": 2 + J, "global_load_lds_dword": 2}
+    + a 4-byte halo piece on 16 lanes), with A the two c rows (one 16-B DMA + one
+    4-byte halo piece), and the J J-ring rows."""
+    return {"global_load_lds_dwordx4": 2 + J + (1 if A else 0), "global_load_lds_dword": 2 + (1 if A else 0)}
 
 
 class P2dSchedule:
     """Python restatement of nls_pass2d.hpp's ring/wait constexprs (p2d_occ, p2d_ds,
-    p2d_np, p2d_after, p2d_i0), with the tuning macros' defaults read from the
-    header itself so that the two cannot drift apart."""
+    p2d_early, p2d_np, p2d_after's issue replay, p2d_i0), with the tuning macros'
+    defaults read from the header itself so that the two cannot drift apart."""
 
     def __init__(self, header: str):
         src = open(header).read()
@@ -148,53 +149,93 @@ class P2dSchedule:
 
         def const(name):
             return int(eval(re.search(rf"constexpr int {name} = ([^;]+);", src).group(1),
-                            {"P2D_TR": self.TR, "__builtins__": {}}))
+                            {"P2D_TR": self.TR, "P2D_SR": 8, "P2D_CRB": 512, "__builtins__": {}}))
         self.OCC0, self.OCC2 = define("NLS_P2D_OCC0"), define("NLS_P2D_OCC2_MAXJ")
+        self.OCC2A, self.EARLYA, self.DS1A = define("NLS_P2A_OCC2_MAXJ"), define("NLS_P2A_EARLY"), define("NLS_P2A_DS1")
         self.DS2, self.DS3 = define("NLS_P2D_DS2_MAXJ"), define("NLS_P2D_DS3_MAXJ")
         self.EARLY, self.NPMAX = define("NLS_P2D_EARLY"), define("NLS_P2D_NP_MAX")
         self.SR, self.SRB, self.LR = const("P2D_SR"), const("P2D_SRB"), const("P2D_LR")
+        self.CSB = const("P2D_CSB")
         self.LDS = 160 * 1024
 
     TR = 4
 
-    def occ(self, J):
+    def occ(self, J, A=0):
+        if A:
+            return 2 if J <= self.OCC2A else 1
         return self.OCC0 if J == 0 else (2 if J <= self.OCC2 else 1)
 
-    def ds(self, J):
-        o = self.occ(J)
+    def ds(self, J, A=0):
+        o = self.occ(J, A)
+        if A:
+            return (2 if J == 0 else 1) if o == 2 else (3 if J <= self.DS3 else (1 if J >= 22 else self.DS1A))
         if o >= 3:
             return 1
         if o == 2:
             return 3 if J == 0 else (2 if J <= self.DS2 else 1)
         return 6 if J == 0 else (3 if J <= self.DS3 else (1 if (J <= 12 or not self.EARLY) else 0))
 
-    def early(self, J):
-        return bool(self.EARLY) and self.occ(J) == 1
+    def early(self, J, A=0):
+        if A:
+            return bool(self.EARLYA) and self.occ(J, A) == 1 and J < 22
+        return bool(self.EARLY) and self.occ(J, A) == 1
 
-    def np(self, J):
+    def np(self, J, A=0):
         if J == 0:
             return 0
-        nsl = self.ds(J) + 3 + (1 if self.early(J) else 0)
-        off_j = nsl * self.SR * self.SRB + 2 * self.LR * 1024
-        avail = self.LDS // self.occ(J) - off_j - 2 * (J + 1) * 16
+        nsl = self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
+        off_j = nsl * self.SR * self.SRB + (nsl * self.CSB if A else 0) + 2 * self.LR * 1024
+        avail = self.LDS // self.occ(J, A) - off_j - 2 * (J + 1) * 16
         return min(avail // (self.TR * 1024 * J), self.NPMAX)
 
-    def after(self, J, stw, i):
-        DS, NP, G = self.ds(J), self.np(J), 4 + J + stw
-        own = 4 + J if self.early(J) else 0
-        if i >= DS:
-            nS = J if DS == 0 else J + stw + (DS - 1) * G + own
-        else:
-            nS = 4 * (DS - 1 - i) + (NP - 1 if NP > 0 else 0) * J + i * G + own
-        if J == 0:
-            return nS
-        nJ = stw + (NP - 2) * G + own if i >= NP - 1 else (NP - 2 - i) * J + i * G + own
-        return min(nJ, nS)
+    def late(self, J, A=0):
+        return J > 0 and self.np(J, A) == 1
 
-    def waits(self, J, stw):
-        """The vmcnt values wait_step<J, STW> can emit (steps 0 .. p2d_i0)."""
-        i0 = self.ds(J) if J == 0 else max(self.np(J) - 1, self.ds(J))
-        return sorted({min(63, max(0, self.after(J, stw, i))) for i in range(i0 + 1)})
+    def after(self, J, stw, i, A=0):
+        DS, NP, NSD = self.ds(J, A), self.np(J, A), 6 if A else 4
+        early, late = self.early(J, A), self.late(J, A)
+        n = lastS = lastJ = 0
+        for d in range(DS):
+            n += NSD
+            if d == i:
+                lastS = n
+        if J > 0:
+            for d in range(1 if late else NP - 1):
+                n += J
+                if d == i:
+                    lastJ = n
+        s = 0
+        while True:
+            if early:
+                n += NSD
+                if s + DS == i:
+                    lastS = n
+                if J > 0 and not late:
+                    n += J
+                    if s + NP - 1 == i:
+                        lastJ = n
+            if s == i:
+                break
+            if not early:
+                n += NSD
+                if s + DS == i:
+                    lastS = n
+                if J > 0 and not late:
+                    n += J
+                    if s + NP - 1 == i:
+                        lastJ = n
+            if late:
+                n += J
+                if s + 1 == i:
+                    lastJ = n
+            n += stw
+            s += 1
+        return min(n - lastS, n - lastJ if J > 0 else 1 << 20)
+
+    def waits(self, J, stw, A=0):
+        """The vmcnt values wait_step<J, STW, A> can emit (steps 0 .. p2d_i0)."""
+        i0 = self.ds(J, A) + self.np(J, A) + 1
+        return sorted({min(63, max(0, self.after(J, stw, i, A))) for i in range(i0 + 1)})
 
 
 def check_p2d(funcs, meta, sched: P2dSchedule):
@@ -210,7 +251,7 @@ def check_p2d(funcs, meta, sched: P2dSchedule):
         prm = p2d_params(name)
         if prm is None or name.endswith(".kd"):
             continue
-        J, hz, d2, pr = prm
+        J, hz, d2, pr, A = prm
         probs = []
         allv = vmem_counts(ins)
         bad = {k: v for k, v in allv.items() if k.startswith(("scratch_", "buffer_", "flat_"))}
@@ -225,15 +266,15 @@ def check_p2d(funcs, meta, sched: P2dSchedule):
         got = vmem_counts(loop)
         stw = 1 + hz
         loads = {k: v for k, v in got.items() if k != "global_store_dwordx4"}
-        if loads != p2d_loop_loads(J):
-            probs.append(f"march loop loads {loads} != the source's {p2d_loop_loads(J)}")
+        if loads != p2d_loop_loads(J, A):
+            probs.append(f"march loop loads {loads} != the source's {p2d_loop_loads(J, A)}")
         if got.get("global_store_dwordx4", 0) not in (stw, 2 * stw):
             probs.append(f"march loop stores {got.get('global_store_dwordx4', 0)} (STW = {stw})")
         waits = sorted({int(re.search(r"vmcnt\((\d+)\)", o).group(1)) for _a, mn, o in loop
                         if mn == "s_waitcnt" and "vmcnt" in o})
-        if waits != sched.waits(J, stw):
-            probs.append(f"march loop vmcnt waits {waits} != p2d_after {sched.waits(J, stw)}")
-        rec = {"J": J, "HZ": hz, "D2": d2, "PR": pr, "vgpr": md.get("vgpr_count"), "agpr": md.get("agpr_count"),
+        if waits != sched.waits(J, stw, A):
+            probs.append(f"march loop vmcnt waits {waits} != p2d_after {sched.waits(J, stw, A)}")
+        rec = {"J": J, "HZ": hz, "D2": d2, "PR": pr, "A": A, "vgpr": md.get("vgpr_count"), "agpr": md.get("agpr_count"),
                "sgpr": md.get("sgpr_count"), "sgpr_spill": md.get("sgpr_spill_count"),
                "vgpr_spill": md.get("vgpr_spill_count"), "lds": md.get("group_segment_fixed_size"),
                "private": md.get("private_segment_fixed_size"), "loop_vmem": got, "loop_vmcnt_waits": waits,

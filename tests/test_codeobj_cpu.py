@@ -1,6 +1,6 @@
 """CPU: the hand-counted vmcnt schedule of k_p2d holds in the compiled gfx950 code
 object (tests/codeobj.py; nls_pass2d.hpp:30-38, p2d_after / wait_step).  For every
-k_p2d<J, HZ, D2, PR> instantiation: no scratch / buffer / flat access, no private
+k_p2d<J, HZ, D2, PR, A> instantiation: no scratch / buffer / flat access, no private
 segment, no VGPR spill; the march loop issues exactly the source's DMA loads and
 stores; and its s_waitcnt vmcnt values are exactly the source's p2d_after values."""
 import os
@@ -29,20 +29,21 @@ def p2d_results(tmp_path_factory):
 
 
 def test_every_p2d_instantiation_found(p2d_results):
-    got = {(r["J"], r["HZ"], r["D2"], r["PR"]) for _n, _p, r in p2d_results}
-    want = {(J, hz, d2, pr) for J in range(0, 16, 2) for hz in (0, 1) for d2, pr in ((0, 0), (1, 0), (1, 1))}
+    got = {(r["J"], r["HZ"], r["D2"], r["PR"], r["A"]) for _n, _p, r in p2d_results}
+    want = {(J, hz, d2, pr, 0) for J in range(0, 16, 2) for hz in (0, 1) for d2, pr in ((0, 0), (1, 0), (1, 1))}
+    want |= {(J, hz, 0, 0, 1) for J in range(0, 24, 2) for hz in (0, 1)}  # the G2 operator (nls_pass2a.hip)
     assert got == want
 
 
 def test_p2d_vmcnt_contract_holds(p2d_results):
-    bad = [(r["J"], r["HZ"], r["D2"], r["PR"], p) for _n, p, r in p2d_results if p]
+    bad = [(r["J"], r["HZ"], r["D2"], r["PR"], r["A"], p) for _n, p, r in p2d_results if p]
     assert not bad, bad
 
 
 def test_checker_flags_an_extra_vmem_op():
     """The loop check is not vacuous: one more load in a synthetic loop body fails it."""
     sched = C.P2dSchedule(HDR)
-    name = "_ZN3nls5k_p2dILi2ELb1ELb0ELb0EEEv"
+    name = "_ZN3nls5k_p2dILi2ELb1ELb0ELb0ELb0EEEv"
     body = [(0x100, "s_waitcnt", "vmcnt(4)")] + \
         [(0x104 + 4 * i, "global_load_lds_dwordx4", "v[2:3], off") for i in range(4)] + \
         [(0x120, "global_load_lds_dword", ""), (0x124, "global_load_lds_dword", ""),

@@ -56,6 +56,29 @@ def solver(dim, nx, ny, nz, dx, m, **kw):
     return nls_amd.Solver(dim, nx, ny, nz, dx, dx, equation=nls_amd.NLSE_G2, m=m, **kw)
 
 
+def set_form(monkeypatch, form):
+    """Two-vector pass form of the G2 operator: "dma" (k_p2d with the c field staged
+    beside S_J, nls_pass2a.hip; where the grid allows it), "reg" (the register form
+    k_p2g_lap + k_p2g, nls_pass2g.hpp) or "one" (one-vector passes)."""
+    monkeypatch.setenv("NLS_PASS2", "0" if form == "one" else "1")
+    monkeypatch.setenv("NLS_P2_REG", "1" if form == "reg" else "0")
+
+
+def dma_form(form, dim, nx, ny, m):
+    """Whether the LDS-DMA pass runs (nls_api.cpp alloc_all: 3D, ny % 4 == 0, nx even, m <= 26)."""
+    return form == "dma" and dim == 3 and ny % 4 == 0 and nx % 2 == 0 and nx >= 4 and m <= 26
+
+
+def check_form(cnt, form, dim, nx, ny, m, runs):
+    """update_count[0] = J = 0 passes: one launch each in the DMA form, two (y = L S_0,
+    then the pass) in the register form; the two-vector passes start at even J only."""
+    if form == "one":
+        assert cnt[1] > 0
+        return
+    assert cnt[1] == 0
+    assert cnt[0] == (runs if dma_form(form, dim, nx, ny, m) else 2 * runs), cnt[:4]
+
+
 @pytest.mark.parametrize("dim,nx,ny,nz", GRIDS)
 def test_aniso_laplacian_matches_oracle(dim, nx, ny, nz):
     dx = 0.37
@@ -94,14 +117,17 @@ def test_neumann_bc_bit_exact(dim, nx, ny, nz):
         assert np.array_equal(s.get_field(), O.neumann_bc(g, u))
 
 
-@pytest.mark.parametrize("pass2", ["1", "0"], ids=["two_vector", "one_vector"])
+@pytest.mark.parametrize("form", ["dma", "reg", "one"])
 @pytest.mark.parametrize("dim,nx,ny,nz,m", [(2, 32, 32, 1, 20), (2, 300, 20, 1, 20), (3, 12, 12, 12, 25),
-                                            (3, 70, 9, 11, 25), (3, 16, 16, 16, 10), (2, 7, 5, 1, 20)])
-def test_g2_trajectory_with_bc_matches_oracle(monkeypatch, pass2, dim, nx, ny, nz, m):
+                                            (3, 70, 9, 11, 25), (3, 16, 16, 16, 10), (2, 7, 5, 1, 20),
+                                            (3, 130, 8, 20, 25), (3, 66, 12, 9, 16)])
+def test_g2_trajectory_with_bc_matches_oracle(monkeypatch, form, dim, nx, ny, nz, m):
     """The driver loop (nlse_cubic_driver_3d.cpp:116-119): step, then apply_bc.  With
-    the two-vector passes (the default: the register form k_p2g_lap + k_p2g for div(c
-    grad), nls_pass2g.hpp) and with the one-vector passes (NLS_PASS2=0)."""
-    monkeypatch.setenv("NLS_PASS2", pass2)
+    the two-vector passes in both forms (set_form: the LDS-DMA pass with c staged
+    beside S_J, the default where the grid allows it, and the register form) and with
+    the one-vector passes.  130 x 8 x 20: a ragged third x tile, two y tiles, the
+    y-wrap across tile and plane edges."""
+    set_form(monkeypatch, form)
     L, dt, steps = 4.0, 1e-3, 12
     dx = 2 * L / (nx - 1)
     u, mf, c = fields(dim, nx, ny, nz, seed=4)
@@ -117,8 +143,7 @@ def test_g2_trajectory_with_bc_matches_oracle(monkeypatch, pass2, dim, nx, ny, n
             s.step(dt, 1)
             s.apply_bc()
         out = s.get_field()
-        cnt = s.timing()["update_count"]
-        assert (cnt[0] > 0 and cnt[1] == 0) == (pass2 == "1")  # s-step passes start at even J only
+        check_form(s.timing()["update_count"], form, dim, nx, ny, m, steps)
         s.set_timing(False)
         s.set_field(u)
         s.step(dt, steps)
@@ -127,11 +152,12 @@ def test_g2_trajectory_with_bc_matches_oracle(monkeypatch, pass2, dim, nx, ny, n
     assert rel_l2(out_nobc, ref_nobc) <= TOL_TRAJ
 
 
-@pytest.mark.parametrize("eq", ["g2", "g2_2d"])
-def test_g2_stiff_two_vector_matches_oracle(eq):
+@pytest.mark.parametrize("eq,form", [("g2", "dma"), ("g2", "reg"), ("g2_2d", "reg")])
+def test_g2_stiff_two_vector_matches_oracle(monkeypatch, eq, form):
     """The G2 production workload's spacing (bench g2_3d_256: L = 10, dx = 20/255, m = 25;
     nlse_cubic_driver_3d.cpp:112-114) on a 48^3 sub-grid, 2D at m = 20 on 256^2 with the
-    2D driver's spacing; two-vector passes (k_p2g), BC after every step, 10 steps."""
+    2D driver's spacing; two-vector passes in both forms (3D), BC after every step, 10 steps."""
+    set_form(monkeypatch, form)
     dim = 3 if eq == "g2" else 2
     n, m = (48, 25) if dim == 3 else (256, 20)
     dx, dt, steps = 20.0 / 255, 1e-3, 10
@@ -148,7 +174,8 @@ def test_g2_stiff_two_vector_matches_oracle(eq):
         out = s.get_field()
         cnt = s.timing()["update_count"]
         # two-vector passes at even J only, the last at J = m - 4 or m - 3
-        assert cnt[0] > 0 and cnt[1] == 0 and max(j for j in range(32) if cnt[j]) >= m - 4
+        check_form(cnt, form, dim, n, n, m, steps)
+        assert max(j for j in range(32) if cnt[j]) >= m - 4
     assert rel_l2(out, ref) <= TOL_TRAJ
 
 
@@ -286,14 +313,14 @@ def test_sinc_action_matches_oracle(dim, nx, ny, nz):
             assert rel_l2(s.krylov_apply(u, t, nls_amd.F_SINC), ref) <= TOL_KRYLOV
 
 
-@pytest.mark.parametrize("pass2", ["1", "0"], ids=["two_vector", "one_vector"])
+@pytest.mark.parametrize("form", ["dma", "reg", "one"])
 @pytest.mark.parametrize("dim,nx,ny,nz,m", [(3, 12, 12, 12, 15), (3, 70, 9, 11, 15), (2, 32, 32, 1, 25),
-                                            (2, 300, 20, 1, 25)])
-def test_sewi_trajectory_matches_oracle(monkeypatch, pass2, dim, nx, ny, nz, m):
+                                            (2, 300, 20, 1, 25), (3, 130, 8, 20, 15)])
+def test_sewi_trajectory_matches_oracle(monkeypatch, form, dim, nx, ny, nz, m):
     """The sEWI driver loop (nlse_cubic_sewi_driver_3d.cpp:116-119): step_sewi(i), apply_bc;
-    its three Krylov actions per step by the two-vector passes (default) or the
-    one-vector passes (NLS_PASS2=0)."""
-    monkeypatch.setenv("NLS_PASS2", pass2)
+    its three Krylov actions per step by the two-vector passes (both forms) or the
+    one-vector passes."""
+    set_form(monkeypatch, form)
     L, dt, steps = 4.0, 1e-3, 8
     dx = 2 * L / (nx - 1)
     u, mf, c = fields(dim, nx, ny, nz, seed=9)
