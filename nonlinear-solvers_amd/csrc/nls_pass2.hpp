@@ -52,30 +52,38 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
   __shared__ cplx bb[2][4];
   __shared__ double nu[3];
   __shared__ double s_prev, s_beta;
+  // C, D, H staged in LDS for the kernel's lifetime (its loops are chains of dependent
+  // reads), written back at the end
+  __shared__ cplx sC[P2M][P2M], sD[P2M][P2M], sH[P2M][P2M];
   const int t = threadIdx.x;
   int Jn;  // J of the next pass
+  for (int e = t; e < P2M * P2M; e += NTHREADS) {
+    (&sC[0][0])[e] = (&ps->C[0][0])[e];
+    (&sD[0][0])[e] = (&ps->D[0][0])[e];
+    (&sH[0][0])[e] = (&ps->H[0][0])[e];
+  }
   if (t == 0) s_prev = ps->H[0][0].re;  // mode 2's shift: the previous step's alpha_0
   __syncthreads();
   if (mode == 0 || mode == 2) {
     for (int e = t; e < P2M * P2M; e += NTHREADS) {
       const int i = e / P2M, k = e % P2M;
-      ps->C[i][k] = {0.0, 0.0};
-      ps->D[i][k] = {0.0, 0.0};
-      ps->H[i][k] = {0.0, 0.0};
+      sC[i][k] = {0.0, 0.0};
+      sD[i][k] = {0.0, 0.0};
+      sH[i][k] = {0.0, 0.0};
     }
     __syncthreads();
     if (t == 0) {
       if (mode == 0) {
         const double b = st->s[0];
         ps->beta = b;
-        ps->C[0][0] = {b > 0.0 ? 1.0 / b : 0.0, 0.0};
-        ps->D[0][0] = {b, 0.0};
+        sC[0][0] = {b > 0.0 ? 1.0 / b : 0.0, 0.0};
+        sD[0][0] = {b, 0.0};
         ps->sigma = st->H[0][0].re;
         ps->blind = 0;
       } else {
         ps->beta = 1.0;
-        ps->C[0][0] = {1.0, 0.0};
-        ps->D[0][0] = {1.0, 0.0};
+        sC[0][0] = {1.0, 0.0};
+        sD[0][0] = {1.0, 0.0};
         ps->sigma = s_prev;
         ps->blind = 1;
       }
@@ -102,8 +110,8 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
         for (int e = 0; e < og; ++e) sw[e] = ib * sw[e];
         for (int e = og; e < og + ng; ++e) sw[e] = (ib * ib) * sw[e];
         ps->beta = b;
-        ps->C[0][0] = {ib, 0.0};
-        ps->D[0][0] = {b, 0.0};
+        sC[0][0] = {ib, 0.0};
+        sD[0][0] = {b, 0.0};
       }
       __syncthreads();
     }
@@ -116,7 +124,7 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       // q_k = W_k^H V_i = sum_{l <= k} conj(C[l][k]) S_l^H V_i
       for (int k = t; k < n; k += NTHREADS) {
         cplx v = {0.0, 0.0};
-        for (int l = 0; l <= k; ++l) v += cj_mul(ps->C[l][k], sv[l]);
+        for (int l = 0; l <= k; ++l) v += cj_mul(sC[l][k], sv[l]);
         q[i][k] = v;
       }
       __syncthreads();
@@ -130,9 +138,9 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       // C[:, n] = (e_n - C q) / nu ; D[:, n] = (q, nu)
       for (int r = t; r <= n; r += NTHREADS) {
         cplx v = {r == n ? 1.0 : 0.0, 0.0};
-        for (int k = r; k < n; ++k) v = v - cmul(ps->C[r][k], q[i][k]);
-        ps->C[r][n] = inu * v;
-        ps->D[r][n] = r < n ? q[i][r] : cplx{nui, 0.0};
+        for (int k = r; k < n; ++k) v = v - cmul(sC[r][k], q[i][k]);
+        sC[r][n] = inu * v;
+        sD[r][n] = r < n ? q[i][r] : cplx{nui, 0.0};
       }
       __syncthreads();
     }
@@ -140,8 +148,8 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
     for (int r = t; r <= J + 1; r += NTHREADS) {
       cplx h = r <= J ? q[0][r] : cplx{nu[0], 0.0};
       if (r == J) h.re += sig;
-      if (r < J) h += cconj(ps->H[J][r]);
-      ps->H[r][J] = h;
+      if (r < J) h += cconj(sH[J][r]);
+      sH[r][J] = h;
     }
     __syncthreads();
     // H column c = J + i (i >= 1), L W_c = (V_{i+1} + sigma V_i - sum_{k<c} q^(i-1)_k L W_k) / nu_{i-1}:
@@ -153,12 +161,12 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
         cplx v = r <= c ? q[i][r] : cplx{nu[i], 0.0};
         const cplx wp = r < c ? q[i - 1][r] : (r == c ? cplx{nu[i - 1], 0.0} : cplx{0.0, 0.0});
         v += sig * wp;
-        for (int k = (r > 0 ? r - 1 : 0); k < c; ++k) v = v - cmul(q[i - 1][k], ps->H[r][k]);
-        ps->H[r][c] = inp * v;
+        for (int k = (r > 0 ? r - 1 : 0); k < c; ++k) v = v - cmul(q[i - 1][k], sH[r][k]);
+        sH[r][c] = inp * v;
       }
       __syncthreads();
     }
-    if (t == 0 && ns > 1) ps->sigma = ps->H[J + ns - 1][J + ns - 1].re;
+    if (t == 0 && ns > 1) ps->sigma = sH[J + ns - 1][J + ns - 1].re;
     Jn = J + ns;
     __syncthreads();
     if (J == 0 && ps->blind) {
@@ -167,8 +175,8 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       const double b = s_beta, ib = b > 0.0 ? 1.0 / b : 0.0;
       for (int e = t; e < ns * P2M; e += NTHREADS) {
         const int l = 1 + e / P2M, k = e % P2M;
-        ps->C[l][k] = ib * ps->C[l][k];
-        ps->D[k][l] = b * ps->D[k][l];
+        sC[l][k] = ib * sC[l][k];
+        sD[k][l] = b * sD[k][l];
       }
       __syncthreads();
       if (t == 0) ps->blind = 0;
@@ -183,15 +191,15 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
     //   b_{i+1}[1] = w_i[j] C_jj - sigma b_i[1],  b_{i+1}[p+1] = b_i[p] - sigma b_i[p+1]
     const int j = Jn;
     const double sig = ps->sigma;
-    const cplx cjj = ps->C[j][j];
+    const cplx cjj = sC[j][j];
     for (int k = t; k <= j; k += NTHREADS) {
       cplx v = {0.0, 0.0};
-      for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) v += cmul(ps->H[k][i], ps->D[i][j]);
+      for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) v += cmul(sH[k][i], sD[i][j]);
       v = cmul(cjj, v);
       lw[k] = {-v.re, -v.im};
       cplx x = lw[k];
       if (k == j) x.re -= sig;
-      if (k < j) x = x - cconj(ps->H[j][k]);
+      if (k < j) x = x - cconj(sH[j][k]);
       w[0][k] = x;
     }
     if (t == 0) bb[0][0] = bb[0][1] = bb[0][2] = bb[0][3] = {0.0, 0.0};
@@ -204,7 +212,7 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       // S-basis coefficients a_i = C w_i
       for (int l = t; l <= j; l += NTHREADS) {
         cplx a = {0.0, 0.0};
-        for (int k = l; k <= j; ++k) a += cmul(ps->C[l][k], w[cu][k]);
+        for (int k = l; k <= j; ++k) a += cmul(sC[l][k], w[cu][k]);
         adst[i][l] = a;
       }
       if (t == 0)
@@ -212,7 +220,7 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       if (i + 1 < nsn) {
         for (int k = t; k <= j; k += NTHREADS) {
           cplx v = {0.0, 0.0};
-          for (int i2 = (k > 0 ? k - 1 : 0); i2 < j; ++i2) v += cmul(ps->H[k][i2], w[cu][i2]);
+          for (int i2 = (k > 0 ? k - 1 : 0); i2 < j; ++i2) v += cmul(sH[k][i2], w[cu][i2]);
           v += cmul(w[cu][j], lw[k]);
           w[nx][k] = v - sig * w[cu][k];
         }
@@ -228,10 +236,16 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
     // T as the reference builds it (alpha_j, j < Jn; norms; T[Jn][Jn] = 0 set by
     // k_reduce_final), s[] = 1 so that k_reduce_final's fin is c = Q f(Lambda) Q^T e_1
     if (t < Jn) {
-      st->Td[t] = ps->H[t][t].re;
-      st->To[t] = ps->H[t + 1][t].re;
+      st->Td[t] = sH[t][t].re;
+      st->To[t] = sH[t + 1][t].re;
     }
     st->s[t] = 1.0;
+  }
+  __syncthreads();
+  for (int e = t; e < P2M * P2M; e += NTHREADS) {
+    (&ps->C[0][0])[e] = (&sC[0][0])[e];
+    (&ps->D[0][0])[e] = (&sD[0][0])[e];
+    (&ps->H[0][0])[e] = (&sH[0][0])[e];
   }
 }
 

@@ -56,7 +56,7 @@ constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
 constexpr int P2D_CRB = 512;
 constexpr int P2D_CSB = P2D_SR * P2D_CRB + P2D_SR * 32;
 #ifndef NLS_P2D_OCC2_MAXJ
-#define NLS_P2D_OCC2_MAXJ 4   // two workgroups per CU up to this J
+#define NLS_P2D_OCC2_MAXJ 6   // two workgroups per CU up to this J (J = 6: late J ring, 512^3 4.08 -> 3.64 ms; J = 8 no gain)
 #endif
 #ifndef NLS_P2A_OCC2_MAXJ
 #define NLS_P2A_OCC2_MAXJ 4   // anisotropic passes: two workgroups per CU up to this J (J = 4: late J ring, 0.655 -> 0.416 ms at G2 256^3)
@@ -128,7 +128,7 @@ __host__ __device__ constexpr int p2d_off_c(int J, bool A = false) {
 __host__ __device__ constexpr int p2d_lds_bytes(int J, bool A = false) { return p2d_off_c(J, A) + 2 * (J + 1) * 16; }
 __host__ __device__ constexpr bool p2d_rings_ok(int J, bool A = false) {
   return J == 0 ? p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS
-                : (J <= (A ? P2D_JMAX_A : P2D_JMAX) && p2d_np(J, A) >= (A ? 1 : 2) &&
+                : (J <= (A ? P2D_JMAX_A : P2D_JMAX) && p2d_np(J, A) >= 1 &&
                    p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS);
 }
 static_assert(p2d_rings_ok(2) && p2d_rings_ok(4) && p2d_rings_ok(6) && p2d_rings_ok(8) && p2d_rings_ok(10) &&
@@ -406,19 +406,21 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
       if (lane < 16) glds4(hb_ + choff, cd_ + P2D_SR * P2D_CRB + 2 * w * 32);           \
     }                                                                                   \
   } while (0)
-  // DMA the J stored vectors of this wave's row of plane p into J-ring slot sl
-  // (planes past the tile load the zero row)
-  const char *sb[J > 0 ? J : 1];
-#pragma unroll
-  for (int l = 0; l < J; ++l) sb[l] = reinterpret_cast<const char *>(W + l * vs) + (int64_t)y * nx * 16;
+  // DMA the J stored vectors of this wave's row of plane p into J-ring slot sl.  One
+  // scalar pointer walks the vectors (vector stride vsb): J per-vector pointers were
+  // 2J SGPRs (spilled to VGPR lanes from J ~ 10) and 3J SALU per step.  A plane past
+  // the tile re-reads the tile's last plane: those rows are never used, the DMA only
+  // keeps every step's issue count the same.
+  const char *const jb0 = reinterpret_cast<const char *>(W) + (int64_t)y * nx * 16;
+  const int64_t vsb = vs * 16;
 #define P2D_ISSUE_J(p, sl)                                                              \
   do {                                                                                  \
-    const int p_ = (p);                                                                 \
-    const int64_t po_ = p_ * P16;                                                       \
+    const char *b_ = jb0 + (int64_t)min((p), k1 - 1) * P16;                             \
     char *dst_ = smem + p2d_off_j(J, A) + (((sl) * J) * P2D_TR + w) * 1024;             \
     _Pragma("unroll") for (int l_ = 0; l_ < J; ++l_) {                                  \
-      const void *b_ = p_ < k1 ? (const void *)(sb[l_] + po_) : (const void *)zbuf;    \
+      asm volatile("" : "+s"(b_));  /* keep the walk: no J loop-invariant pointers */   \
       dma16(b_, xoff, dst_ + l_ * P2D_TR * 1024, 1);                                    \
+      b_ += vsb;                                                                        \
     }                                                                                   \
   } while (0)
   // A: c of ring slot sl, tile row tr, row index i (0..63: x0 + i; 64..67: the halo
