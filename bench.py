@@ -93,9 +93,11 @@ def moved_bytes_per_cell_step(w, m, sched, pass2, u_frac, tm, steps):
       two-vector Gautschi (SG, two bases of f64, cell pairs): per basis the passes +
         alpha + tail; the mid tail reads S_0..S_{m-2}, m(x), u_past and writes u_past,
         g_0 (m+3), the end tail reads S_0..S_{m-2}, u_past, u and writes u, u_past (m+3);
-      two-vector G2 NLSE (register form, nls_pass2g.hpp): per pass the y = L S_J
-        launch (S_J + c in, y out) and the pass (y + c + S_0..S_J in, ns out), the
-        tail's alpha (+ c), the tail (m-1 reads + c + m(x), u and W_0 written);
+      two-vector G2 NLSE: LDS-DMA form (k_p2d with c staged beside S_J): per pass
+        S_0..S_J + c in, ns out; register form (nls_pass2g.hpp, two launches per
+        pass -- told apart by the J = 0 launch count): the y = L S_J launch (S_J + c
+        in, y out) and the pass (y + c + S_0..S_J in, ns out); then the tail's alpha
+        (+ c), the tail (m-1 reads + c + m(x), u and W_0 written);
       one-vector G2 NLSE (div(c grad), m(x)): alpha passes j = 0..m-3 (W_j + c), the
         tail's alpha (W_{m-2} + c), updates J = 0..m-3 ((J+2) vectors + c), tail (m-1
         reads + c + m(x), u and W_0 written)."""
@@ -110,9 +112,13 @@ def moved_bytes_per_cell_step(w, m, sched, pass2, u_frac, tm, steps):
         per_basis = sum(j + 1 + ns for j, ns in sched) + 1
         return 8 * (2 * per_basis + 2 * (m + 3))
     if pass2 and eq == 3:
-        # register two-vector passes (k_p2g_lap + k_p2g): per pass S_J + c read and y =
-        # L S_J written, then y (stencil) + c + S_0..S_J read and ns vectors written
-        passes = sum((j + 1 + ns) * 16 + (16 + 8 + 16) + (16 + 8) for j, ns in sched)
+        reg = tm["update_count"][0] > 1.5 * max(1, tm["steps"])  # two J = 0 launches per run
+        if reg:
+            # register two-vector passes (k_p2g_lap + k_p2g): per pass S_J + c read and y =
+            # L S_J written, then y (stencil) + c + S_0..S_J read and ns vectors written
+            passes = sum((j + 1 + ns) * 16 + (16 + 8 + 16) + (16 + 8) for j, ns in sched)
+        else:
+            passes = sum((j + 1 + ns) * 16 + 8 for j, ns in sched)
         return passes + (16 + 8) + ((m - 1) * 16 + 8 + 8 + 16 + 16)
     if not pass2 and eq == 3:
         alpha = (m - 1) * (16 + 8)

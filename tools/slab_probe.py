@@ -47,6 +47,12 @@ VARIANTS = [
     (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "60", "NLS_P2_BND": "dma"}),
     (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "64", "NLS_P2_SPLIT": "0"}),
     (128, {}), (128, {"NLS_FORCE_RCCL": "1"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_GRID": "256", "NLS_P2B_LGRID": "512"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_GRID": "128", "NLS_P2B_LGRID": "256"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_GRID": "512", "NLS_P2B_LGRID": "1024"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_LATE": "1"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_LATE": "1", "NLS_P2B_GRID": "256", "NLS_P2B_LGRID": "256"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_INLINE": "1"}),
 ]
 if len(sys.argv) > 1:  # a subset: python tools/slab_probe.py 0 2 3
     VARIANTS = [VARIANTS[int(i)] for i in sys.argv[1:]]
