@@ -130,6 +130,7 @@ struct nls_handle {
   int p2lapgrid = 0;           // k_lap grid over planes [-1, nzl]
   int p2mkz = 16;              // tile depth of k_lap / k_p2m (G2 256^3 m=25: 13.36 ms/step vs 13.76 at 32)
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
+  int p2order = 0;             // k_p2d tile order (Geo::remap bits: 2 x-fastest, 4 no XCD bands; NLS_P2_ORDER)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
   // a new state was set (nls_set_*): the next step starts its bases cold, so it is
   // issued eagerly, never replayed from a graph captured warm (run-to-run bitwise
@@ -791,6 +792,7 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
   int64_t vs = h->p2_pr ? h->vs / 2 : h->vs;  // in the kernel's 16-B cells
   Geo g = p2_geo(h);
   g.kz = h->p2kz;
+  g.remap = h->p2order;
   cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(ps) + p2state_sums_offset());
   const bool split = p2_split(h);
   for (size_t si = 0; si < sched.size(); ++si) {
@@ -1047,6 +1049,11 @@ void alloc_all(nls_handle *h) {
     h->p2kz = (int)std::max<int64_t>(std::min<int64_t>(16, span), std::min<int64_t>(256, (span + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("NLS_P2_BLIND")) h->p2_blind = std::atoi(e) != 0;
+    // tile order (round 3, tools/order_sweep.py, tools/wl_ab.sh): 3D x-fastest without XCD
+    // bands (512^3 passes 25.6 -> 25.1 ms per step; 256^3 -0.5 %); 2D keeps the bands
+    // (4096^2 passes 3.14 -> 3.34 ms without them)
+    h->p2order = dim == 3 ? 6 : 0;
+    if (const char *e = std::getenv("NLS_P2_ORDER")) h->p2order = std::atoi(e);
     h->p2grid = p2_grid(h);
     if (h->p2reg)
       for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, h->p2mgrid[J]);
@@ -1066,14 +1073,19 @@ void alloc_all(nls_handle *h) {
     if (const char *e = std::getenv("NLS_KZ_ALPHA2")) h->kz_alpha2 = std::max(1, std::atoi(e));
     g2.kz = h->kz_alpha2;
     h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_l2_rows_per_thread()));
-    if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
-    Geo gf = g;
-    if (h->kz_fused) gf.kz = h->kz_fused;
-    const int64_t tt = stencil_tiles(gf, dim, fused_rows_per_thread());
     // large slabs: one tile per workgroup (the tail reduces nothing, so the grid
     // size only sets the dispatch balance): 512^3 m=16 tail 6.64 -> 6.38 ms against
     // two tiles per workgroup (tools/tail_sweep.sh, same box, two rounds)
     const bool one_tile = g.nloc > (int64_t(1) << 25) && !std::getenv("NLS_GRID_MULT");
+    // shallow tail tiles there and in 2D (4 planes / rows per wave; round 3,
+    // tools/order_sweep.py, tools/wl_ab.sh, same box): 512^3 6.25 -> 6.00 ms, 4096^2
+    // 0.775 -> 0.74, SG 8192^2 2.62 -> 2.51; the persistent grids of small 3D slabs keep
+    // the stencil depth (256^3: no gain)
+    h->kz_fused = (one_tile || dim == 2) ? 4 : 0;
+    if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
+    Geo gf = g;
+    if (h->kz_fused) gf.kz = h->kz_fused;
+    const int64_t tt = stencil_tiles(gf, dim, fused_rows_per_thread());
     for (int mode = 0; mode < 8; ++mode) {
       const void *ft = kernel_tail(tail_is_cplx(h, mode), dim, mode, h->m, ani);
       if (ft) h->tail_grid[mode] = one_tile ? (int)tt : occupancy_grid(h, ft, tt);

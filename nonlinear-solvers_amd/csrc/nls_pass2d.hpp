@@ -313,10 +313,23 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   const int nzc = g.q2 > 0 ? 2 * nz1 : nz1;
   const int ntiles = ntx * nty * nzc;
   // XCD-banded order: the 8 XCDs take contiguous tile ranges, so the y-adjacent
-  // tiles sharing S_J halo rows run on one XCD (its L2) at the same time
+  // tiles sharing S_J halo rows run on one XCD (its L2) at the same time (g.remap
+  // bit 4: plain order).  y-fastest inside a band, or (bit 2) x-fastest: the tiles
+  // of one 4-row group are then consecutive and read its rows whole together
   const int b = blockIdx.x, T8 = ntiles / 8;
-  const int tile = b < 8 * T8 ? (b % 8) * T8 + b / 8 : b;
-  const int yt = tile % nty, rest = tile / nty, xt = rest % ntx, zc = rest / ntx;
+  const int tile = (g.remap & 4) || b >= 8 * T8 ? b : (b % 8) * T8 + b / 8;
+  int yt, xt, zc;
+  if (g.remap & 2) {
+    xt = tile % ntx;
+    const int r_ = tile / ntx;
+    yt = r_ % nty;
+    zc = r_ / nty;
+  } else {
+    yt = tile % nty;
+    const int r_ = tile / nty;
+    xt = r_ % ntx;
+    zc = r_ / ntx;
+  }
   const int x0 = xt * P2D_XO, y0 = yt * P2D_TR;
   const bool hi = g.q2 > 0 && zc >= nz1;  // uniform
   const int za = hi ? g.q2 : qa, zb = hi ? g.q2 + (qb - qa) : qb;
