@@ -1024,7 +1024,11 @@ void alloc_all(nls_handle *h) {
     // (tools/slab_probe.py, profiles/r03/slab_probe.txt)
     const Geo gm = p2_geo(h);
     const int64_t cols = ((gm.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * std::max<int64_t>(1, gm.nyp / P2D_ROWS);
-    const int64_t nzc = std::max<int64_t>(1, (P2D_MIN_TILES + cols - 1) / cols);
+    // 3D: at least ~two tiles per CU (G2 256^3 m = 25: kz 128, 512 tiles: passes 10.42 ->
+    // 10.15 ms per step against kz 64 / 1024 tiles, 10.59 at kz 256 / 256 tiles; round 3,
+    // tools/wl_ab.sh); 2D planes of 4 rows keep P2D_MIN_TILES
+    const int64_t min_tiles = dim == 3 ? P2D_MIN_TILES / 2 : P2D_MIN_TILES;
+    const int64_t nzc = std::max<int64_t>(1, (min_tiles + cols - 1) / cols);
     if (h->p2reg) {
       const size_t lb = (size_t)(g.nzl + 2) * g.P * sizeof(cplx);
       hip_check(h, hipMalloc(&h->p2gbuf, lb), "hipMalloc(p2gbuf)");

@@ -34,6 +34,25 @@ __global__ __launch_bounds__(256) void kflat(const c2* __restrict__ W, long vs, 
   }
 }
 
+// one cell per thread, one short-lived workgroup per 256 cells (bw_probe3's best case);
+// dynamic LDS only to cap the resident workgroups per CU (occupancy of the real kernels)
+template <int K, int NW>
+__global__ __launch_bounds__(256) void kflat1(const c2* __restrict__ W, long vs, long n, c2* __restrict__ out) {
+  extern __shared__ char dyn[];
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  c2 s = {0, 0}, t = {0, 0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    c2 v = ldnt(W + k * vs + p);
+    s.x += v.x; s.y += v.y;
+    t.x += (k + 1) * v.x; t.y -= v.y;
+  }
+  if (s.x == 12345.0) dyn[threadIdx.x] = 1;
+  stnt(out + p, s);
+  if (NW > 1) stnt(out + vs + p, t);
+}
+
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 0 ? 0 : (N > 63 ? 63 : N)) : "memory");
 }
@@ -119,6 +138,14 @@ template <int K, int NW> void flat_case() {
            (K + NW) * g_n * 16.0 / 1e9 / (ms * 1e-3));
   }
 }
+template <int K, int NW> void flat1_case() {
+  for (int lds : {0, 40 * 1024, 80 * 1024, 160 * 1024}) {
+    if (lds > 64 * 1024) CHECK(hipFuncSetAttribute((const void*)kflat1<K, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    const float ms = timeit([&] { kflat1<K, NW><<<(int)((g_n + 255) / 256), 256, lds>>>(g_W, g_vs, g_n, g_out); }, 5);
+    printf("K=%2d NW=%d flat one cell/thread, LDS %3d KiB/WG   %7.3f ms %7.1f GB/s\n", K, NW, lds / 1024, ms,
+           (K + NW) * g_n * 16.0 / 1e9 / (ms * 1e-3));
+  }
+}
 template <int K, int NW, int NP, int NWV, int OCC> void dma_case() {
   const long nrows = g_n / 64;
   for (int R : {64, 256}) {
@@ -132,14 +159,23 @@ template <int K, int NW, int NP, int NWV, int OCC> void dma_case() {
 
 int main(int argc, char** argv) {
   const int n1 = argc > 1 ? atoi(argv[1]) : 512;
+  const long pad = argc > 2 ? atol(argv[2]) : 4096;  // stream stride pad in cells (4096: 64 KiB, the library's)
+  const int quick = argc > 3 ? atoi(argv[3]) : 0;
   g_n = (long)n1 * n1 * n1;
-  g_vs = g_n + 256;
+  g_vs = g_n + pad;
+  printf("n = %d^3, stream pad %ld cells\n", n1, pad);
   CHECK(hipMalloc(&g_W, (size_t)15 * g_vs * sizeof(c2)));
   CHECK(hipMalloc(&g_out, (size_t)2 * g_vs * sizeof(c2)));
   CHECK(hipMemset(g_W, 0, (size_t)15 * g_vs * sizeof(c2)));
   CHECK(hipDeviceGetAttribute(&g_ncu, hipDeviceAttributeMultiprocessorCount, 0));
   // the fused tail's pattern
+  flat1_case<15, 1>();
   flat_case<15, 1>();
+  if (quick) {
+    flat1_case<13, 2>();
+    flat1_case<1, 1>();
+    return 0;
+  }
   dma_case<15, 1, 2, 4, 1>();
   dma_case<15, 1, 2, 2, 2>();
   dma_case<15, 1, 3, 1, 3>();
