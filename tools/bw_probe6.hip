@@ -78,6 +78,30 @@ __global__ __launch_bounds__(256) void kpers(const c2* __restrict__ W, long vs, 
   }
 }
 
+// persistent grid with dynamic tile assignment: each workgroup takes the next tile
+// index from a global counter (vector atomic by one lane), so the tiles in flight
+// stay the next ones in order, as with one tile per workgroup
+template <int K, int NW, int FMA>
+__global__ __launch_bounds__(256) void kdyn(const c2* __restrict__ W, long vs, int nx, int ny, int nz, int kz,
+                                             c2* __restrict__ out, double a, int* ctr) {
+  extern __shared__ char dyn[];
+  __shared__ int s_t;
+  if (a == 12345.0) dyn[threadIdx.x] = 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ntx = nx / 64, nty = ny / 4, tiles = ntx * nty * (nz / kz);
+  const long P = (long)nx * ny;
+  for (;;) {
+    if (threadIdx.x == 0) s_t = atomicAdd(ctr, 1);
+    __syncthreads();
+    const int t = s_t;
+    __syncthreads();
+    if (t >= tiles) break;
+    const int xt = t % ntx, yt = (t / ntx) % nty, zt = t / (ntx * nty);
+    const long base = (long)(yt * 4 + w) * nx + xt * 64 + lane;
+    for (int q = zt * kz; q < zt * kz + kz; ++q) cell<K, NW, FMA>(W, vs, q * P + base, out, a);
+  }
+}
+
 template <class F> float timeit(F f, int reps) {
   hipEvent_t e0, e1; CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
   f(); CHECK(hipDeviceSynchronize());
@@ -89,9 +113,11 @@ template <class F> float timeit(F f, int reps) {
 static const int NX = 512;
 static long g_n, g_vs;
 static c2 *g_W, *g_out;
+static int* g_ctr;
 
 template <int K, int NW, int FMA> void run(int lds) {
   if (lds > 64 * 1024) {
+    CHECK(hipFuncSetAttribute((const void*)kdyn<K, NW, FMA>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     CHECK(hipFuncSetAttribute((const void*)kpers<K, NW, FMA>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     CHECK(hipFuncSetAttribute((const void*)kflat1<K, NW, FMA>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     CHECK(hipFuncSetAttribute((const void*)ktile<K, NW, FMA>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -102,6 +128,14 @@ template <int K, int NW, int FMA> void run(int lds) {
   int ncu = 0;
   CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
   const int per_cu = lds >= 160 * 1024 ? 1 : (lds >= 80 * 1024 ? 2 : 4);
+  for (int kz : {4, 16, 64}) {
+    ms = timeit([&] {
+      CHECK(hipMemsetAsync(g_ctr, 0, sizeof(int)));
+      kdyn<K, NW, FMA><<<ncu * per_cu, 256, lds>>>(g_W, g_vs, NX, NX, NX, kz, g_out, 1.0000001, g_ctr);
+    }, 5);
+    printf("K=%2d NW=%d FMA=%3d LDS %3d KiB  dynamic    kz=%-3d x-fast %7.3f ms %7.1f GB/s\n", K, NW, FMA, lds / 1024, kz, ms,
+           gb / ms * 1e3);
+  }
   for (int kz : {4, 16}) {
     ms = timeit([&] { kpers<K, NW, FMA><<<ncu * per_cu, 256, lds>>>(g_W, g_vs, NX, NX, NX, kz, g_out, 1.0000001); }, 5);
     printf("K=%2d NW=%d FMA=%3d LDS %3d KiB  persistent kz=%-3d x-fast %7.3f ms %7.1f GB/s\n", K, NW, FMA, lds / 1024, kz, ms,
@@ -123,12 +157,11 @@ int main() {
   CHECK(hipMalloc(&g_W, (size_t)15 * g_vs * sizeof(c2)));
   CHECK(hipMalloc(&g_out, (size_t)2 * g_vs * sizeof(c2)));
   CHECK(hipMemset(g_W, 0, (size_t)15 * g_vs * sizeof(c2)));
+  CHECK(hipMalloc(&g_ctr, sizeof(int)));
   // the fused tail (15 reads + 1 write) at the tail's occupancy (2 workgroups per CU)
   // and unlimited, without and with a compute phase
   run<15, 1, 0>(80 * 1024);
-  run<15, 1, 256>(80 * 1024);
   // the J = 12 pass pattern (13 reads + 2 writes), one workgroup per CU
   run<13, 2, 0>(160 * 1024);
-  run<13, 2, 0>(80 * 1024);
   return 0;
 }
