@@ -269,6 +269,17 @@ enum nls_op_kind {
 };
 int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n);
 
+/* Launch-shape knobs of a live handle, for same-allocation A/B measurements
+ * (tools/knob_ab.py; the environment variables of the same names set them at
+ * nls_create).  Results are unchanged up to the order of partial sums (the
+ * k_p2d tile order); not with NLS_GRAPH.  No reference counterpart. */
+enum nls_knob {
+  NLS_KNOB_TAIL_DYN = 1,  /* fused tail through the dynamic tile queue (NLS_TAIL_DYN) */
+  NLS_KNOB_KZ_FUSED = 2,  /* fused tail tile depth (NLS_KZ_FUSED; 0 = the stencil depth) */
+  NLS_KNOB_P2_ORDER = 3   /* k_p2d tile order bits (NLS_P2_ORDER) */
+};
+int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value);
+
 #ifdef __cplusplus
 }
 #endif

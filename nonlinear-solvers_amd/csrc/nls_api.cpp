@@ -140,6 +140,10 @@ struct nls_handle {
   bool p2_ani = false;         // k_p2d with the G2 operator (nls_pass2a.hip)          // real field marched as cell pairs by k_p2d (p2_geo)
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
+  int tail_dyn_grid[8] = {};  // resident workgroups of each tail kernel (dynamic tile queue)
+  bool tail_dyn = false;      // fused tail through the dynamic tile queue (NLS_TAIL_DYN)
+  bool tail_one_tile = false; // one tile per workgroup for the static tail grids
+  int32_t *tailq = nullptr;   // its counters (Geo::tq)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
   // the alpha pass j+1 is skipped (march_q; NLS_FUSED_ALPHA=0 disables)
   bool fused_alpha = false;
@@ -966,6 +970,27 @@ void ensure_scratch(nls_handle *h) {
     hip_check(h, hipMalloc(&h->scratch, (size_t)h->geo.nloc * h->esize), "hipMalloc(scratch)");
 }
 
+// grids of the fused tail kernels for the handle's tail depth: one tile per workgroup
+// (large slabs) or the occupancy grid, and the resident grid of the dynamic tile queue
+void tail_grids(nls_handle *h, bool one_tile) {
+  const int dim = h->cfg.dim;
+  Geo gf = h->geo;
+  if (h->kz_fused) gf.kz = h->kz_fused;
+  const int64_t tt = stencil_tiles(gf, dim, fused_rows_per_thread());
+  int ncu = 0;
+  hip_check(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev), "hipDeviceGetAttribute");
+  for (int mode = 0; mode < 8; ++mode) {
+    const void *ft = kernel_tail(tail_is_cplx(h, mode), dim, mode, h->m, h->ani);
+    h->tail_grid[mode] = h->tail_dyn_grid[mode] = 0;
+    if (!ft) continue;
+    h->tail_grid[mode] = one_tile ? (int)tt : occupancy_grid(h, ft, tt);
+    int per_cu = 0;
+    hip_check(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ft, NTHREADS, 0),
+              "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    h->tail_dyn_grid[mode] = (int)std::min<int64_t>(tt, (int64_t)std::max(per_cu, 1) * std::max(ncu, 1));
+  }
+}
+
 void alloc_all(nls_handle *h) {
   const Geo &g = h->geo;
   const bool c = h->cplx_;
@@ -1087,13 +1112,13 @@ void alloc_all(nls_handle *h) {
     // the stencil depth (256^3: no gain)
     h->kz_fused = (one_tile || dim == 2) ? 4 : 0;
     if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
-    Geo gf = g;
-    if (h->kz_fused) gf.kz = h->kz_fused;
-    const int64_t tt = stencil_tiles(gf, dim, fused_rows_per_thread());
-    for (int mode = 0; mode < 8; ++mode) {
-      const void *ft = kernel_tail(tail_is_cplx(h, mode), dim, mode, h->m, ani);
-      if (ft) h->tail_grid[mode] = one_tile ? (int)tt : occupancy_grid(h, ft, tt);
-    }
+    // the dynamic tile queue of the tail (nls_stencil.hpp tq_next): two counters, zero
+    // between launches (the last workgroup of each launch resets them)
+    if (const char *e = std::getenv("NLS_TAIL_DYN")) h->tail_dyn = std::atoi(e) != 0;
+    hip_check(h, hipMalloc(&h->tailq, 2 * sizeof(int32_t)), "hipMalloc(tailq)");
+    hip_check(h, hipMemsetAsync(h->tailq, 0, 2 * sizeof(int32_t), h->stream), "hipMemset");
+    h->tail_one_tile = one_tile;
+    tail_grids(h, one_tile);
   }
   // vectors stored per basis: m - 1 where every Lanczos run on it ends in a fused
   // tail (its k_tail exists for each use), else m.  1024^3 m=16 NLSE: 15 x 17.2 GB.
@@ -1211,9 +1236,11 @@ void free_all(nls_handle *h) {
   if (h->u_slot) h->u = nullptr;  // part of the basis allocation
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
                   (void *)h->vel, h->xedge, (void *)h->partX, h->p2, (void *)h->partP2,
-                  (void *)h->zbuf, (void *)h->p2lbuf, (void *)h->p2gbuf, (void *)h->partA, (void *)h->partU})
+                  (void *)h->zbuf, (void *)h->p2lbuf, (void *)h->p2gbuf, (void *)h->partA, (void *)h->partU,
+                  (void *)h->tailq})
     if (p) (void)hipFree(p);
   h->p2 = nullptr;
+  h->tailq = nullptr;
   h->partP2 = h->zbuf = h->p2lbuf = h->p2gbuf = nullptr;
   h->u = h->scratch = h->snap = h->uprev = nullptr;
   h->up = h->mf = h->cfb = h->vel = nullptr;
@@ -1569,9 +1596,10 @@ bool use_tail(const nls_handle *h, int mode) { return h->fused_tail && h->tail_g
 void tail_launch(nls_handle *h, int mode, TailArgs ta) {
   Geo g = h->geo;
   if (h->kz_fused) g.kz = h->kz_fused;
+  if (h->tail_dyn) g.tq = h->tailq;
   void *args[] = {&ta, &g};
   launch(h, 5, h->m, kernel_tail(tail_is_cplx(h, mode), (int)h->cfg.dim, mode, h->m, h->ani),
-         h->tail_grid[mode], args);
+         h->tail_dyn ? h->tail_dyn_grid[mode] : h->tail_grid[mode], args);
 }
 
 TailArgs tail_args(nls_handle *h, int b) {
@@ -2067,6 +2095,21 @@ int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n) {
   std::memcpy(out, h->oplog.data(), (size_t)std::min(cnt, cap) * 4 * sizeof(int32_t));
   h->oplog.clear();
   return NLS_OK;
+}
+
+int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value) {
+  return guarded(h, [&] {
+    if (h->use_graph) fail(h, NLS_ERR_STATE, "nls_debug_knob: not with NLS_GRAPH");
+    switch (knob) {
+      case NLS_KNOB_TAIL_DYN: h->tail_dyn = value != 0; break;
+      case NLS_KNOB_KZ_FUSED:
+        h->kz_fused = std::max(0, (int)value);
+        if (h->fused_tail) tail_grids(h, h->tail_one_tile);
+        break;
+      case NLS_KNOB_P2_ORDER: h->p2order = value; break;
+      default: fail(h, NLS_ERR_ARG, "nls_debug_knob: unknown knob");
+    }
+  });
 }
 
 int nls_reset_timing(nls_handle *h) {

@@ -64,6 +64,8 @@ struct Geo {
   int32_t qa, qb; // local planes [qa, qb) covered by a stencil launch (default 0, nzl)
   int32_t q2;     // k_p2d only: > 0 adds the range [q2, q2 + qb - qa) to the launch (the two
                   // boundary plane pairs of a split multi-rank pass in one grid); 0: none
+  int32_t *tq;       // march only: non-null = dynamic tile queue ([0] next tile, [1] workgroups
+                     // done; both back to 0 when the launch ends), else a static tile stride
   const double *cf;  // G2 anisotropic operator: c field at local plane 0 (ghost planes at
                      // -P and nzl*P, like a basis vector); unused by the isotropic operator
 };

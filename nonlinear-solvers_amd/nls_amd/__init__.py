@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "nls_rccl_unique_id", "nls_group_create", "nls_group_destroy", "nls_set_timing",
     "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
     "nls_get_field_async", "nls_wait_field", "nls_host_alloc", "nls_host_free", "nls_slab_planes",
-    "nls_step_sewi", "nls_debug_oplog",
+    "nls_step_sewi", "nls_debug_oplog", "nls_debug_knob",
 )
 # nls_debug_oplog entry kinds (include/nls.h enum nls_op_kind)
 OP_ALLREDUCE, OP_SEND, OP_RECV, OP_WAIT_HALO, OP_WAIT_COMPUTE = 1, 2, 3, 4, 5
@@ -124,6 +124,7 @@ def lib():
     L.nls_get_timing.argtypes = [H, C.POINTER(Timing)]
     L.nls_reset_timing.argtypes = [H]
     L.nls_debug_oplog.argtypes = [H, C.POINTER(C.c_int32), C.c_uint64, C.POINTER(C.c_uint64)]
+    L.nls_debug_knob.argtypes = [H, C.c_int32, C.c_int32]
     if L.nls_abi_version() != 5:
         raise RuntimeError("libnls_amd ABI mismatch")
     _LIB = L
@@ -342,6 +343,11 @@ class Solver:
         buf = (C.c_int32 * (4 * max(1, n.value)))()
         self._call(lib().nls_debug_oplog, buf, n.value, C.byref(n))  # copies and clears
         return [tuple(buf[4 * i:4 * i + 4]) for i in range(n.value)]
+
+    def debug_knob(self, knob: int, value: int):
+        """Launch-shape knob of this live handle (nls_debug_knob: 1 tail dynamic tile
+        queue, 2 tail tile depth, 3 k_p2d tile order), for same-allocation A/B runs."""
+        self._call(lib().nls_debug_knob, int(knob), int(value))
 
     def timing(self) -> dict:
         t = Timing()

@@ -18,7 +18,7 @@ m = int(sys.argv[2])
 steps = int(sys.argv[3])
 rounds = int(sys.argv[4])
 configs = sys.argv[5:] or [""]
-KNOBS = ("NLS_P2_ORDER", "NLS_P2_KZ", "NLS_KZ_FUSED", "NLS_TILE_REMAP", "NLS_KZ_ALPHA2")
+KNOBS = ("NLS_P2_ORDER", "NLS_P2_KZ", "NLS_KZ_FUSED", "NLS_TILE_REMAP", "NLS_KZ_ALPHA2", "NLS_TAIL_DYN")
 dx = 20.0 / (n - 1)
 rng = np.random.default_rng(0)
 x = np.linspace(-10, 10, n)
