@@ -71,6 +71,28 @@ __device__ __forceinline__ double bcast(double v, int l) { return __shfl(v, l, 6
 __device__ __forceinline__ cplx bcast(cplx v, int l) { return {__shfl(v.re, l, 64), __shfl(v.im, l, 64)}; }
 
 
+// Dynamic tile queue (Geo::tq, the fused tail's march): a resident grid whose workgroups take
+// the next tile index from a global counter, so the tiles being streamed at any moment
+// are the next ones in order -- a compact address window, which streams faster than
+// long per-workgroup marches that drift apart (DESIGN.md section 4, round 3;
+// tools/bw_probe6.hip: 15 reads + 1 write at 6.59 TB/s with 4-plane tiles against
+// 5.82-5.90 for one 256-plane march per workgroup).  Only for kernels without
+// per-workgroup partial sums: the tile -> workgroup assignment varies run to run.
+__device__ __forceinline__ int tq_next(int32_t *tq) {
+  __shared__ int s_tile;
+  __syncthreads();  // every thread has read the previous index
+  if (threadIdx.x == 0) s_tile = atomicAdd(tq, 1);
+  __syncthreads();
+  return s_tile;
+}
+// the last workgroup to finish (every other one has taken its last index) resets the queue
+__device__ __forceinline__ void tq_done(int32_t *tq) {
+  if (threadIdx.x == 0 && atomicAdd(tq + 1, 1) == (int)gridDim.x - 1) {
+    atomicExch(tq, 0);
+    atomicExch(tq + 1, 0);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Nonlinear half step, tau = 1j*dt
 //  0 cubic (nlse_solver.hpp:66-69): out = exp(-0.5*tau*rho) u, rho = re^2 + im^2

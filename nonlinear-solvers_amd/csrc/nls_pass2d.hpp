@@ -316,7 +316,8 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   // tiles sharing S_J halo rows run on one XCD (its L2) at the same time (g.remap
   // bit 4: plain order).  y-fastest inside a band, or (bit 2) x-fastest: the tiles
   // of one 4-row group are then consecutive and read its rows whole together
-  const int b = blockIdx.x, T8 = ntiles / 8;
+  const int b = blockIdx.x;
+  const int T8 = ntiles / 8;
   const int tile = (g.remap & 4) || b >= 8 * T8 ? b : (b % 8) * T8 + b / 8;
   int yt, xt, zc;
   if (g.remap & 2) {

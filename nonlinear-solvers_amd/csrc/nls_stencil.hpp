@@ -49,28 +49,6 @@ template <int DIM, int RB> __host__ __device__ inline void tile_counts(const Geo
 // zero when the neighbour is not coupled
 __device__ __forceinline__ double face_w(bool e, double ca, double cb) { return e ? 0.5 * (ca + cb) : 0.0; }
 
-// Dynamic tile queue (Geo::tq, the fused tail): a resident grid whose workgroups take
-// the next tile index from a global counter, so the tiles being streamed at any moment
-// are the next ones in order -- a compact address window, which streams faster than
-// long per-workgroup marches that drift apart (DESIGN.md section 4, round 3;
-// tools/bw_probe6.hip: 15 reads + 1 write at 6.59 TB/s with 4-plane tiles against
-// 5.82-5.90 for one 256-plane march per workgroup).  Only for kernels without
-// per-workgroup partial sums: the tile -> workgroup assignment varies run to run.
-__device__ __forceinline__ int tq_next(int32_t *tq) {
-  __shared__ int s_tile;
-  __syncthreads();  // every thread has read the previous index
-  if (threadIdx.x == 0) s_tile = atomicAdd(tq, 1);
-  __syncthreads();
-  return s_tile;
-}
-// the last workgroup to finish (every other one has taken its last index) resets the queue
-__device__ __forceinline__ void tq_done(int32_t *tq) {
-  if (threadIdx.x == 0 && atomicAdd(tq + 1, 1) == (int)gridDim.x - 1) {
-    atomicExch(tq, 0);
-    atomicExch(tq + 1, 0);
-  }
-}
-
 // fn(p, cur, lap) for every local cell p of the workgroup's tiles, with
 // cur = V[p] and lap = (L V)[p] (laplacians.hpp:10-105, flat-index form).
 // Local indices are 32-bit (the host guarantees (nzl+4)*P + pad < 2^31); the flat

@@ -4,7 +4,9 @@ to handle on one box, more than the effects measured here, so every variant runs
 the SAME handle, rounds interleaved.  Prints per variant and round the per-pass times,
 the tail and the step's kernel classes.
 usage: python tools/knob_ab.py n m steps rounds "knob=v,knob=v" ...
-knobs: tail_dyn (1), kz_fused (2), p2_order (3); "" = as created."""
+knobs: tail_dyn (1), kz_fused (2), p2_order (3); "" = as created.  (Tiles of k_p2d by
+ticket of a global counter measured +1.8 % pass time, and the tail's queue on the full
+tile grid +50 %: removed, profiles/r03/knob_ab_dyn.txt.)"""
 import os
 import sys
 
@@ -22,7 +24,6 @@ rng = np.random.default_rng(0)
 x = np.linspace(-10, 10, n)
 u0 = (np.exp(-(x[:, None, None] ** 2 + x[None, :, None] ** 2 + x[None, None, :] ** 2) / 8)
       + 1e-3 * rng.standard_normal((n, n, n))).astype(np.complex128).ravel()
-created = {}
 with nls_amd.Solver(3, n, n, n, dx, dx, m=m) as s:
     s.set_field(u0)
     s.step(1e-3, 2)
