@@ -1111,11 +1111,14 @@ void alloc_all(nls_handle *h) {
     // 0.775 -> 0.74, SG 8192^2 2.62 -> 2.51; the persistent grids of small 3D slabs keep
     // the stencil depth (256^3: no gain)
     h->kz_fused = (one_tile || dim == 2) ? 4 : 0;
-    // large 3D slabs: the dynamic tile queue on a resident grid with 16-plane tiles
-    // (512^3, same handle, tools/knob_ab.py: tail 6.03 -> 5.93 and 6.19 -> 6.13 ms on two
-    // boxes against one 4-plane tile per workgroup; profiles/r03/knob_ab_*.txt)
-    h->tail_dyn = one_tile && dim == 3;
-    if (h->tail_dyn) h->kz_fused = 16;
+    // the dynamic tile queue on a resident grid: large 3D slabs with 16-plane tiles (512^3,
+    // same handle, tools/knob_ab.py: tail 6.03 -> 5.93 and 6.19 -> 6.13 ms on two boxes
+    // against one 4-plane tile per workgroup; profiles/r03/knob_ab_*.txt) and the complex
+    // 2D fields with 4 rows per wave (4096^2: 0.744 -> 0.684-0.69 ms, tools/wl_ab.sh, two
+    // rounds); not the real 2D Gautschi tails (SG 8192^2: 2.53 -> 2.55) nor small 3D slabs
+    // (G2 256^3: 1.23-1.31 -> 1.26-1.36)
+    h->tail_dyn = (one_tile && dim == 3) || (dim == 2 && c);
+    if (h->tail_dyn && dim == 3) h->kz_fused = 16;
     if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
     // the dynamic tile queue of the tail (nls_stencil.hpp tq_next): two counters, zero
     // between launches (the last workgroup of each launch resets them)
