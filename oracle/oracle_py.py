@@ -100,6 +100,19 @@ def laplacian_r(g, x):
     return out
 
 
+def lanczos_c(g, u, m):
+    """lanczos_L (eigen_krylov_complex.hpp:10-53): V as m rows of n, T (m x m, T[r, c]),
+    beta0 = ||u||."""
+    ui = _c(u)
+    n = ui.size // 2
+    V = np.zeros(2 * n * m)
+    T = np.zeros(2 * m * m)
+    b = C.c_double(0.0)
+    _check(lib().oracle_lanczos_c(C.byref(g), ui, m, V, T, C.byref(b)))
+    # column-major n x m -> rows; column-major m x m -> T[r, c]
+    return V.view(np.complex128).reshape(m, n), T.view(np.complex128).reshape(m, m).T.copy(), b.value
+
+
 def krylov_c(g, u, t, m, func=0):
     ui = _c(u)
     out = np.zeros_like(ui)

@@ -36,20 +36,25 @@ def rel():
 # trajectory from an initial field perturbed by one ulp per component
 # (perturb_ulp, two seeds; self_floor).  Where it exceeds the north_star
 # tolerance the reference algorithm cannot resolve 1e-10 on that problem, and a
-# GPU trajectory is held to FLOOR_FACTOR x that floor instead.  The factor is the
-# per-step rounding of a valid implementation in units of that one-ulp start: the
+# GPU trajectory is held to a per-case factor x that floor instead.  The factor is
+# the per-step rounding of a valid implementation in units of that one-ulp start: the
 # GPU's first SS2 step differs from the oracle's by 8-14x the one-ulp floor
 # (different but equally exact summation orders: CGS / s-step vs MGS, tiles,
 # FMA), the numpy twin's by 25-140x, and the reference algorithm then amplifies
-# either deviation at the same rate (profiles/r03/parity_floor.txt: GPU/floor
-# stays 3-15 from step 1 to step 20).  The stiff tests also check that mechanism
-# directly (PROPAGATED_FACTOR x the oracle continued from the GPU's step-1 field).
-FLOOR_FACTOR = 32.0
-PROPAGATED_FACTOR = 4.0
+# either deviation at the same rate.  FLOOR_FACTORS are ~2x the largest GPU/floor
+# ratio observed where the floor exceeds the tolerance (profiles/r03/parity_floor.txt):
+# C1 0.71, 2D cubic at C2's spacing 7.8, 2D cubic-quintic 15.0, sine-Gordon at C4's
+# spacing 5.8.  The floored tests also check the mechanism directly: the GPU within
+# PROPAGATED_FACTOR x the oracle continued from the GPU's own early field (observed
+# GPU/propagated 0.57-1.34).
+# ("resolved": cases held to the tolerance at every checkpoint; the factor only labels
+# the parity record)
+FLOOR_FACTORS = {"c1": 2.0, "nlse2d_cubic": 16.0, "nlse2d_cq": 30.0, "sg": 12.0, "resolved": 1.0}
+PROPAGATED_FACTOR = 3.0
 
 
-def parity_bound(tol, floor):
-    return max(tol, FLOOR_FACTOR * floor)
+def parity_bound(tol, floor, case):
+    return max(tol, FLOOR_FACTORS[case] * floor)
 
 
 def perturb_ulp(u, seed):
@@ -82,10 +87,11 @@ def self_floor(run, u0, seeds=(101, 202)):
     return base, fl
 
 
-def record_parity(case, rows):
+def record_parity(case, rows, kind):
     """Append one case's per-checkpoint parity record to $NLS_PARITY_LOG (JSON
     lines; tools/parity_floor.py formats profiles/<round>/parity_floor.txt).
-    rows: [(checkpoint, gpu_err, self_floor, twin_floor or None[, propagated])]."""
+    rows: [(checkpoint, gpu_err, self_floor, twin_floor or None[, propagated])];
+    kind: the FLOOR_FACTORS key of the case."""
     path = os.environ.get("NLS_PARITY_LOG")
     if not path:
         return
@@ -94,5 +100,5 @@ def record_parity(case, rows):
         f.write(json.dumps({"case": case, "rows": [
             {"checkpoint": r[0], "gpu_err": r[1], "self_floor": r[2], "twin_floor": r[3],
              "propagated": r[4] if len(r) > 4 else None,
-             "bound": parity_bound(1e-10, r[2]), "ratio_gpu_self": (r[1] / r[2]) if r[2] > 0 else None}
+             "bound": parity_bound(1e-10, r[2], kind), "ratio_gpu_self": (r[1] / r[2]) if r[2] > 0 else None}
             for r in rows]}) + "\n")

@@ -87,9 +87,13 @@ def test_c1_nlse_call_full_run_matches_oracle(tmp_path):
     high-mode rounding noise up by prod ||L|| / beta_j): the oracle started from
     u0 moved by one ulp per component drifts from the unperturbed oracle to ~1e-6
     after 5 steps and saturates near 1e-5 (conftest.self_floor).  The bound per
-    snapshot is parity_bound(1e-10, that self-floor); one step is checked at 1e-10
-    through the C-ABI directly."""
-    from conftest import parity_bound, record_parity, self_floor
+    snapshot is parity_bound(1e-10, that self-floor, "c1") = max(1e-10, 2 x floor)
+    (observed GPU / floor <= 0.71, profiles/r03/parity_floor.txt); one step is checked
+    at 1e-10 through the C-ABI directly, and the mechanism itself: the oracle continued
+    from the GPU's field after that one step lands within PROPAGATED_FACTOR of the GPU
+    at every later snapshot (the GPU's deviation is its first step's rounding, amplified
+    by the reference algorithm at its own rate)."""
+    from conftest import PROPAGATED_FACTOR, parity_bound, record_parity, self_floor
     n, L, T, nt, ns = 256, 10.0, 0.5, 500, 100
     u0 = ic(2, n, L)
     fi, fo = tmp_path / "u0.npy", tmp_path / "traj.npy"
@@ -105,11 +109,6 @@ def test_c1_nlse_call_full_run_matches_oracle(tmp_path):
     ref, floor = self_floor(lambda u: reference_trajectory(2, n, L, u, T, nt, ns), u0.ravel())
     ref = ref.reshape(ns, n, n)
     twin = twin_trajectory(n, L, u0, T, nt, ns).reshape(ns, n, n) if os.environ.get("NLS_PARITY_LOG") else None
-    rows = [(k, rel_l2(out[k], ref[k]), floor[k], rel_l2(twin[k], ref[k]) if twin is not None else None)
-            for k in range(ns)]
-    record_parity("C1 nlse_call 256^2 T=0.5 nt=500 ns=100 (snapshot = every 5 steps)", rows)
-    bad = [(k, e, f) for k, e, f, _ in rows if e > parity_bound(1e-10, f)]
-    assert not bad, "snapshot, gpu err, self-floor: " + ", ".join(f"({k}, {e:.2e}, {f:.2e})" for k, e, f in bad[:8])
     # one SS2 step of the same workload: below the floor's growth, 1e-10 holds
     import nls_amd
     dx = 2 * L / (n - 1)
@@ -118,7 +117,20 @@ def test_c1_nlse_call_full_run_matches_oracle(tmp_path):
         s.set_field(u)
         s.step(T / nt, 1)
         one = s.get_field()
-    assert rel_l2(one, O.nlse_steps(O.grid(2, n, n, 1, dx, dx), u, T / nt, 1, 10)) <= 1e-10
+    g = O.grid(2, n, n, 1, dx, dx)
+    assert rel_l2(one, O.nlse_steps(g, u, T / nt, 1, 10)) <= 1e-10
+    # the oracle continued from the GPU's step-1 field, snapshot by snapshot
+    prop, v, freq = {}, one, nt // ns
+    for k in range(1, ns):  # snapshot k is step k * freq; v holds step 1, then (k-1) * freq
+        v = O.nlse_steps(g, v, T / nt, freq - 1 if k == 1 else freq, 10)
+        prop[k] = rel_l2(v, ref[k])
+    rows = [(k, rel_l2(out[k], ref[k]), floor[k], rel_l2(twin[k], ref[k]) if twin is not None else None,
+             prop.get(k)) for k in range(ns)]
+    record_parity("C1 nlse_call 256^2 T=0.5 nt=500 ns=100 (snapshot = every 5 steps)", rows, "c1")
+    bad = [(k, e, f, p) for k, e, f, _, p in rows
+           if e > parity_bound(1e-10, f, "c1") or (p is not None and e > max(1e-10, PROPAGATED_FACTOR * p))]
+    assert not bad, "snapshot, gpu err, self-floor, propagated: " + ", ".join(
+        f"({k}, {e:.2e}, {f:.2e}, {p if p is None else f'{p:.2e}'})" for k, e, f, p in bad[:8])
 
 
 def test_nlse_call_3d_matches_oracle(tmp_path):

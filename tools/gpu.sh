@@ -1,0 +1,88 @@
+#!/bin/bash
+# One launcher for every GPU measurement of a round (replaces the per-call scripts).
+#   bash tools/gpu.sh TAG STEP [STEP ...]        (run through gpurun, from the repo root)
+# Output goes to gpurun_out/TAG/.  Steps (each under its own time limit; the chain
+# stops at the first step that faults, aborts, times out or fails):
+#   suite          pytest -m gpu (one process)            -> suite.txt
+#   suite:EXPR     the same restricted to -k EXPR
+#   smoke          __graft_entry__.smoke()                 -> smoke.txt
+#   bench          python bench.py (headline, cpu baseline) -> bench_nlse3d_512.json
+#   bench:WL       python bench.py --workload WL            -> bench_WL.json
+#   set            bench of every BASELINE workload + KG    -> bench_*.json
+#   prof[:WL]      bench under rocprofv3 --kernel-trace --stats -> prof_WL/, bench_WL_under_rocprof.json
+#   pmc[:WL]       FETCH_SIZE / WRITE_SIZE / TCC hit passes, one counter group per run -> pmc_WL/
+#   py:SCRIPT[:ARGS] python SCRIPT ARGS (a probe)           -> py_<name>.txt
+set -o pipefail
+TAG=$1
+shift
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+run() {  # run LIMIT OUTFILE CMD...: stop the chain on any failure
+  local lim=$1 out=$2
+  shift 2
+  echo "[gpu.sh] $(date +%T) $*"
+  timeout -k 10 "$lim" "$@" > "$out" 2> "$out.err"
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "[gpu.sh] '$*' exited $rc; stopping" >&2
+    tail -20 "$out" "$out.err" >&2
+    exit $rc
+  fi
+}
+for st in "$@"; do
+  name=${st%%:*}
+  arg=""
+  [ "$name" != "$st" ] && arg=${st#*:}
+  case $name in
+    suite)
+      if [ -n "$arg" ]; then
+        run 900 "$OUT/suite.txt" python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$arg"
+      else
+        run 900 "$OUT/suite.txt" python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+      fi
+      tail -3 "$OUT/suite.txt" ;;
+    smoke)
+      run 180 "$OUT/smoke.txt" python -c "import __graft_entry__ as g; g.smoke()"
+      cat "$OUT/smoke.txt" ;;
+    bench)
+      if [ -n "$arg" ]; then
+        run 300 "$OUT/bench_$arg.json" python bench.py --workload "$arg" --no-cpu-baseline
+        cat "$OUT/bench_$arg.json"
+      else
+        run 300 "$OUT/bench_nlse3d_512.json" python bench.py
+        cat "$OUT/bench_nlse3d_512.json"
+      fi ;;
+    set)
+      for w in nlse2d_4096 sg2d_8192 g2_3d_256 kg_3d_256 cq3d_1024 nlse3d_512; do
+        run 300 "$OUT/bench_$w.json" python bench.py --workload "$w" --steps 10 --warmup 2 --no-cpu-baseline
+        cat "$OUT/bench_$w.json"
+      done ;;
+    prof)
+      wl=${arg:-nlse3d_512}
+      run 300 "$OUT/bench_${wl}_under_rocprof.json" rocprofv3 --kernel-trace --stats -d "$OUT/prof_$wl" -o run \
+        --output-format csv -- python3 bench.py --workload "$wl" --steps 10 --warmup 2 --no-cpu-baseline
+      cat "$OUT/bench_${wl}_under_rocprof.json" ;;
+    pmc)
+      wl=${arg:-nlse3d_512}
+      i=0
+      mkdir -p "$OUT/pmc_$wl"
+      for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+        i=$((i + 1))
+        echo "[gpu.sh] $(date +%T) pmc $grp"
+        timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_$wl/p$i" -o run -- \
+          python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/pmc_$wl/p$i.log" 2>&1 || exit $?
+      done ;;
+    py)
+      script=${arg%%:*}
+      args=""
+      [ "$script" != "$arg" ] && args=${arg#*:}
+      # shellcheck disable=SC2086
+      run 600 "$OUT/py_$(basename "$script" .py).txt" python -u "$script" $args
+      tail -40 "$OUT/py_$(basename "$script" .py).txt" ;;
+    *)
+      echo "[gpu.sh] unknown step $st" >&2
+      exit 2 ;;
+  esac
+done
+echo "[gpu.sh] $(date +%T) done"
