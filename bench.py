@@ -114,7 +114,7 @@ def moved_bytes_per_cell_step(w, m, sched, pass2, u_frac, tm, steps):
     if pass2 and eq == 3:
         reg = tm["update_count"][0] > 1.5 * max(1, tm["steps"])  # two J = 0 launches per run
         if reg:
-            # register two-vector passes (k_p2g_lap + k_p2g): per pass S_J + c read and y =
+            # register two-vector passes (k_lap + k_p2m): per pass S_J + c read and y =
             # L S_J written, then y (stencil) + c + S_0..S_J read and ns vectors written
             passes = sum((j + 1 + ns) * 16 + (16 + 8 + 16) + (16 + 8) for j, ns in sched)
         else:

@@ -255,8 +255,9 @@ int nls_reset_timing(nls_handle *h);
  * the cross-stream dependencies between them.  Recorded only when the
  * environment has NLS_OPLOG=1 at nls_create.  Entries are 4 int32 each:
  * {kind, stream (0 compute, 1 halo), count (doubles), peer rank (-1: none)}.
- * Sets *n to the number recorded; with out != NULL also copies at most cap
- * entries into out and clears the log (out == NULL: size query only).  The invariant the tests check: an operation
+ * Sets *n to the number recorded; with out != NULL also copies the oldest
+ * min(*n, cap) entries into out and removes exactly those from the log (out ==
+ * NULL: size query only).  The log keeps at most NLS_OPLOG_MAX entries (the newest).  The invariant the tests check: an operation
  * on one stream is ordered after every earlier operation on the other stream
  * by a NLS_OP_WAIT_* entry in between (RCCL never sees one communicator's
  * operations in flight on two streams at once). */
@@ -267,6 +268,7 @@ enum nls_op_kind {
   NLS_OP_WAIT_HALO = 4,      /* compute stream waits for the halo stream */
   NLS_OP_WAIT_COMPUTE = 5    /* halo stream waits for the compute stream */
 };
+#define NLS_OPLOG_MAX 65536
 int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n);
 
 /* Launch-shape knobs of a live handle, for same-allocation A/B measurements

@@ -97,11 +97,9 @@ struct nls_handle {
   int gfun = -1;            // G2 Gautschi family (NLS_SG_G2 .. NLS_PHI4): GautschiForce; -1 G1 sine-Gordon
   double *vel = nullptr;    // KG velocity v = (u - u_past)/dt of the last step
   bool vel_valid = false;   //   (set by every KG step, before the driver's BC)
-  bool u_slot = false;      // u stored as slot nvec[0] of basis 0
   int nvec[2] = {0, 0};     // vectors stored per basis (m, or m - 1 with a fused tail)
   void *uprev = nullptr;    // G2 sEWI: u of the previous step (nlse_dev.hpp:206-229)
   bool uprev_set = false;
-  int64_t u_off = 0;        // extra element offset of that slot
   bool coef_set = false;
   void *scratch = nullptr;  // nloc elements
   cplx *partA = nullptr, *partU = nullptr;
@@ -129,8 +127,8 @@ struct nls_handle {
   int p2mgrid[MMAX] = {};      // k_p2m grid per J
   int p2lapgrid = 0;           // k_lap grid over planes [-1, nzl]
   int p2mkz = 16;              // tile depth of k_lap / k_p2m (G2 256^3 m=25: 13.36 ms/step vs 13.76 at 32)
-  bool p2_blind = true;        // J = 0 pass without an alpha pass once warm (NLS_P2_BLIND=0: off)
-  int p2order = 0;             // k_p2d tile order (Geo::remap bits: 2 x-fastest, 4 no XCD bands; NLS_P2_ORDER)
+  bool p2_blind = true;        // J = 0 pass without an alpha pass once warm
+  int p2order = 0;             // k_p2d tile order (Geo::remap bits: 2 x-fastest, 4 no XCD bands; debug knob 3)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
   // a new state was set (nls_set_*): the next step starts its bases cold, so it is
   // issued eagerly, never replayed from a graph captured warm (run-to-run bitwise
@@ -141,7 +139,7 @@ struct nls_handle {
   int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
   int tail_dyn_grid[8] = {};  // resident workgroups of each tail kernel (dynamic tile queue)
-  bool tail_dyn = false;      // fused tail through the dynamic tile queue (NLS_TAIL_DYN)
+  bool tail_dyn = false;      // fused tail through the dynamic tile queue (debug knob 1)
   bool tail_one_tile = false; // one tile per workgroup for the static tail grids
   int32_t *tailq = nullptr;   // its counters (Geo::tq)
   // folded alpha (single-rank handles): update pass j also reduces q = y^H L y and
@@ -173,7 +171,7 @@ struct nls_handle {
   hipStream_t cstream = nullptr;
   hipEvent_t ev_bnd = nullptr, ev_halo = nullptr, ev_bdone = nullptr;
   bool halo_pending = false;
-  bool bnd_side = true;  // boundary-plane launches on cstream (NLS_BND_SIDE=0: in order on the compute stream)
+  bool bnd_side = true;  // boundary-plane launches on cstream
   // debug (NLS_OPLOG=1 at nls_create): the transport operations in issue order, with
   // the cross-stream waits between them (nls_debug_oplog; tests/test_gpu_oplog.py)
   bool oplog_on = false;
@@ -185,11 +183,6 @@ struct nls_handle {
   hipEvent_t ev_snap = nullptr, ev_snap_done = nullptr;
   void *snap = nullptr;
   bool snap_issued = false;
-  // bounded host run-ahead: at most `runahead` steps enqueued beyond the GPU
-  static constexpr int RA_MAX = 16;
-  hipEvent_t stepev[RA_MAX] = {};
-  int runahead = 0;  // NLS_RUNAHEAD=k: off by default (no measured effect, tools/exp_runahead.sh)
-  uint64_t steps_issued = 0;
   // hipGraph replay of steady-state steps (single-rank handles): one graph
   // launch per step instead of ~3m kernel launches; keyed by dt
   bool use_graph = false;
@@ -247,7 +240,9 @@ char *vec_ptr(nls_handle *h, int b, int k) {  // local plane 0 of vector k of ba
 
 // debug op log (NLS_OPLOG=1): transport operations and cross-stream waits in issue order
 void oplog(nls_handle *h, int kind, int stream, int64_t count, int peer) {
+  // bounded (NLS_OPLOG_MAX entries): a long run with the log on keeps the newest ones
   if (!h->oplog_on) return;
+  if (h->oplog.size() >= 4 * (size_t)NLS_OPLOG_MAX) h->oplog.erase(h->oplog.begin(), h->oplog.begin() + 4);
   h->oplog.insert(h->oplog.end(), {(int32_t)kind, (int32_t)stream, (int32_t)count, (int32_t)peer});
 }
 int stream_id(const nls_handle *h, hipStream_t st) { return st && st == h->cstream ? 1 : 0; }
@@ -710,7 +705,7 @@ int64_t min_slab_planes(const nls_handle *h) { return h->geo.npl / std::max(1, h
 // (nyp = 4, npl = ny/4, P = 4 nx; single rank), whose row wrap is the 2D y neighbour
 Geo p2_geo(const nls_handle *h) {
   Geo g = h->geo;
-  if (h->p2reg) return g;  // k_p2g works on the handle's own planes
+  if (h->p2reg) return g;  // k_lap + k_p2m work on the handle's own planes
   if (h->p2_pr) {  // pairs of cells along x
     g.nx = h->geo.nx / 2;
     g.P = h->geo.P / 2;
@@ -945,15 +940,13 @@ void setup_geometry(nls_handle *h) {
   // 16-32; on small slabs (persistent grids) it is slower (tools/exp_kz.sh)
   h->kz_alpha = (c.dim == 3 && g.nloc > (int64_t(1) << 25)) ? 4 : g.kz;
   if (const char *e = std::getenv("NLS_KZ_ALPHA")) h->kz_alpha = std::max(1, std::atoi(e));
-  g.remap = 0;
-  if (const char *e = std::getenv("NLS_TILE_REMAP")) g.remap = std::atoi(e) != 0;
+  g.remap = 0;  // (march's XCD-banded order, Geo::remap, measured no gain for these kernels)
   // Pad the vector stride so the m streams of one update pass do not start on
   // the same HBM channel (strides of 2^k * plane bytes camp on one channel).
   // 4096 elements (64 KiB of complex<double>): same-box A/B sweeps (tools/exp_pad3.sh,
   // exp_pad4.sh) gave 512^3 update passes -5 % (two boxes), 4096^2 +6 % vs the former
   // 4 KiB pad, within 1 % elsewhere; no pad at all is ~15 % slower (tools/bw_probe.hip)
   h->vpad = 4096;
-  if (const char *e = std::getenv("NLS_VEC_PAD")) h->vpad = std::max<int64_t>(0, std::atoll(e));
   // (the vector stride h->vs follows in alloc_all, once the ghost depth is known)
 }
 
@@ -1017,7 +1010,7 @@ void alloc_all(nls_handle *h) {
                       g.nloc + 2 * g.P < (int64_t(1) << 31);  // 32-bit cell indices
     // k_p2d: whole 4-row tiles, rings for J <= m-4 within LDS
     const bool dma = (dim == 3 ? g.nyp % P2D_ROWS == 0 && g.nyp >= 4 : d2) && h->m - 4 <= P2D_MAXJ;
-    // the register form k_p2g (complex fields): the G2 anisotropic NLSE (div(c grad); not
+    // the register form k_lap + k_p2m (complex fields): the G2 anisotropic NLSE (div(c grad); not
     // the real Klein-Gordon) and the isotropic grids k_p2d does not take (ny % 4 != 0,
     // 2D slabs, m > 18); J <= 28
     const bool reg = c && !h->kg && h->nbasis == 1 && h->m >= 3 && h->m <= MMAX - 2 &&
@@ -1058,7 +1051,6 @@ void alloc_all(nls_handle *h) {
       const size_t lb = (size_t)(g.nzl + 2) * g.P * sizeof(cplx);
       hip_check(h, hipMalloc(&h->p2gbuf, lb), "hipMalloc(p2gbuf)");
       hip_check(h, hipMemsetAsync(h->p2gbuf, 0, lb, h->stream), "hipMemset");
-      if (const char *e = std::getenv("NLS_P2M_KZ")) h->p2mkz = std::max(1, std::atoi(e));
       const Geo gl = p2m_lap_geo(h);
       h->p2lapgrid = occupancy_grid(h, kernel_lap(true, dim, ani), stencil_tiles(gl, dim, alpha_rows_per_thread()));
       Geo gm = g;
@@ -1077,12 +1069,10 @@ void alloc_all(nls_handle *h) {
     const int64_t span = p2_split(h) ? gm.nzl - 4 : gm.nzl;
     h->p2kz = (int)std::max<int64_t>(std::min<int64_t>(16, span), std::min<int64_t>(256, (span + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("NLS_P2_BLIND")) h->p2_blind = std::atoi(e) != 0;
     // tile order (round 3, tools/order_sweep.py, tools/wl_ab.sh): 3D x-fastest without XCD
     // bands (512^3 passes 25.6 -> 25.1 ms per step; 256^3 -0.5 %); 2D keeps the bands
     // (4096^2 passes 3.14 -> 3.34 ms without them)
     h->p2order = dim == 3 ? 6 : 0;
-    if (const char *e = std::getenv("NLS_P2_ORDER")) h->p2order = std::atoi(e);
     h->p2grid = p2_grid(h);
     if (h->p2reg)
       for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, h->p2mgrid[J]);
@@ -1099,7 +1089,6 @@ void alloc_all(nls_handle *h) {
   if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && (std::atoi(e) != 0 || h->pass2);
   if (h->fused_tail) {
     Geo g2 = g;
-    if (const char *e = std::getenv("NLS_KZ_ALPHA2")) h->kz_alpha2 = std::max(1, std::atoi(e));
     g2.kz = h->kz_alpha2;
     h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_l2_rows_per_thread()));
     // large slabs: one tile per workgroup (the tail reduces nothing, so the grid
@@ -1119,10 +1108,8 @@ void alloc_all(nls_handle *h) {
     // (G2 256^3: 1.23-1.31 -> 1.26-1.36)
     h->tail_dyn = (one_tile && dim == 3) || (dim == 2 && c);
     if (h->tail_dyn && dim == 3) h->kz_fused = 16;
-    if (const char *e = std::getenv("NLS_KZ_FUSED")) h->kz_fused = std::max(0, std::atoi(e));
     // the dynamic tile queue of the tail (nls_stencil.hpp tq_next): two counters, zero
     // between launches (the last workgroup of each launch resets them)
-    if (const char *e = std::getenv("NLS_TAIL_DYN")) h->tail_dyn = std::atoi(e) != 0;
     hip_check(h, hipMalloc(&h->tailq, 2 * sizeof(int32_t)), "hipMalloc(tailq)");
     hip_check(h, hipMemsetAsync(h->tailq, 0, 2 * sizeof(int32_t), h->stream), "hipMemset");
     h->tail_one_tile = one_tile;
@@ -1144,16 +1131,10 @@ void alloc_all(nls_handle *h) {
     }
   }
 
-  // NLS_U_SLOT=1 [NLS_U_OFF=k]: keep the NLSE state u in an extra slot after
-  // the basis vectors (+k elements) instead of its own allocation.  Measured:
-  // no systematic effect; the final pass is bimodal (6.6 / 7.45 ms at 512^3)
-  // from run to run with either placement (tools/exp_uslot.sh).
-  h->u_slot = false;
-  if (const char *e = std::getenv("NLS_U_SLOT")) h->u_slot = h->cplx_ && std::atoi(e) != 0;
-  if (const char *e = std::getenv("NLS_U_OFF")) h->u_off = std::max<int64_t>(0, std::atoll(e));
+  // (u in an extra slot after the basis vectors measured no systematic effect against
+  // its own allocation, tools/exp_uslot.sh in round 1; removed in round 4)
   for (int b = 0; b < h->nbasis; ++b) {
-    const size_t bytes = (size_t)(h->nvec[b] + (b == 0 && h->u_slot ? 1 : 0)) * h->vs * h->esize +
-                         (b == 0 && h->u_slot ? (size_t)h->u_off * h->esize : 0);
+    const size_t bytes = (size_t)h->nvec[b] * h->vs * h->esize;
     hip_check(h, hipMalloc(&h->B[b].W, bytes), "hipMalloc(basis)");
     hip_check(h, hipMemsetAsync(h->B[b].W, 0, bytes, h->stream), "hipMemset");
     hip_check(h, hipMalloc(&h->B[b].st, sizeof(KState)), "hipMalloc(state)");
@@ -1161,8 +1142,7 @@ void alloc_all(nls_handle *h) {
   }
   const size_t nbytes = (size_t)g.nloc * h->esize;
   if (h->cplx_) {
-    if (h->u_slot) h->u = vec_ptr(h, 0, h->nvec[0]) + h->u_off * (int64_t)h->esize;
-    else hip_check(h, hipMalloc(&h->u, nbytes), "hipMalloc(u)");
+    hip_check(h, hipMalloc(&h->u, nbytes), "hipMalloc(u)");
     if (h->ani || h->nonlin == 3) hip_check(h, hipMalloc(&h->mf, (size_t)g.nloc * sizeof(double)), "hipMalloc(m)");
   } else {
     hip_check(h, hipMalloc(&h->up, nbytes), "hipMalloc(u_past)");
@@ -1241,7 +1221,6 @@ void free_all(nls_handle *h) {
     if (h->B[b].st) (void)hipFree(h->B[b].st);
     h->B[b] = Basis{};
   }
-  if (h->u_slot) h->u = nullptr;  // part of the basis allocation
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
                   (void *)h->vel, h->xedge, (void *)h->partX, h->p2, (void *)h->partP2,
                   (void *)h->zbuf, (void *)h->p2lbuf, (void *)h->p2gbuf, (void *)h->partA, (void *)h->partU,
@@ -1359,8 +1338,6 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
   h->s2 = {c.sigma2[0], c.sigma2[1]};
   h->rank = c.rank;
   h->nranks = c.nranks;
-  if (const char *e = std::getenv("NLS_RUNAHEAD"))
-    h->runahead = std::min(nls_handle::RA_MAX, std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("NLS_GRAPH")) h->use_graph = std::atoi(e) != 0;
   if (const char *e = std::getenv("NLS_OPLOG")) h->oplog_on = std::atoi(e) != 0;
   h->dbg_sums = std::getenv("NLS_DEBUG_SUMS") != nullptr;
@@ -1398,7 +1375,6 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
       rccl_check(h, ncclCommInitRank(&h->comm, 1, id, 0), "ncclCommInitRank");
     }
     h->collective = h->nranks > 1 || h->comm != nullptr;
-    if (const char *e = std::getenv("NLS_BND_SIDE")) h->bnd_side = std::atoi(e) != 0;
     if (h->collective) {
       // (a high-priority stream here measured every kernel of the process 2x slower)
       hip_check(h, hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking), "hipStreamCreate");
@@ -1434,8 +1410,6 @@ int nls_destroy(nls_handle *h) {
   if (h->xstream) (void)hipStreamSynchronize(h->xstream);
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_bdone, h->ev_snap, h->ev_snap_done})
-    if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : h->stepev)
     if (e) (void)hipEventDestroy(e);
   if (h->cstream) (void)hipStreamDestroy(h->cstream);
   if (h->xstream) (void)hipStreamDestroy(h->xstream);
@@ -1493,6 +1467,10 @@ int nls_local_planes(const nls_handle *h, uint32_t *z0, uint32_t *nzl, uint64_t 
 void p2_cold(nls_handle *h) {
   h->p2_warm[0] = h->p2_warm[1] = false;
   h->p2_fresh = true;
+  // the tail's tile-queue counters return to 0 at the end of every launch; a launch
+  // that did not complete would leave them set, and every later tail on this handle
+  // would skip tiles -- every new state starts from zeroed counters
+  if (h->tailq) hip_check(h, hipMemsetAsync(h->tailq, 0, 2 * sizeof(int32_t), h->stream), "hipMemset");
 }
 
 int nls_set_field(nls_handle *h, const double *u, uint64_t n) {
@@ -1841,7 +1819,7 @@ void finish_step_flags(nls_handle *h, double dt) {
 // events, and for the NLSE a live start vector W_0 built with this dt (otherwise
 // the step begins with k_nl_init).  The graph is captured on first use per dt.
 bool graph_ready(nls_handle *h, double dt) {
-  if (!h->use_graph || h->collective || h->timing || h->runahead > 0) return false;
+  if (!h->use_graph || h->collective || h->timing) return false;
   if (h->pass2 && h->p2_fresh) return false;  // the first step after nls_set_*: cold bases
   if (h->cplx_ && (!h->w0_ready || h->w0_dt != dt)) return false;
   if (h->gexec && h->gdt == dt) return true;
@@ -1874,11 +1852,6 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
     if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");
     if (h->kg && !(dt > 0.0)) fail(h, NLS_ERR_ARG, "KG: dt must be > 0 (v = (u - u_past)/dt)");
     for (uint32_t s = 0; s < nsteps; ++s) {
-      // Optionally keep the host at most `runahead` steps ahead of the device
-      // (bounded queue depth for callers that enqueue thousands of steps).
-      const int ra = h->runahead;
-      if (ra > 0 && h->steps_issued >= (uint64_t)ra)
-        hip_check(h, hipEventSynchronize(h->stepev[h->steps_issued % ra]), "hipEventSynchronize");
       if (graph_ready(h, dt)) {
         hip_check(h, hipGraphLaunch(h->gexec, h->stream), "hipGraphLaunch");
         finish_step_flags(h, dt);
@@ -1895,12 +1868,6 @@ int nls_step(nls_handle *h, double dt, uint32_t nsteps) {
         h->p2_fresh = false;  // every basis of the step is warm now
       }
       h->tacc.steps += 1;
-      if (ra > 0) {
-        hipEvent_t &e = h->stepev[h->steps_issued % ra];
-        if (!e) hip_check(h, hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-        hip_check(h, hipEventRecord(e, h->stream), "hipEventRecord");
-      }
-      ++h->steps_issued;
     }
     hip_check(h, hipGetLastError(), "kernel launch");
   });
@@ -2100,8 +2067,11 @@ int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n) {
   const uint64_t cnt = h->oplog.size() / 4;
   *n = cnt;
   if (!out) return NLS_OK;  // size query: the log is kept
-  std::memcpy(out, h->oplog.data(), (size_t)std::min(cnt, cap) * 4 * sizeof(int32_t));
-  h->oplog.clear();
+  // copy the oldest min(n, cap) entries and drop only those: a short buffer drains the
+  // log over several calls instead of losing the rest
+  const uint64_t take = std::min(cnt, cap);
+  std::memcpy(out, h->oplog.data(), (size_t)take * 4 * sizeof(int32_t));
+  h->oplog.erase(h->oplog.begin(), h->oplog.begin() + (ptrdiff_t)(take * 4));
   return NLS_OK;
 }
 

@@ -24,7 +24,7 @@
 namespace nls {
 
 // The per-workgroup partials of a pass whose accumulators are split over wave pairs
-// (HZ: X set on even waves, Z set on odd ones; k_p2g, k_p2b) in k_p2d's column order:
+// (HZ: X set on even waves, Z set on odd ones; k_p2m, k_p2b) in k_p2d's column order:
 // [S_l^H X (l <= J)] [S_l^H Z] [X^H X] [X^H Z] [Z^H Z] [||S_0||^2 (J = 0)], without Z
 // [S_l^H X] [X^H X] [||S_0||^2] summed over all four waves.
 template <int J, bool HZ, int NC, int NH>

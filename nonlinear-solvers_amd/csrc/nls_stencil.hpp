@@ -83,186 +83,314 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
       const int x = it * 64 + lane;
       const bool xin = x < nx;
       const int yb = jt * (4 * RB) + w * RB;
-      if (yb >= nyp) continue;  // wave-uniform
-      const int q0 = qa + kt * kz;
-      const int q1 = q0 + kz < qb ? q0 + kz : qb;
-      bool rv[RB];
-      int off[RB];
-      S prev[RB], cur[RB];
-      double cprv[RB], ccur[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        rv[r] = yb + r < nyp;
-        off[r] = (yb + r) * nx + x;
-        const bool ld = xin && rv[r];
-        prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + off[r]] : zero<S>();
-        cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
-        if constexpr (ANI) {
-          cprv[r] = (ld && z0 + q0 > 0) ? C[(q0 - 1) * P + off[r]] : 0.0;
-          ccur[r] = ld ? C[q0 * P + off[r]] : 0.0;
-        }
-      }
-      const bool bx = (x == 0) || (x == nx - 1);
-      for (int q = q0; q < q1; ++q) {
-        const int gq = z0 + q;
-        const bool bz = gq == 0 || gq == npl - 1;
-        const bool has_next = gq + 1 < npl;
-        S next[RB], lapv[RB];
-        double cnxt[RB];
-        int pv[RB];
-        bool okv[RB];
-#pragma unroll
+      // wave-uniform; guarded rather than skipped with continue, so the tile queue's
+      // barrier (tq_next) is reached from one point of uniform control flow
+      if (yb < nyp) {
+        const int q0 = qa + kt * kz;
+        const int q1 = q0 + kz < qb ? q0 + kz : qb;
+        bool rv[RB];
+        int off[RB];
+        S prev[RB], cur[RB];
+        double cprv[RB], ccur[RB];
+  #pragma unroll
         for (int r = 0; r < RB; ++r) {
-          const bool ld = xin && rv[r] && has_next;
-          next[r] = ld ? V[(q + 1) * P + off[r]] : zero<S>();
-          if constexpr (ANI) cnxt[r] = ld ? C[(q + 1) * P + off[r]] : 0.0;
-        }
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          pv[r] = q * P + off[r];
-          okv[r] = false;
-          lapv[r] = zero<S>();
-          if (!rv[r]) continue;  // wave-uniform
-          const int p = q * P + off[r];
-          const int y = yb + r;
-          const bool eym = gq > 0 || y > 0;            // idx - nx >= 0
-          const bool eyp = gq < npl - 1 || y < nyp - 1;  // idx + nx < N
-          const bool inner_yp = r + 1 < RB && rv[r + 1 < RB ? r + 1 : r];
-          S ym, yp;
-          if (r > 0) ym = cur[r - 1];
-          else ym = (xin && eym) ? V[p - nx] : zero<S>();
-          if (inner_yp) yp = cur[r + 1 < RB ? r + 1 : r];
-          else yp = (xin && eyp) ? V[p + nx] : zero<S>();
-          S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
-          const bool edge_ld = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin;
-          const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
-          if (lane == 0) xm = xe;
-          if (lane == 63) xp = xe;
-          if (!(x > 0)) xm = zero<S>();
-          if (!(x + 1 < nx)) xp = zero<S>();
-          S lap;
+          rv[r] = yb + r < nyp;
+          off[r] = (yb + r) * nx + x;
+          const bool ld = xin && rv[r];
+          prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + off[r]] : zero<S>();
+          cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
           if constexpr (ANI) {
-            const double cc = ccur[r];
-            double cym, cyp;
-            if (r > 0) cym = ccur[r - 1];
-            else cym = (xin && eym) ? C[p - nx] : 0.0;
-            if (inner_yp) cyp = ccur[r + 1 < RB ? r + 1 : r];
-            else cyp = (xin && eyp) ? C[p + nx] : 0.0;
-            double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
-            const double cxe = edge_ld ? C[p + (lane == 0 ? -1 : 1)] : 0.0;
-            if (lane == 0) cxm = cxe;
-            if (lane == 63) cxp = cxe;
-            const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
-            const double wym = face_w(eym, cc, cym), wyp = face_w(eyp, cc, cyp);
-            const double wzm = face_w(gq > 0, cc, cprv[r]), wzp = face_w(has_next, cc, cnxt[r]);
-            lap = g.s * ((((wzm * prev[r] + wzp * next[r]) + (wxm * xm + wxp * xp)) +
-                          (wym * ym + wyp * yp)) -
-                         (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * cur[r]);
-          } else {
-            const bool bnd = bx || bz || y == 0 || y == nyp - 1;
-            lap = g.s * (((prev[r] + next[r]) + (xm + xp)) + (ym + yp)) +
-                  (bnd ? g.sd_bd : g.sd_in) * cur[r];
-          }
-          if constexpr (PLANE) {
-            okv[r] = xin;
-            lapv[r] = lap;
-          } else {
-            if (xin) fn(p, cur[r], lap);
+            cprv[r] = (ld && z0 + q0 > 0) ? C[(q0 - 1) * P + off[r]] : 0.0;
+            ccur[r] = ld ? C[q0 * P + off[r]] : 0.0;
           }
         }
-        if constexpr (PLANE) fn(pv, cur, lapv, okv);
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          prev[r] = cur[r];
-          cur[r] = next[r];
-          if constexpr (ANI) {
-            cprv[r] = ccur[r];
-            ccur[r] = cnxt[r];
+        const bool bx = (x == 0) || (x == nx - 1);
+        for (int q = q0; q < q1; ++q) {
+          const int gq = z0 + q;
+          const bool bz = gq == 0 || gq == npl - 1;
+          const bool has_next = gq + 1 < npl;
+          S next[RB], lapv[RB];
+          double cnxt[RB];
+          int pv[RB];
+          bool okv[RB];
+  #pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const bool ld = xin && rv[r] && has_next;
+            next[r] = ld ? V[(q + 1) * P + off[r]] : zero<S>();
+            if constexpr (ANI) cnxt[r] = ld ? C[(q + 1) * P + off[r]] : 0.0;
+          }
+  #pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            pv[r] = q * P + off[r];
+            okv[r] = false;
+            lapv[r] = zero<S>();
+            if (!rv[r]) continue;  // wave-uniform
+            const int p = q * P + off[r];
+            const int y = yb + r;
+            const bool eym = gq > 0 || y > 0;            // idx - nx >= 0
+            const bool eyp = gq < npl - 1 || y < nyp - 1;  // idx + nx < N
+            const bool inner_yp = r + 1 < RB && rv[r + 1 < RB ? r + 1 : r];
+            S ym, yp;
+            if (r > 0) ym = cur[r - 1];
+            else ym = (xin && eym) ? V[p - nx] : zero<S>();
+            if (inner_yp) yp = cur[r + 1 < RB ? r + 1 : r];
+            else yp = (xin && eyp) ? V[p + nx] : zero<S>();
+            S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
+            const bool edge_ld = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin;
+            const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
+            if (lane == 0) xm = xe;
+            if (lane == 63) xp = xe;
+            if (!(x > 0)) xm = zero<S>();
+            if (!(x + 1 < nx)) xp = zero<S>();
+            S lap;
+            if constexpr (ANI) {
+              const double cc = ccur[r];
+              double cym, cyp;
+              if (r > 0) cym = ccur[r - 1];
+              else cym = (xin && eym) ? C[p - nx] : 0.0;
+              if (inner_yp) cyp = ccur[r + 1 < RB ? r + 1 : r];
+              else cyp = (xin && eyp) ? C[p + nx] : 0.0;
+              double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
+              const double cxe = edge_ld ? C[p + (lane == 0 ? -1 : 1)] : 0.0;
+              if (lane == 0) cxm = cxe;
+              if (lane == 63) cxp = cxe;
+              const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
+              const double wym = face_w(eym, cc, cym), wyp = face_w(eyp, cc, cyp);
+              const double wzm = face_w(gq > 0, cc, cprv[r]), wzp = face_w(has_next, cc, cnxt[r]);
+              lap = g.s * ((((wzm * prev[r] + wzp * next[r]) + (wxm * xm + wxp * xp)) +
+                            (wym * ym + wyp * yp)) -
+                           (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * cur[r]);
+            } else {
+              const bool bnd = bx || bz || y == 0 || y == nyp - 1;
+              lap = g.s * (((prev[r] + next[r]) + (xm + xp)) + (ym + yp)) +
+                    (bnd ? g.sd_bd : g.sd_in) * cur[r];
+            }
+            if constexpr (PLANE) {
+              okv[r] = xin;
+              lapv[r] = lap;
+            } else {
+              if (xin) fn(p, cur[r], lap);
+            }
+          }
+          if constexpr (PLANE) fn(pv, cur, lapv, okv);
+  #pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            prev[r] = cur[r];
+            cur[r] = next[r];
+            if constexpr (ANI) {
+              cprv[r] = ccur[r];
+              ccur[r] = cnxt[r];
+            }
           }
         }
       }
     } else {
       const int q0 = qa + (kt * 4 + w) * kz;
-      if (q0 >= qb) continue;  // wave-uniform
-      const int q1 = q0 + kz < qb ? q0 + kz : qb;
-      int xr[RB];
-      S prev[RB], cur[RB];
-      double cprv[RB], ccur[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        xr[r] = it * 64 * RB + 64 * r + lane;
-        const bool ld = xr[r] < nx;
-        prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + xr[r]] : zero<S>();
-        cur[r] = ld ? V[q0 * P + xr[r]] : zero<S>();
-        if constexpr (ANI) {
-          cprv[r] = (ld && z0 + q0 > 0) ? C[(q0 - 1) * P + xr[r]] : 0.0;
-          ccur[r] = ld ? C[q0 * P + xr[r]] : 0.0;
+      if (q0 < qb) {  // wave-uniform (see the 3D branch)
+        const int q1 = q0 + kz < qb ? q0 + kz : qb;
+        int xr[RB];
+        S prev[RB], cur[RB];
+        double cprv[RB], ccur[RB];
+  #pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          xr[r] = it * 64 * RB + 64 * r + lane;
+          const bool ld = xr[r] < nx;
+          prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + xr[r]] : zero<S>();
+          cur[r] = ld ? V[q0 * P + xr[r]] : zero<S>();
+          if constexpr (ANI) {
+            cprv[r] = (ld && z0 + q0 > 0) ? C[(q0 - 1) * P + xr[r]] : 0.0;
+            ccur[r] = ld ? C[q0 * P + xr[r]] : 0.0;
+          }
+        }
+        for (int q = q0; q < q1; ++q) {
+          const int gq = z0 + q;
+          const bool bz = gq == 0 || gq == npl - 1;
+          const bool has_next = gq + 1 < npl;
+          S next[RB], lapv[RB];
+          double cnxt[RB];
+          int pv[RB];
+          bool okv[RB];
+  #pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const bool ld = xr[r] < nx && has_next;
+            next[r] = ld ? V[(q + 1) * P + xr[r]] : zero<S>();
+            if constexpr (ANI) cnxt[r] = ld ? C[(q + 1) * P + xr[r]] : 0.0;
+          }
+  #pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const int x = xr[r];
+            const int p = q * P + x;
+            pv[r] = p;
+            S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
+            const S cm = bcast(cur[r > 0 ? r - 1 : 0], 63);
+            const S cp = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
+            const bool edge_ld = (lane == 0 && r == 0 && x < nx && x > 0) ||
+                                 (lane == 63 && r + 1 == RB && x + 1 < nx);
+            const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
+            if (lane == 0) xm = r > 0 ? cm : xe;
+            if (lane == 63) xp = r + 1 < RB ? cp : xe;
+            if (!(x > 0)) xm = zero<S>();
+            if (!(x + 1 < nx)) xp = zero<S>();
+            S lap;
+            if constexpr (ANI) {
+              const double cc = ccur[r];
+              double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
+              const double ccm = bcast(ccur[r > 0 ? r - 1 : 0], 63);
+              const double ccp = bcast(ccur[r + 1 < RB ? r + 1 : r], 0);
+              const double cxe = edge_ld ? C[p + (lane == 0 ? -1 : 1)] : 0.0;
+              if (lane == 0) cxm = r > 0 ? ccm : cxe;
+              if (lane == 63) cxp = r + 1 < RB ? ccp : cxe;
+              const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
+              const double wzm = face_w(gq > 0, cc, cprv[r]), wzp = face_w(has_next, cc, cnxt[r]);
+              lap = g.s * (((wzm * prev[r] + wzp * next[r]) + (wxm * xm + wxp * xp)) -
+                           ((wzm + wzp) + (wxm + wxp)) * cur[r]);
+            } else {
+              const bool bnd = x == 0 || x == nx - 1 || bz;
+              lap = g.s * ((prev[r] + next[r]) + (xm + xp)) + (bnd ? g.sd_bd : g.sd_in) * cur[r];
+            }
+            if constexpr (PLANE) {
+              okv[r] = x < nx;
+              lapv[r] = lap;
+            } else {
+              if (x < nx) fn(p, cur[r], lap);
+            }
+          }
+          if constexpr (PLANE) fn(pv, cur, lapv, okv);
+  #pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            prev[r] = cur[r];
+            cur[r] = next[r];
+            if constexpr (ANI) {
+              cprv[r] = ccur[r];
+              ccur[r] = cnxt[r];
+            }
+          }
         }
       }
-      for (int q = q0; q < q1; ++q) {
+    }
+  }
+  if (tq) tq_done(tq);
+}
+
+// The fused tail's 3D march with software pipelining (one row per wave).  Per plane the
+// tail reads the stencil vector and M-2 streamed vectors at every cell; with the loads
+// of a plane issued only when that plane is computed, each wave alternates between a
+// full memory latency and its arithmetic, and two waves per SIMD do not cover it.  Here
+// every load plane q+1 needs -- the stencil plane q+2, the y / x-edge neighbours of
+// plane q+1 and the streamed cells Ld(p, Buf) of plane q+1 -- is issued BEFORE plane q
+// is computed, into the second of two register buffers, so a wave keeps a plane of loads
+// in flight while it computes (the compiler counts the vmcnt of the older plane).  Loads
+// are unconditional: lanes past a ragged x tile load the row's last cell, ghost planes
+// (two per side) absorb the plane q+2 / y-wrap addresses, and zeros are selected after
+// the load, so no load sits behind an exec-masked branch.  Same operator and the same
+// arithmetic as march (laplacians.hpp:55-105 / 158-218): bitwise the same lap.
+// Fn(p, cur, lap, Buf &, ok): p the (clamped) local cell, ok = the lane's x is in the grid.
+template <class S, bool ANI, class Buf, class Ld, class Fn>
+__device__ __forceinline__ void march_pf(const S *__restrict__ V, const Geo &g, Ld &&ld, Fn &&fn) {
+  const double *__restrict__ C = g.cf;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t ntx64, nty64, ntz64;
+  tile_counts<3, 1>(g, ntx64, nty64, ntz64);
+  const int ntx = (int)ntx64, nty = (int)nty64;
+  const int tiles = (int)(ntx64 * nty64 * ntz64);
+  const int T8 = tiles / 8;
+  const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, qa = g.qa, qb = g.qb, kz = g.kz;
+  const int z0 = (int)g.z0, npl = (int)g.npl;
+  const double s = g.s, sdb = g.sd_bd, sdi = g.sd_in;
+  int32_t *const tq = g.tq;
+  for (int t0 = tq ? tq_next(tq) : (int)blockIdx.x; t0 < tiles; t0 = tq ? tq_next(tq) : t0 + (int)gridDim.x) {
+    const int t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
+    const int it = t % ntx, rest = t / ntx, jt = rest % nty, kt = rest / nty;
+    const int y = jt * 4 + w;
+    if (y < nyp) {  // wave-uniform; the tile queue's barrier stays outside, in uniform flow
+      const int x = it * 64 + lane;
+      const bool xin = x < nx;
+      const int xc = xin ? x : nx - 1;
+      const int off = y * nx + xc;
+      const int q0 = qa + kt * kz, q1 = q0 + kz < qb ? q0 + kz : qb;
+      // the x neighbour outside the wave: lane 0 reads x-1, lane 63 x+1 (else its own cell)
+      const int dxe = lane == 0 ? (x > 0 ? -1 : 0) : (lane == 63 && xc + 1 < nx ? 1 : 0);
+      const bool bxy = x == 0 || x == nx - 1 || y == 0 || y == nyp - 1;
+      // register queue: stencil planes q-1, q, q+1 (c field alike), neighbours of plane q
+      S prev = V[(q0 - 1) * P + off], cur = V[q0 * P + off], nxt = V[(q0 + 1) * P + off];
+      S ym = V[q0 * P + off - nx], yp = V[q0 * P + off + nx], xe = V[q0 * P + off + dxe];
+      double cprv = 0.0, ccur = 0.0, cnxt = 0.0, cym = 0.0, cyp = 0.0, cxe = 0.0;
+      if constexpr (ANI) {
+        cprv = C[(q0 - 1) * P + off];
+        ccur = C[q0 * P + off];
+        cnxt = C[(q0 + 1) * P + off];
+        cym = C[q0 * P + off - nx];
+        cyp = C[q0 * P + off + nx];
+        cxe = C[q0 * P + off + dxe];
+      }
+      Buf bA, bB;
+      ld(q0 * P + off, bA);
+      auto plane = [&](int q, Buf &bc, Buf &bn) {
+        const bool more = q + 1 < q1;  // uniform
+        S nn = zero<S>(), ym1 = zero<S>(), yp1 = zero<S>(), xe1 = zero<S>();
+        double cnn = 0.0, cym1 = 0.0, cyp1 = 0.0, cxe1 = 0.0;
+        if (more) {
+          const int p1 = (q + 1) * P + off;
+          nn = V[p1 + P];
+          ym1 = V[p1 - nx];
+          yp1 = V[p1 + nx];
+          xe1 = V[p1 + dxe];
+          if constexpr (ANI) {
+            cnn = C[p1 + P];
+            cym1 = C[p1 - nx];
+            cyp1 = C[p1 + nx];
+            cxe1 = C[p1 + dxe];
+          }
+          ld(p1, bn);
+        }
+        asm volatile("" ::: "memory");  // the prefetch stays ahead of the plane's arithmetic
         const int gq = z0 + q;
-        const bool bz = gq == 0 || gq == npl - 1;
-        const bool has_next = gq + 1 < npl;
-        S next[RB], lapv[RB];
-        double cnxt[RB];
-        int pv[RB];
-        bool okv[RB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const bool ld = xr[r] < nx && has_next;
-          next[r] = ld ? V[(q + 1) * P + xr[r]] : zero<S>();
-          if constexpr (ANI) cnxt[r] = ld ? C[(q + 1) * P + xr[r]] : 0.0;
+        const bool eym = gq > 0 || y > 0, eyp = gq < npl - 1 || y < nyp - 1;
+        const bool hasp = gq > 0, hasn = gq + 1 < npl;
+        const S zp = hasp ? prev : zero<S>(), zn = hasn ? nxt : zero<S>();
+        const S yv0 = eym ? ym : zero<S>(), yv1 = eyp ? yp : zero<S>();
+        S xm = shfl_up1(cur), xp = shfl_dn1(cur);
+        if (lane == 0) xm = xe;
+        if (lane == 63) xp = xe;
+        if (!(x > 0)) xm = zero<S>();
+        if (!(x + 1 < nx)) xp = zero<S>();
+        S lap;
+        if constexpr (ANI) {
+          const double cc = ccur;
+          double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
+          if (lane == 0) cxm = cxe;
+          if (lane == 63) cxp = cxe;
+          const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
+          const double wym = face_w(eym, cc, cym), wyp = face_w(eyp, cc, cyp);
+          const double wzm = face_w(hasp, cc, cprv), wzp = face_w(hasn, cc, cnxt);
+          lap = s * ((((wzm * zp + wzp * zn) + (wxm * xm + wxp * xp)) + (wym * yv0 + wyp * yv1)) -
+                     (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * cur);
+        } else {
+          const bool bnd = bxy || gq == 0 || gq == npl - 1;
+          lap = s * (((zp + zn) + (xm + xp)) + (yv0 + yv1)) + (bnd ? sdb : sdi) * cur;
         }
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const int x = xr[r];
-          const int p = q * P + x;
-          pv[r] = p;
-          S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
-          const S cm = bcast(cur[r > 0 ? r - 1 : 0], 63);
-          const S cp = bcast(cur[r + 1 < RB ? r + 1 : r], 0);
-          const bool edge_ld = (lane == 0 && r == 0 && x < nx && x > 0) ||
-                               (lane == 63 && r + 1 == RB && x + 1 < nx);
-          const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
-          if (lane == 0) xm = r > 0 ? cm : xe;
-          if (lane == 63) xp = r + 1 < RB ? cp : xe;
-          if (!(x > 0)) xm = zero<S>();
-          if (!(x + 1 < nx)) xp = zero<S>();
-          S lap;
-          if constexpr (ANI) {
-            const double cc = ccur[r];
-            double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
-            const double ccm = bcast(ccur[r > 0 ? r - 1 : 0], 63);
-            const double ccp = bcast(ccur[r + 1 < RB ? r + 1 : r], 0);
-            const double cxe = edge_ld ? C[p + (lane == 0 ? -1 : 1)] : 0.0;
-            if (lane == 0) cxm = r > 0 ? ccm : cxe;
-            if (lane == 63) cxp = r + 1 < RB ? ccp : cxe;
-            const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
-            const double wzm = face_w(gq > 0, cc, cprv[r]), wzp = face_w(has_next, cc, cnxt[r]);
-            lap = g.s * (((wzm * prev[r] + wzp * next[r]) + (wxm * xm + wxp * xp)) -
-                         ((wzm + wzp) + (wxm + wxp)) * cur[r]);
-          } else {
-            const bool bnd = x == 0 || x == nx - 1 || bz;
-            lap = g.s * ((prev[r] + next[r]) + (xm + xp)) + (bnd ? g.sd_bd : g.sd_in) * cur[r];
-          }
-          if constexpr (PLANE) {
-            okv[r] = x < nx;
-            lapv[r] = lap;
-          } else {
-            if (x < nx) fn(p, cur[r], lap);
-          }
+        fn(q * P + off, cur, lap, bc, xin);
+        prev = cur;
+        cur = nxt;
+        nxt = nn;
+        ym = ym1;
+        yp = yp1;
+        xe = xe1;
+        if constexpr (ANI) {
+          cprv = ccur;
+          ccur = cnxt;
+          cnxt = cnn;
+          cym = cym1;
+          cyp = cyp1;
+          cxe = cxe1;
         }
-        if constexpr (PLANE) fn(pv, cur, lapv, okv);
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          prev[r] = cur[r];
-          cur[r] = next[r];
-          if constexpr (ANI) {
-            cprv[r] = ccur[r];
-            ccur[r] = cnxt[r];
-          }
-        }
+      };
+      int q = q0;
+      for (; q + 1 < q1; q += 2) {  // two planes per trip: the buffers swap roles without copies
+        plane(q, bA, bB);
+        plane(q + 1, bB, bA);
       }
+      if (q < q1) plane(q, bA, bB);
     }
   }
   if (tq) tq_done(tq);
@@ -658,85 +786,115 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
   const double *__restrict__ W2 = static_cast<const double *>(ta.W2);
   const int64_t vs = ta.vs;
   const S *__restrict__ VJ = W + (int64_t)J * vs;
-  // one row per thread: with the epilogue at the end of the combination, two
-  // rows no longer fit in the 256 registers of two waves per SIMD
-  constexpr int RB = FUSED_RB;
-  march<S, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
-    S wk[RB][J];
-    double w2[RB][M2];
+  // the per-cell inputs besides the stencil vector: the J streamed basis vectors, the
+  // KG sinc^2 basis, and the epilogue's own reads (e0, e1 of the state type, d0 f64)
+  struct TBuf {
+    S wk[J];
+    double w2[M2];
+    S e0, e1;
+    double d0;
+  };
+  auto load = [&](int q, TBuf &b) {
+    const S *__restrict__ src = W + q;
 #pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const S *__restrict__ src = W + p[r];
+    for (int k = 0; k < J; ++k) {
+      b.wk[k] = ld_nt(src);
+      src += vs;
+    }
+    if constexpr (KG) {
+      const double *__restrict__ s2 = W2 + q;
 #pragma unroll
-      for (int k = 0; k < J; ++k) {
-        wk[r][k] = ok[r] ? ld_nt(src) : zero<S>();
-        src += vs;
-      }
-      if constexpr (KG) {
-        const double *__restrict__ s2 = W2 + p[r];
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-          w2[r][k] = ok[r] ? ld_nt(s2) : 0.0;
-          s2 += vs;
-        }
+      for (int k = 0; k < M; ++k) {
+        b.w2[k] = ld_nt(s2);
+        s2 += vs;
       }
     }
-    asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      if (!ok[r]) continue;
-      S y[NF];
-#pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        S acc = zero<S>();
-#pragma unroll
-        for (int k = 0; k < J; ++k) acc = acc + smul(cf[f][k], wk[r][k]);
-        acc = acc + smul(cf[f][J], cur[r]);
-        acc = acc + smul(cf[f][J + 1], lap[r]);
-        y[f] = acc;
-      }
-      const int q = p[r];
-      if constexpr (MODE == TAIL_NLSE) {
-        const double mv = ta.nonlin >= 2 ? ta.mf[q] : 0.0;
-        const cplx un = nl_half(to_c(y[0]), mv, ta.dt, ta.nonlin, ta.s1, ta.s2);
-        if (ta.u) st_nt(static_cast<cplx *>(ta.u) + q, un);  // NULL: another step follows
-        st_nt(reinterpret_cast<cplx *>(W) + q, nl_half(un, mv, ta.dt, ta.nonlin, ta.s1, ta.s2));
-      } else if constexpr (MODE == TAIL_SG_MID) {
-        double *__restrict__ up = static_cast<double *>(ta.up);
-        st_nt(static_cast<double *>(ta.out) + q, ta.mf[q] * (-sin_rl(to_c(y[0]).re)));
-        st_nt(up + q, 2 * to_c(y[1]).re - up[q]);
-      } else if constexpr (MODE == TAIL_GG_MID) {  // e.g. phi4_single.cuh:38-45
-        double *__restrict__ up = static_cast<double *>(ta.up);
-        st_nt(static_cast<double *>(ta.out) + q, -ta.mf[q] * gg_force(to_c(y[0]).re, ta.nonlin));
-        st_nt(up + q, 2 * to_c(y[1]).re - up[q]);
-      } else if constexpr (MODE == TAIL_SG_END) {
-        double *__restrict__ u = static_cast<double *>(ta.u);
-        double *__restrict__ up = static_cast<double *>(ta.up);
-        const double uo = u[q];
-        u[q] = up[q] + (ta.dt * ta.dt) * to_c(y[0]).re;
-        up[q] = uo;
-      } else if constexpr (MODE == TAIL_KG_END) {
-        double ys = 0.0;
-#pragma unroll
-        for (int k = 0; k < M2; ++k) ys += c2[k] * w2[r][k];
-        double *__restrict__ up = static_cast<double *>(ta.up);
-        const double uo = to_c(wk[r][0]).re;  // u is W_0 of the tail (cos) basis
-        const double un = (to_c(y[0]).re * 2.0 - up[q]) + ys * (ta.dt * ta.dt);
-        reinterpret_cast<double *>(W)[q] = un;
-        up[q] = uo;
-        static_cast<double *>(ta.v)[q] = (un - uo) / ta.dt;
-      } else if constexpr (MODE == TAIL_COMBINE_W0) {
-        W[q] = y[0];
-      } else if constexpr (MODE == TAIL_COMBINE) {
-        static_cast<S *>(ta.out)[q] = y[0];
-      } else {  // TAIL_SEWI_END
-        cplx *__restrict__ u = static_cast<cplx *>(ta.u);
-        const cplx uo = u[q];
-        u[q] = to_c(y[0]) - cmul({0.0, 2.0 * ta.dt}, static_cast<const cplx *>(ta.e)[q]);
-        static_cast<cplx *>(ta.up)[q] = uo;
-      }
+    b.e0 = b.e1 = zero<S>();
+    b.d0 = 0.0;
+    if constexpr (MODE == TAIL_NLSE) {
+      if (ta.nonlin >= 2) b.d0 = ta.mf[q];
+    } else if constexpr (MODE == TAIL_SG_MID || MODE == TAIL_GG_MID) {
+      b.d0 = ta.mf[q];
+      b.e0 = static_cast<const S *>(ta.up)[q];
+    } else if constexpr (MODE == TAIL_SG_END) {
+      b.e0 = static_cast<const S *>(ta.u)[q];
+      b.e1 = static_cast<const S *>(ta.up)[q];
+    } else if constexpr (MODE == TAIL_KG_END) {
+      b.e0 = static_cast<const S *>(ta.up)[q];
+    } else if constexpr (MODE == TAIL_SEWI_END) {
+      b.e0 = static_cast<const S *>(ta.u)[q];
+      b.e1 = static_cast<const S *>(ta.e)[q];
     }
-  });
+  };
+  // y_f = sum_k cf[f][k] W_k + cf[f][J+1] L W_J, then the step's epilogue at cell q
+  auto finish = [&](int q, const S &cur, const S &lap, const TBuf &b) {
+    S y[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      S acc = zero<S>();
+#pragma unroll
+      for (int k = 0; k < J; ++k) acc = acc + smul(cf[f][k], b.wk[k]);
+      acc = acc + smul(cf[f][J], cur);
+      acc = acc + smul(cf[f][J + 1], lap);
+      y[f] = acc;
+    }
+    if constexpr (MODE == TAIL_NLSE) {
+      const cplx un = nl_half(to_c(y[0]), b.d0, ta.dt, ta.nonlin, ta.s1, ta.s2);
+      if (ta.u) st_nt(static_cast<cplx *>(ta.u) + q, un);  // NULL: another step follows
+      st_nt(reinterpret_cast<cplx *>(W) + q, nl_half(un, b.d0, ta.dt, ta.nonlin, ta.s1, ta.s2));
+    } else if constexpr (MODE == TAIL_SG_MID) {
+      st_nt(static_cast<double *>(ta.out) + q, b.d0 * (-sin_rl(to_c(y[0]).re)));
+      st_nt(static_cast<double *>(ta.up) + q, 2 * to_c(y[1]).re - to_c(b.e0).re);
+    } else if constexpr (MODE == TAIL_GG_MID) {  // e.g. phi4_single.cuh:38-45
+      st_nt(static_cast<double *>(ta.out) + q, -b.d0 * gg_force(to_c(y[0]).re, ta.nonlin));
+      st_nt(static_cast<double *>(ta.up) + q, 2 * to_c(y[1]).re - to_c(b.e0).re);
+    } else if constexpr (MODE == TAIL_SG_END) {
+      const double uo = to_c(b.e0).re;
+      static_cast<double *>(ta.u)[q] = to_c(b.e1).re + (ta.dt * ta.dt) * to_c(y[0]).re;
+      static_cast<double *>(ta.up)[q] = uo;
+    } else if constexpr (MODE == TAIL_KG_END) {
+      double ys = 0.0;
+#pragma unroll
+      for (int k = 0; k < M2; ++k) ys += c2[k] * b.w2[k];
+      const double uo = to_c(b.wk[0]).re;  // u is W_0 of the tail (cos) basis
+      const double un = (to_c(y[0]).re * 2.0 - to_c(b.e0).re) + ys * (ta.dt * ta.dt);
+      reinterpret_cast<double *>(W)[q] = un;
+      static_cast<double *>(ta.up)[q] = uo;
+      static_cast<double *>(ta.v)[q] = (un - uo) / ta.dt;
+    } else if constexpr (MODE == TAIL_COMBINE_W0) {
+      W[q] = y[0];
+    } else if constexpr (MODE == TAIL_COMBINE) {
+      static_cast<S *>(ta.out)[q] = y[0];
+    } else {  // TAIL_SEWI_END
+      static_cast<cplx *>(ta.u)[q] = to_c(y[0]) - cmul({0.0, 2.0 * ta.dt}, to_c(b.e1));
+      static_cast<cplx *>(ta.up)[q] = to_c(b.e0);
+    }
+  };
+  // the pipelined 3D march holds two planes of streamed cells in registers: where they fit
+  // beside the epilogue at two waves per SIMD (<= 256 VGPRs: c128 J <= 14 isotropic, 12
+  // anisotropic; f64 J + M2 <= 18), else the plain march
+  constexpr bool PF = DIM == 3 && (std::is_same<S, cplx>::value ? J <= (ANI ? 12 : 14) : J + M2 <= 18);
+  if constexpr (PF) {
+    // software-pipelined march (march_pf): plane q+1's reads in flight while plane q computes
+    march_pf<S, ANI, TBuf>(VJ, g, load, [&](int q, const S &cur, const S &lap, const TBuf &b, bool ok) {
+      asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
+      if (ok) finish(q, cur, lap, b);
+    });
+  } else {
+    // one row per thread: with the epilogue at the end of the combination, two
+    // rows no longer fit in the 256 registers of two waves per SIMD
+    constexpr int RB = FUSED_RB;
+    march<S, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
+      TBuf b[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        if (ok[r]) load(p[r], b[r]);
+      asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        if (ok[r]) finish(p[r], cur[r], lap[r], b[r]);
+    });
+  }
 }
 
 #define NLS_J_LIST(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \

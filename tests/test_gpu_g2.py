@@ -59,7 +59,7 @@ def solver(dim, nx, ny, nz, dx, m, **kw):
 def set_form(monkeypatch, form):
     """Two-vector pass form of the G2 operator: "dma" (k_p2d with the c field staged
     beside S_J, nls_pass2a.hip; where the grid allows it), "reg" (the register form
-    k_p2g_lap + k_p2g, nls_pass2g.hpp) or "one" (one-vector passes)."""
+    k_lap + k_p2m, nls_pass2g.hpp) or "one" (one-vector passes)."""
     monkeypatch.setenv("NLS_PASS2", "0" if form == "one" else "1")
     monkeypatch.setenv("NLS_P2_REG", "1" if form == "reg" else "0")
 
@@ -258,6 +258,56 @@ def test_g2_slabs_match_single_rank(dim, n, nranks):
     grp.close()
     assert not err, err
     assert rel_l2(np.concatenate(out), ref) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("form", ["dma", "reg"])
+@pytest.mark.parametrize("dim,n,nranks", [(3, 16, 2), (3, 13, 3), (2, 40, 2)])
+def test_sewi_slabs_match_single_rank(monkeypatch, form, dim, n, nranks):
+    """sEWI (three Krylov actions per step on one basis, run_lanczos2 on collective
+    handles: two-plane halos, the basis re-warmed for each action) on 2-3 z-slabs of
+    the in-process group == the single-rank GPU run == the oracle.  3D n = 16 takes the
+    LDS-DMA pass (ny % 4 == 0), n = 13 and 2D the register form."""
+    set_form(monkeypatch, form)
+    m, dt, steps = 15, 1e-3, 4
+    dx = 8.0 / (n - 1)
+    u, mf, c = fields(dim, n, n, n, seed=12)
+    P = n * n if dim == 3 else n
+    g = O.grid(dim, n, n, n, dx, dx)
+    ref, _ = O.nlse_sewi_steps(g, c, mf, u, None, dt, 1, steps, m, bc=True)
+    with solver(dim, n, n, n, dx, m) as s1:
+        s1.set_coefficients(mf, c)
+        s1.set_field(u)
+        for i in range(1, steps + 1):
+            s1.step_sewi(dt, i)
+            s1.apply_bc()
+        one = s1.get_field()
+    grp = nls_amd.Group(nranks)
+    out = [None] * nranks
+    err = []
+
+    def work(r):
+        try:
+            s = solver(dim, n, n, n, dx, m, device=0, nranks=nranks, rank=r, group=grp)
+            sl = slice(s.z0 * P, (s.z0 + s.nzl) * P)
+            s.set_coefficients(mf[sl], c[sl])
+            s.set_field(u[sl])
+            for i in range(1, steps + 1):
+                s.step_sewi(dt, i)
+                s.apply_bc()
+            out[r] = s.get_field()
+            s.close()
+        except Exception as e:  # noqa: BLE001
+            err.append((r, e))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    grp.close()
+    assert not err, err
+    slabs = np.concatenate(out)
+    assert rel_l2(one, ref) <= TOL_TRAJ
+    assert rel_l2(slabs, ref) <= TOL_TRAJ
+    assert rel_l2(slabs, one) <= TOL_TRAJ
 
 
 @pytest.mark.parametrize("dim", [3, 2])

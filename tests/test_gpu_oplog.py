@@ -73,3 +73,30 @@ def test_oplog_off_by_default():
         s.set_field(field(n ** 3, 2))
         s.step(1e-3, 1)
         assert s.oplog() == []
+
+
+def test_oplog_partial_drain(monkeypatch):
+    """nls_debug_oplog with cap < n copies the oldest cap entries and keeps the rest:
+    the two reads of one step's log concatenate to the log of an identical step."""
+    import ctypes as C
+    monkeypatch.setenv("NLS_OPLOG", "1")
+    monkeypatch.setenv("NLS_FORCE_RCCL", "1")
+    n = 16
+    dx = 20.0 / (n - 1)
+    u = field(n ** 3, 5)
+    with nls_amd.Solver(3, n, n, n, dx, dx, m=8, device=0) as s:
+        s.set_field(u)
+        s.step(1e-3, 1)
+        s.sync()
+        full = s.oplog()
+        assert len(full) >= 4
+        s.set_field(u)
+        s.step(1e-3, 1)
+        s.sync()
+        L = nls_amd.lib()
+        cnt = C.c_uint64()
+        buf = (C.c_int32 * 8)()
+        assert L.nls_debug_oplog(s._h, buf, 2, C.byref(cnt)) == 0 and cnt.value == len(full)
+        first = [tuple(buf[4 * i:4 * i + 4]) for i in range(2)]
+        rest = s.oplog()
+        assert first + rest == full

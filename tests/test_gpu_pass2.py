@@ -27,7 +27,7 @@ def _pass2(monkeypatch):
 
 def _eligible(nx, ny, m):
     """Does the handle run the two-vector pass (nls_api.cpp alloc_all)?  k_p2d for
-    ny % 4 == 0 and m <= 18, the register form k_p2g (nls_pass2g.hpp) for the other
+    ny % 4 == 0 and m <= 18, the register form k_lap + k_p2m (nls_pass2g.hpp) for the other
     complex shapes up to m = 30."""
     return 3 <= m <= 30
 
@@ -103,7 +103,7 @@ def test_multi_step_call_equals_single_steps(eq):
 
 
 def _eligible2d(ny, m):
-    return 3 <= m <= 30  # k_p2d on planes of 4 rows (ny % 4 == 0, ny >= 8, m <= 18), else k_p2g
+    return 3 <= m <= 30  # k_p2d on planes of 4 rows (ny % 4 == 0, ny >= 8, m <= 18), else k_lap + k_p2m
 
 
 @pytest.mark.parametrize("nx,ny,m", [(64, 64, 16), (300, 20, 10), (50, 12, 16), (130, 8, 5), (70, 66, 16),

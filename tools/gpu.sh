@@ -73,6 +73,29 @@ for st in "$@"; do
         timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_$wl/p$i" -o run -- \
           python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/pmc_$wl/p$i.log" 2>&1 || exit $?
       done ;;
+    sq)
+      # issue / wait fractions and instruction counts per wave (8 SQ counters, one pass)
+      wl=${arg:-nlse3d_512}
+      mkdir -p "$OUT/sq_$wl"
+      echo "[gpu.sh] $(date +%T) sq $wl"
+      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/sq_$wl/p1" -o run -- \
+        python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/sq_$wl/p1.log" 2>&1 || exit $?
+      python3 tools/pmc_table.py "$OUT/sq_$wl" > "$OUT/sq_$wl.txt" && cat "$OUT/sq_$wl.txt" ;;
+    ab)
+      # same-box A/B: nonlinear-solvers_amd/lib_v0 (the reference build) against lib, two
+      # rounds interleaved, one bench process each -> ab_WL.txt (ms/step, dominant kernel ms)
+      wl=${arg:-nlse3d_512}
+      for rep in 1 2; do
+        for v in lib_v0 lib; do
+          NLS_AMD_LIB=$PWD/nonlinear-solvers_amd/$v/libnls_amd.so run 300 "$OUT/ab_${wl}_${v}_$rep.json" \
+            python bench.py --workload "$wl" --steps 10 --warmup 2 --no-cpu-baseline
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; k=d['step_roofline']['gpu_kernel_ms_per_step']; \
+print(f\"$v rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} dominant {r['avg_launch_ms']:.4f} ms frac {r['frac']:.3f} \
+\" + ' '.join(f'{a}:{b:.3f}' for a, b in k.items()))" "$OUT/ab_${wl}_${v}_$rep.json" \
+            | tee -a "$OUT/ab_$wl.txt"
+        done
+      done ;;
     py)
       script=${arg%%:*}
       args=""
