@@ -114,12 +114,11 @@ struct nls_handle {
   void *p2 = nullptr;          // P2State
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
+  int p2kz2 = 0, p2zbig = 0;   // k_p2d: the last chunks of kz2 planes after zbig chunks of p2kz (Geo::kz2)
+  int p2grid_alloc = 0;        // tiles the pass partial array holds (debug knobs may raise p2grid up to it)
   bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
   bool p2_split_on = true;     // collective handles: boundary/interior split (NLS_P2_SPLIT=0: off)
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
-  cplx *p2lbuf = nullptr;      // split passes: L S_J at the 8 planes around the slab's ends (k_p2b_lap)
-  int p2bgrid = 0;             // workgroups of the boundary-plane kernel k_p2b
-  bool p2b_dma = false;        // A/B (NLS_P2_BND=dma): boundary planes by k_p2d tiles of depth 2 instead
   // register form of the two-vector pass (k_lap + k_p2m, nls_pass2g.hpp): the G2
   // anisotropic NLSE and the isotropic shapes k_p2d does not take
   bool p2reg = false;
@@ -723,26 +722,25 @@ Geo p2_geo(const nls_handle *h) {
 }
 // tiles of one k_p2d launch over local planes [qa, qb) with tile depth kz: one
 // workgroup per 64 x 4-row tile column chunk
-int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz) {
+int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz, int kz2 = 0, int zbig = 0) {
   const Geo g = p2_geo(h);
-  const int64_t nzc = (qb - qa + kz - 1) / kz;
+  const int64_t nzc = p2_nchunks((int)(qb - qa), (int)kz, kz2, zbig);
   return (int)(((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * (g.nyp / P2D_ROWS) * nzc);
 }
 // Multi-rank handles (3D slabs of >= 8 planes) compute each pass's first two and
-// last two planes with the register-only boundary kernels k_p2b_lap + k_p2b on the
-// halo stream, followed there by the two-plane halo exchange of the new stencil
-// vector, while the interior planes run as k_p2d on the compute stream
-// (nls_pass2b.hpp).
+// last two planes first (k_p2d tiles of depth 2, one launch for both ends), then
+// exchange the new stencil vector's two boundary planes on the halo stream while
+// the interior planes run as k_p2d on the compute stream (run_lanczos2).
 bool p2_split(const nls_handle *h) {
   return h->collective && min_slab_planes(h) >= 8 && h->p2_split_on && !h->p2_d2 && !h->p2_pr && !h->p2reg &&
          !h->p2_ani;
 }
-int p2_bnd_tiles(const nls_handle *h) { return h->p2b_dma ? 2 * p2_tiles(h, 0, 2, 2) : h->p2bgrid; }
+int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
 int p2_grid(const nls_handle *h, int J = 0) {
   if (h->p2reg) return h->p2mgrid[J];
   const int64_t nzl = p2_geo(h).nzl;
-  if (!p2_split(h)) return p2_tiles(h, 0, nzl, h->p2kz);
-  return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, h->p2kz);
+  if (!p2_split(h)) return p2_tiles(h, 0, nzl, h->p2kz, h->p2kz2, h->p2zbig);
+  return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, h->p2kz, h->p2kz2, h->p2zbig);
 }
 
 // Two new vectors per pass (nls_pass2.hpp): the alpha pass + reduction of W_0
@@ -791,6 +789,8 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
   int64_t vs = h->p2_pr ? h->vs / 2 : h->vs;  // in the kernel's 16-B cells
   Geo g = p2_geo(h);
   g.kz = h->p2kz;
+  g.kz2 = h->p2kz2;
+  g.zbig = h->p2zbig;
   g.remap = h->p2order;
   cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(ps) + p2state_sums_offset());
   const bool split = p2_split(h);
@@ -820,44 +820,29 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
       launch(h, 1, J, fn, nb, args);
       if (h->collective) halo_begin(h, b, out);
     } else {
-      // the boundary planes [0, 2) and [nzl-2, nzl) by the register-only kernels on
-      // the halo stream, then the exchange of the new stencil vector's two boundary
-      // planes there, while the interior runs on the compute stream
+      // the boundary planes [0, 2) and [nzl-2, nzl) first, as k_p2d tiles of depth 2 in
+      // one grid (Geo::q2), on the compute stream; the exchange of the new stencil
+      // vector's two boundary planes then runs on the halo stream while the interior
+      // planes are computed.  The all-reduce waits for the exchange (halo_wait), which
+      // the interior has covered by then: one communicator, one stream at a time.
       const int64_t nzl = h->geo.nzl;
       const int tb = p2_bnd_tiles(h);
-      halo_after_compute(h);
-      if (h->p2b_dma) {  // A/B: k_p2d over both boundary plane pairs (Geo::q2)
-        Geo gb = g;
-        gb.kz = 2;
-        gb.qa = 0;
-        gb.qb = 2;
-        gb.q2 = (int32_t)(nzl - 2);
-        int poff = 0;
-        void *args[] = {&W, &vs, &gb, &ps, &h->partP2, &nb, &h->zbuf, &poff};
-        launch(h, 1, J, fn, tb, args, h->cstream);
-      } else {
-        void *SJ = vec_ptr(h, b, J);
-        Geo gb = h->geo;
-        int lg = (int)std::min<int64_t>(2048, (P2B_LPLANES_H * gb.P + NTHREADS - 1) / NTHREADS);
-        void *la[] = {&SJ, &gb, &h->p2lbuf};
-        launch(h, 1, J, kernel_p2b_lap(), lg, la, h->cstream);
-        int poff = 0;
-        void *args[] = {&W, &vs, &gb, &ps, &h->partP2, &nb, &h->p2lbuf, &poff};
-        launch(h, 1, J, kernel_p2b(J, ns == 2), tb, args, h->cstream);
-      }
-      hip_check(h, hipEventRecord(h->ev_bdone, h->cstream), "hipEventRecord");
-      halo_planes(h, vec_ptr(h, b, out), (int64_t)h->esize, h->cstream, 2);
-      hip_check(h, hipEventRecord(h->ev_halo, h->cstream), "hipEventRecord");
-      h->halo_pending = true;
+      Geo gb = g;
+      gb.kz = 2;
+      gb.kz2 = 0;
+      gb.qa = 0;
+      gb.qb = 2;
+      gb.q2 = (int32_t)(nzl - 2);
+      int poff = 0;
+      void *args[] = {&W, &vs, &gb, &ps, &h->partP2, &nb, &h->zbuf, &poff};
+      launch(h, 1, J, fn, tb, args);
+      halo_begin(h, b, out);
       Geo gi = g;
       gi.qa = 2;
       gi.qb = (int32_t)(nzl - 2);
-      int poff = tb;
-      void *args[] = {&W, &vs, &gi, &ps, &h->partP2, &nb, &h->zbuf, &poff};
-      launch(h, 1, J, fn, nb - tb, args);
-      // (the partials of the boundary launch; the exchange itself is awaited by
-      // the all-reduce / the next pass)
-      hip_check(h, hipStreamWaitEvent(h->stream, h->ev_bdone, 0), "hipStreamWaitEvent");
+      int poffi = tb;
+      void *argsi[] = {&W, &vs, &gi, &ps, &h->partP2, &nb, &h->zbuf, &poffi};
+      launch(h, 1, J, fn, nb - tb, argsi);
     }
     // columns: S-dots per new vector, the Gram's upper triangle, J = 0: ||S_0||^2
     const cplx *pA = nullptr;
@@ -995,7 +980,6 @@ void alloc_all(nls_handle *h) {
   // NLS_PASS2=0/1 forces it off / on where a pass form exists.
   h->pass2 = false;
   if (const char *e = std::getenv("NLS_P2_SPLIT")) h->p2_split_on = std::atoi(e) != 0;
-  if (const char *e = std::getenv("NLS_P2_BND")) h->p2b_dma = std::string(e) == "dma";
   {
     const char *e = std::getenv("NLS_PASS2");
     const bool want = e ? std::atoi(e) != 0 : true;
@@ -1060,12 +1044,6 @@ void alloc_all(nls_handle *h) {
         h->p2mgrid[J] = fm ? occupancy_grid(h, fm, stencil_tiles(gm, dim, p2m_rows_per_thread(J))) : 0;
       }
     }
-    if (p2_split(h)) {
-      // the boundary kernel: one thread per cell of the 4 planes, grid-stride over at
-      // most 1024 workgroups (their partial sums share the pass's partial array)
-      h->p2bgrid = (int)std::min<int64_t>(1024, (4 * g.P + NTHREADS - 1) / NTHREADS);
-      hip_check(h, hipMalloc(&h->p2lbuf, (size_t)P2B_LPLANES_H * g.P * sizeof(cplx)), "hipMalloc(p2lbuf)");
-    }
     const int64_t span = p2_split(h) ? gm.nzl - 4 : gm.nzl;
     h->p2kz = (int)std::max<int64_t>(std::min<int64_t>(16, span), std::min<int64_t>(256, (span + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
@@ -1078,7 +1056,8 @@ void alloc_all(nls_handle *h) {
       for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, h->p2mgrid[J]);
     hip_check(h, hipMalloc(&h->p2, p2state_bytes() * h->nbasis), "hipMalloc(p2)");  // one per basis
     hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes() * h->nbasis, h->stream), "hipMemset");
-    hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)),
+    h->p2grid_alloc = h->p2reg ? h->p2grid : 4 * h->p2grid;  // room for shorter tiles (knobs 4, 5)
+    hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid_alloc * (3 * MMAX + 8) * sizeof(cplx)),
               "hipMalloc(partP2)");
     const size_t zb = (size_t)std::max<int64_t>(g.nx, 64) * sizeof(cplx);
     hip_check(h, hipMalloc(&h->zbuf, zb), "hipMalloc(zbuf)");
@@ -1223,12 +1202,12 @@ void free_all(nls_handle *h) {
   }
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
                   (void *)h->vel, h->xedge, (void *)h->partX, h->p2, (void *)h->partP2,
-                  (void *)h->zbuf, (void *)h->p2lbuf, (void *)h->p2gbuf, (void *)h->partA, (void *)h->partU,
+                  (void *)h->zbuf, (void *)h->p2gbuf, (void *)h->partA, (void *)h->partU,
                   (void *)h->tailq})
     if (p) (void)hipFree(p);
   h->p2 = nullptr;
   h->tailq = nullptr;
-  h->partP2 = h->zbuf = h->p2lbuf = h->p2gbuf = nullptr;
+  h->partP2 = h->zbuf = h->p2gbuf = nullptr;
   h->u = h->scratch = h->snap = h->uprev = nullptr;
   h->up = h->mf = h->cfb = h->vel = nullptr;
   h->xedge = nullptr;
@@ -2085,6 +2064,13 @@ int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value) {
         if (h->fused_tail) tail_grids(h, h->tail_one_tile);
         break;
       case NLS_KNOB_P2_ORDER: h->p2order = value; break;
+      case NLS_KNOB_P2_KZ2:
+      case NLS_KNOB_P2_ZBIG:
+        if (h->collective) fail(h, NLS_ERR_STATE, "nls_debug_knob: k_p2d chunks on a single-rank handle only");
+        (knob == NLS_KNOB_P2_KZ2 ? h->p2kz2 : h->p2zbig) = std::max(0, (int)value);
+        h->p2grid = std::max(h->p2grid, p2_grid(h));
+        if (h->p2grid > h->p2grid_alloc) fail(h, NLS_ERR_ARG, "nls_debug_knob: more k_p2d tiles than allocated");
+        break;
       default: fail(h, NLS_ERR_ARG, "nls_debug_knob: unknown knob");
     }
   });

@@ -191,4 +191,28 @@ __device__ __forceinline__ cplx nl_half(cplx u, double mval, double dt, int nonl
   return cmul({er * cs, er * sn}, u);
 }
 
+// Both half steps of the fused tail's epilogue: u = N(y) and the next start vector
+// N(u) = N(N(y)).  For the unit-modulus phases (nonlin 0, 2, 3: rho depends on |u|
+// only and |N(y)| = |y|) N(N(y)) = y exp(2 i ph): the second phase comes from the
+// first by the double-angle identities instead of a second sin/cos evaluation (one
+// rounding away from applying N twice, far below every parity tolerance).  The
+// complex-sigma cubic-quintic (nonlin 1) changes |u| and applies N twice.
+__device__ __forceinline__ void nl_half2(cplx y, double mval, double dt, int nonlin, cplx s1, cplx s2, cplx &u,
+                                         cplx &u2) {
+  if (nonlin == 1) {
+    u = nl_half(y, mval, dt, nonlin, s1, s2);
+    u2 = nl_half(u, mval, dt, nonlin, s1, s2);
+    return;
+  }
+  const double d = y.re * y.re + y.im * y.im;
+  const double ph = nonlin == 3 ? (-0.5 * dt) * (mval * (s1.re * d + s2.re * (d * d)))
+                  : nonlin == 0 ? (-0.5 * dt) * d
+                                : (0.5 * dt) * (mval * d);
+  double sn, cs;
+  nl_sincos(ph, sn, cs);
+  u = {cs * y.re - sn * y.im, cs * y.im + sn * y.re};
+  const double c2 = fma(cs, cs, -sn * sn), s2n = 2.0 * sn * cs;
+  u2 = {c2 * y.re - s2n * y.im, c2 * y.im + s2n * y.re};
+}
+
 }  // namespace nls

@@ -27,7 +27,6 @@
 #include "nls_stencil.hpp"
 #include "nls_pass2.hpp"
 #include "nls_pass2d.hpp"
-#include "nls_pass2b.hpp"
 
 namespace nls {
 
@@ -842,17 +841,6 @@ static_assert(offsetof(P2State, bZ2) == offsetof(P2State, bZ1) + sizeof(cplx) &&
                   offsetof(P2State, bY2) == offsetof(P2State, bY1) + sizeof(cplx) &&
                   offsetof(P2State, bY3) == offsetof(P2State, bY2) + sizeof(cplx),
               "k_p2coef writes the b coefficients of a vector as an array");
-// boundary planes of a split multi-rank pass (nls_pass2b.hpp): 3D complex isotropic
-const void *kernel_p2b(int J, bool hz) {
-  switch (J) {
-#define X(J) \
-  case J: return hz ? reinterpret_cast<const void *>(&k_p2b<J, true>) : reinterpret_cast<const void *>(&k_p2b<J, false>);
-    X(0) X(2) X(4) X(6) X(8) X(10) X(12) X(14)
-#undef X
-    default: return nullptr;
-  }
-}
-const void *kernel_p2b_lap() { return reinterpret_cast<const void *>(&k_p2b_lap); }
 const void *kernel_p2tail() { return reinterpret_cast<const void *>(&k_p2tail); }
 const void *kernel_p2tfin() { return reinterpret_cast<const void *>(&k_p2tfin); }
 const void *kernel_p2coef() { return reinterpret_cast<const void *>(&k_p2coef); }

@@ -62,18 +62,12 @@ const void *kernel_colsum();
 //   pass2 : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* zbuf, int poff)
 const void *kernel_pass2(int J, bool hz, bool d2 = false, bool pr = false);  // hz: also Z (k_p2d)
 constexpr int P2D_WAVE_XO = 64, P2D_ROWS = 4, P2D_MAXJ = 14, P2D_MAXJ_A = 22;  // == P2D_XO, P2D_TR, P2D_JMAX, P2D_JMAX_A
-//   p2b_lap: (const cplx* S_J, Geo g, cplx* lbuf)  -- L S_J at the 8 planes around the slab's ends
-//   p2b    : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* lbuf, int poff)
-//            -- the slab's planes 0, 1, nzl-2, nzl-1 of k_p2d<J, hz> (nls_pass2b.hpp)
-const void *kernel_p2b(int J, bool hz);
 //   p2m    : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* lbuf, int poff)
 //            -- the register two-vector pass (nls_pass2g.hpp; lbuf = y = L S_J at local planes
 //            [-1, nzl], local plane 0 at lbuf + P, from k_lap); J even <= 28
 const void *kernel_p2m(int dim, int J, bool hz, bool ani);
 const void *kernel_pass2a(int J, bool hz);  // k_p2d of the G2 operator div(c grad) (3D, J <= P2D_MAXJ_A)
 int p2m_rows_per_thread(int J);
-const void *kernel_p2b_lap();
-constexpr int P2B_LPLANES_H = 8;  // == P2B_LPLANES: planes of the lbuf scratch
 //   p2tail: (P2State*, KState*, const cplx* sums, int m);  p2tfin: (const P2State*, KState*, int m, int nf)
 const void *kernel_p2tail();
 const void *kernel_p2tfin();

@@ -308,8 +308,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   const int nzl = (int)g.nzl, z0 = (int)g.z0;
   const int ntx = (nx + P2D_XO - 1) / P2D_XO, nty = ny / P2D_TR;
   const int qa = g.qa, qb = g.qb;
-  // z chunks of [qa, qb), and with g.q2 > 0 as many again of [q2, q2 + qb - qa)
-  const int nz1 = (qb - qa + g.kz - 1) / g.kz;
+  // z chunks of [qa, qb) (kz planes, the last ones kz2 with Geo::kz2), and with g.q2 > 0
+  // as many again of [q2, q2 + qb - qa)
+  const int nz1 = p2_nchunks(qb - qa, g.kz, g.kz2, g.zbig);
   const int nzc = g.q2 > 0 ? 2 * nz1 : nz1;
   const int ntiles = ntx * nty * nzc;
   // XCD-banded order: the 8 XCDs take contiguous tile ranges, so the y-adjacent
@@ -334,7 +335,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   const int x0 = xt * P2D_XO, y0 = yt * P2D_TR;
   const bool hi = g.q2 > 0 && zc >= nz1;  // uniform
   const int za = hi ? g.q2 : qa, zb = hi ? g.q2 + (qb - qa) : qb;
-  const int k0 = za + (hi ? zc - nz1 : zc) * g.kz, k1 = min(k0 + g.kz, zb);
+  int zoff, zlen;
+  p2_chunk(qb - qa, g.kz, g.kz2, g.zbig, hi ? zc - nz1 : zc, zoff, zlen);
+  const int k0 = za + zoff, k1 = min(k0 + zlen, zb);
   const int x = x0 + lane;
   const bool xin = x < nx;
   const bool full = x0 + P2D_XO <= nx;                    // uniform

@@ -426,10 +426,25 @@ constexpr int RB_ALPHA = 4;
 #define NLS_RB_L2 1  // measured at 512^3: RB 1 / kz 32 0.50 ms vs RB 4 / kz 8 0.58 ms (tools/exp_l2.sh)
 #endif
 constexpr int RB_L2 = NLS_RB_L2;  // rows per thread of k_alpha_l2
+#ifndef NLS_L2_PF
+#define NLS_L2_PF 1  // 3D k_alpha_l2 through the pipelined march (march_pf)
+#endif
 #ifndef NLS_FUSED_RB
 #define NLS_FUSED_RB 1
 #endif
 constexpr int FUSED_RB = NLS_FUSED_RB;  // rows per thread of k_tail
+#ifndef NLS_TAIL_PF
+#define NLS_TAIL_PF 1  // 3D tails through the software-pipelined march (march_pf)
+#endif
+#ifndef NLS_TAIL_NACC
+#define NLS_TAIL_NACC 4  // partial sums of the tail's combination (plain march)
+#endif
+#ifndef NLS_TAIL_NACC_PF
+#define NLS_TAIL_NACC_PF 2  // the same with the pipelined march (registers: two planes of loads)
+#endif
+#ifndef NLS_TAIL_OCC
+#define NLS_TAIL_OCC 2  // k_tail's __launch_bounds__ minimum waves per SIMD (2: <= 256 VGPRs)
+#endif
 
 // y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
 template <class S, int DIM, bool ANI>
@@ -727,11 +742,22 @@ template <class S, int DIM, bool ANI>
 __global__ __launch_bounds__(NTHREADS) void k_alpha_l2(const S *__restrict__ V, Geo g,
                                                        cplx *__restrict__ part) {
   double a = 0.0, n2 = 0.0, l2 = 0.0;
-  march<S, DIM, RB_L2, false, ANI>(V, g, [&](int, const S &c, const S &lap) {
+  auto acc = [&](const S &c, const S &lap) {
     a += to_c(cj_mul(c, lap)).re;
     n2 += abs2(c);
     l2 += abs2(lap);
-  });
+  };
+  if constexpr (DIM == 3 && RB_L2 == 1 && NLS_L2_PF) {
+    // the pipelined march (march_pf: the neighbours of plane q+1 and the stencil plane
+    // q+2 in flight while plane q is reduced); the same cells in the same order, so the
+    // same partial sums bit for bit
+    struct NoBuf {};
+    march_pf<S, ANI, NoBuf>(V, g, [](int, NoBuf &) {}, [&](int, const S &c, const S &lap, const NoBuf &, bool ok) {
+      if (ok) acc(c, lap);
+    });
+  } else {
+    march<S, DIM, RB_L2, false, ANI>(V, g, [&](int, const S &c, const S &lap) { acc(c, lap); });
+  }
   cplx v[3] = {{a, 0.0}, {n2, 0.0}, {l2, 0.0}};
   block_store<3>(v, part, gridDim.x, 0);
 }
@@ -759,7 +785,7 @@ __device__ __forceinline__ double sin_rl(double x) {
 }
 
 template <class S, int DIM, int M, bool ANI, int MODE>
-__global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
+__global__ __launch_bounds__(NTHREADS, NLS_TAIL_OCC) void k_tail(TailArgs ta, Geo g) {
   static_assert(M >= 3, "the stencil vector must not be W_0 (updated in place)");
   constexpr int J = M - 2;
   constexpr int NF = tail_nf(MODE);
@@ -794,6 +820,11 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
     S e0, e1;
     double d0;
   };
+  // the pipelined 3D march holds two planes of streamed cells in registers: where they fit
+  // beside the epilogue at two waves per SIMD (<= 256 VGPRs: c128 J <= 14 isotropic, 12
+  // anisotropic; f64 J + M2 <= 18), else the plain march
+  constexpr bool PF = NLS_TAIL_PF && DIM == 3 && (std::is_same<S, cplx>::value ? J <= (ANI ? 12 : 14) : J + M2 <= 18);
+  constexpr int NACC = PF ? NLS_TAIL_NACC_PF : NLS_TAIL_NACC;
   auto load = [&](int q, TBuf &b) {
     const S *__restrict__ src = W + q;
 #pragma unroll
@@ -826,22 +857,26 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
       b.e1 = static_cast<const S *>(ta.e)[q];
     }
   };
-  // y_f = sum_k cf[f][k] W_k + cf[f][J+1] L W_J, then the step's epilogue at cell q
+  // y_f = sum_k cf[f][k] W_k + cf[f][J+1] L W_J, then the step's epilogue at cell q.
+  // NACC partial sums (term k into sum k mod NACC): a single chain of 2(J+2) dependent
+  // f64 FMAs per component left the waves issue-stalled (SQ_WAIT_INST_ANY 0.55 of the
+  // wave cycles at 512^3, m = 16); shorter chains overlap
   auto finish = [&](int q, const S &cur, const S &lap, const TBuf &b) {
     S y[NF];
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      S acc = zero<S>();
+      S a4[4] = {zero<S>(), zero<S>(), zero<S>(), zero<S>()};
 #pragma unroll
-      for (int k = 0; k < J; ++k) acc = acc + smul(cf[f][k], b.wk[k]);
-      acc = acc + smul(cf[f][J], cur);
-      acc = acc + smul(cf[f][J + 1], lap);
-      y[f] = acc;
+      for (int k = 0; k < J; ++k) smac(a4[k % NACC], cf[f][k], b.wk[k]);
+      smac(a4[J % NACC], cf[f][J], cur);
+      smac(a4[(J + 1) % NACC], cf[f][J + 1], lap);
+      y[f] = NACC == 4 ? (a4[0] + a4[1]) + (a4[2] + a4[3]) : (NACC == 2 ? a4[0] + a4[1] : a4[0]);
     }
     if constexpr (MODE == TAIL_NLSE) {
-      const cplx un = nl_half(to_c(y[0]), b.d0, ta.dt, ta.nonlin, ta.s1, ta.s2);
+      cplx un, w0;
+      nl_half2(to_c(y[0]), b.d0, ta.dt, ta.nonlin, ta.s1, ta.s2, un, w0);  // u = N(y), W_0 = N(u)
       if (ta.u) st_nt(static_cast<cplx *>(ta.u) + q, un);  // NULL: another step follows
-      st_nt(reinterpret_cast<cplx *>(W) + q, nl_half(un, b.d0, ta.dt, ta.nonlin, ta.s1, ta.s2));
+      st_nt(reinterpret_cast<cplx *>(W) + q, w0);
     } else if constexpr (MODE == TAIL_SG_MID) {
       st_nt(static_cast<double *>(ta.out) + q, b.d0 * (-sin_rl(to_c(y[0]).re)));
       st_nt(static_cast<double *>(ta.up) + q, 2 * to_c(y[1]).re - to_c(b.e0).re);
@@ -870,10 +905,6 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
       static_cast<cplx *>(ta.up)[q] = to_c(b.e0);
     }
   };
-  // the pipelined 3D march holds two planes of streamed cells in registers: where they fit
-  // beside the epilogue at two waves per SIMD (<= 256 VGPRs: c128 J <= 14 isotropic, 12
-  // anisotropic; f64 J + M2 <= 18), else the plain march
-  constexpr bool PF = DIM == 3 && (std::is_same<S, cplx>::value ? J <= (ANI ? 12 : 14) : J + M2 <= 18);
   if constexpr (PF) {
     // software-pipelined march (march_pf): plane q+1's reads in flight while plane q computes
     march_pf<S, ANI, TBuf>(VJ, g, load, [&](int q, const S &cur, const S &lap, const TBuf &b, bool ok) {

@@ -143,13 +143,17 @@ def _ran_pass2(s, m):
     return cnt[0] > 0 and cnt[1] == 0  # s-step passes start at J = 0, 2, (5,) ... never at 1
 
 
+@pytest.mark.parametrize("split", ["1", "0"], ids=["split", "unsplit"])
 @pytest.mark.parametrize("nranks,m", [(4, 16), (3, 15), (2, 10)])
-def test_pass2_slabs_match_oracle(nranks, m):
+def test_pass2_slabs_match_oracle(monkeypatch, nranks, m, split):
     """The two-vector passes (k_p2d, the default for the 3D NLSE) on z slabs: two
     ghost planes per stored vector, two-plane halos of every stencil vector (incl.
     the 3D y-wrap across slab boundaries at the radius-2 march), all-reduced pass
     sums; uneven slabs (40 planes over 3 ranks) and an odd m (X-only last pass).
-    Spacing of the 512^3 bench (dx = 20/511): the stiff regime."""
+    Spacing of the 512^3 bench (dx = 20/511): the stiff regime.  split: the slabs'
+    boundary planes as their own k_p2d launch ahead of the interior (the default,
+    slabs of >= 8 planes) or one launch per pass (NLS_P2_SPLIT=0)."""
+    monkeypatch.setenv("NLS_P2_SPLIT", split)
     nx, ny, nz = 64, 24, 40
     dx = 20.0 / 511
     P = nx * ny

@@ -83,11 +83,12 @@ for st in "$@"; do
         python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/sq_$wl/p1.log" 2>&1 || exit $?
       python3 tools/pmc_table.py "$OUT/sq_$wl" > "$OUT/sq_$wl.txt" && cat "$OUT/sq_$wl.txt" ;;
     ab)
-      # same-box A/B: nonlinear-solvers_amd/lib_v0 (the reference build) against lib, two
+      # same-box A/B: every variant build nonlinear-solvers_amd/lib_v*/ against lib, two
       # rounds interleaved, one bench process each -> ab_WL.txt (ms/step, dominant kernel ms)
       wl=${arg:-nlse3d_512}
+      vars=$(cd nonlinear-solvers_amd && ls -d lib_v* 2>/dev/null | tr '\n' ' ')
       for rep in 1 2; do
-        for v in lib_v0 lib; do
+        for v in $vars lib; do
           NLS_AMD_LIB=$PWD/nonlinear-solvers_amd/$v/libnls_amd.so run 300 "$OUT/ab_${wl}_${v}_$rep.json" \
             python bench.py --workload "$wl" --steps 10 --warmup 2 --no-cpu-baseline
           python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; k=d['step_roofline']['gpu_kernel_ms_per_step']; \
@@ -96,6 +97,14 @@ print(f\"$v rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} domina
             | tee -a "$OUT/ab_$wl.txt"
         done
       done ;;
+    probe6)
+      # pure-stream rates of the tail / pass access patterns (tools/bw_probe6.hip, prebuilt)
+      run 300 "$OUT/bw_probe6_512.txt" tools/bw_probe6
+      cat "$OUT/bw_probe6_512.txt" ;;
+    slab)
+      # per-rank cost of the 8-GPU slabs on one GPU (tools/slab_probe.py)
+      run 600 "$OUT/slab_probe.txt" python -u tools/slab_probe.py
+      cat "$OUT/slab_probe.txt" ;;
     py)
       script=${arg%%:*}
       args=""

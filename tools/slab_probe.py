@@ -40,20 +40,14 @@ print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} kz={os.environ.g
 
 # (nz, extra environment): the tile depth follows the slab's own plane count (its
 # interior on split collective handles), the same as an N-rank handle of 512^3
-# computes it; NLS_P2_KZ pins it, NLS_P2_SPLIT=0 drops the boundary/interior split
-VARIANTS = [
-    (64, {}), (64, {"NLS_P2_KZ": "64"}),
-    (64, {"NLS_FORCE_RCCL": "1"}), (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "60"}),
-    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "60", "NLS_P2_BND": "dma"}),
-    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_KZ": "64", "NLS_P2_SPLIT": "0"}),
+# computes it; NLS_P2_SPLIT=0 drops the boundary/interior split (the exchange would
+# then follow each pass).  Two interleaved rounds: separate processes differ by a few
+# per cent from the placement of their allocations.
+BASE = [
+    (64, {}), (64, {"NLS_FORCE_RCCL": "1"}), (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_SPLIT": "0"}),
     (128, {}), (128, {"NLS_FORCE_RCCL": "1"}),
-    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_GRID": "256", "NLS_P2B_LGRID": "512"}),
-    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_GRID": "128", "NLS_P2B_LGRID": "256"}),
-    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_GRID": "512", "NLS_P2B_LGRID": "1024"}),
-    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_LATE": "1"}),
-    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_LATE": "1", "NLS_P2B_GRID": "256", "NLS_P2B_LGRID": "256"}),
-    (64, {"NLS_FORCE_RCCL": "1", "NLS_P2B_INLINE": "1"}),
 ]
+VARIANTS = BASE + BASE
 if len(sys.argv) > 1:  # a subset: python tools/slab_probe.py 0 2 3
     VARIANTS = [VARIANTS[int(i)] for i in sys.argv[1:]]
 for nz, extra in VARIANTS:
