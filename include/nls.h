@@ -278,9 +278,7 @@ int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n);
 enum nls_knob {
   NLS_KNOB_TAIL_DYN = 1,  /* fused tail through the dynamic tile queue (NLS_TAIL_DYN) */
   NLS_KNOB_KZ_FUSED = 2,  /* fused tail tile depth (NLS_KZ_FUSED; 0 = the stencil depth) */
-  NLS_KNOB_P2_ORDER = 3,  /* k_p2d tile order bits */
-  NLS_KNOB_P2_KZ2 = 4,    /* k_p2d: planes of the last tiles (0: one depth throughout) */
-  NLS_KNOB_P2_ZBIG = 5    /* k_p2d: chunks of the full depth before them */
+  NLS_KNOB_P2_ORDER = 3   /* k_p2d tile order bits */
 };
 int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value);
 

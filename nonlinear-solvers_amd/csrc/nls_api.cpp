@@ -114,8 +114,6 @@ struct nls_handle {
   void *p2 = nullptr;          // P2State
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
-  int p2kz2 = 0, p2zbig = 0;   // k_p2d: the last chunks of kz2 planes after zbig chunks of p2kz (Geo::kz2)
-  int p2grid_alloc = 0;        // tiles the pass partial array holds (debug knobs may raise p2grid up to it)
   bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
   bool p2_split_on = true;     // collective handles: boundary/interior split (NLS_P2_SPLIT=0: off)
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
@@ -722,9 +720,9 @@ Geo p2_geo(const nls_handle *h) {
 }
 // tiles of one k_p2d launch over local planes [qa, qb) with tile depth kz: one
 // workgroup per 64 x 4-row tile column chunk
-int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz, int kz2 = 0, int zbig = 0) {
+int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz) {
   const Geo g = p2_geo(h);
-  const int64_t nzc = p2_nchunks((int)(qb - qa), (int)kz, kz2, zbig);
+  const int64_t nzc = (qb - qa + kz - 1) / kz;
   return (int)(((g.nx + P2D_WAVE_XO - 1) / P2D_WAVE_XO) * (g.nyp / P2D_ROWS) * nzc);
 }
 // Multi-rank handles (3D slabs of >= 8 planes) compute each pass's first two and
@@ -739,8 +737,8 @@ int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
 int p2_grid(const nls_handle *h, int J = 0) {
   if (h->p2reg) return h->p2mgrid[J];
   const int64_t nzl = p2_geo(h).nzl;
-  if (!p2_split(h)) return p2_tiles(h, 0, nzl, h->p2kz, h->p2kz2, h->p2zbig);
-  return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, h->p2kz, h->p2kz2, h->p2zbig);
+  if (!p2_split(h)) return p2_tiles(h, 0, nzl, h->p2kz);
+  return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, h->p2kz);
 }
 
 // Two new vectors per pass (nls_pass2.hpp): the alpha pass + reduction of W_0
@@ -789,8 +787,6 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
   int64_t vs = h->p2_pr ? h->vs / 2 : h->vs;  // in the kernel's 16-B cells
   Geo g = p2_geo(h);
   g.kz = h->p2kz;
-  g.kz2 = h->p2kz2;
-  g.zbig = h->p2zbig;
   g.remap = h->p2order;
   cplx *sums = reinterpret_cast<cplx *>(static_cast<char *>(ps) + p2state_sums_offset());
   const bool split = p2_split(h);
@@ -829,7 +825,6 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
       const int tb = p2_bnd_tiles(h);
       Geo gb = g;
       gb.kz = 2;
-      gb.kz2 = 0;
       gb.qa = 0;
       gb.qb = 2;
       gb.q2 = (int32_t)(nzl - 2);
@@ -1056,8 +1051,7 @@ void alloc_all(nls_handle *h) {
       for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, h->p2mgrid[J]);
     hip_check(h, hipMalloc(&h->p2, p2state_bytes() * h->nbasis), "hipMalloc(p2)");  // one per basis
     hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes() * h->nbasis, h->stream), "hipMemset");
-    h->p2grid_alloc = h->p2reg ? h->p2grid : 4 * h->p2grid;  // room for shorter tiles (knobs 4, 5)
-    hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid_alloc * (3 * MMAX + 8) * sizeof(cplx)),
+    hip_check(h, hipMalloc(&h->partP2, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)),
               "hipMalloc(partP2)");
     const size_t zb = (size_t)std::max<int64_t>(g.nx, 64) * sizeof(cplx);
     hip_check(h, hipMalloc(&h->zbuf, zb), "hipMalloc(zbuf)");
@@ -1086,7 +1080,9 @@ void alloc_all(nls_handle *h) {
     // rounds); not the real 2D Gautschi tails (SG 8192^2: 2.53 -> 2.55) nor small 3D slabs
     // (G2 256^3: 1.23-1.31 -> 1.26-1.36)
     h->tail_dyn = (one_tile && dim == 3) || (dim == 2 && c);
-    if (h->tail_dyn && dim == 3) h->kz_fused = 16;
+    // 8-plane queue tiles in 3D (512^3 m = 16, one handle, three interleaved rounds:
+    // 5.77 ms against 5.86 with 16 planes and 5.95 with 4, profiles/r04/knob_ab_512.txt)
+    if (h->tail_dyn && dim == 3) h->kz_fused = 8;
     // the dynamic tile queue of the tail (nls_stencil.hpp tq_next): two counters, zero
     // between launches (the last workgroup of each launch resets them)
     hip_check(h, hipMalloc(&h->tailq, 2 * sizeof(int32_t)), "hipMalloc(tailq)");
@@ -2064,13 +2060,6 @@ int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value) {
         if (h->fused_tail) tail_grids(h, h->tail_one_tile);
         break;
       case NLS_KNOB_P2_ORDER: h->p2order = value; break;
-      case NLS_KNOB_P2_KZ2:
-      case NLS_KNOB_P2_ZBIG:
-        if (h->collective) fail(h, NLS_ERR_STATE, "nls_debug_knob: k_p2d chunks on a single-rank handle only");
-        (knob == NLS_KNOB_P2_KZ2 ? h->p2kz2 : h->p2zbig) = std::max(0, (int)value);
-        h->p2grid = std::max(h->p2grid, p2_grid(h));
-        if (h->p2grid > h->p2grid_alloc) fail(h, NLS_ERR_ARG, "nls_debug_knob: more k_p2d tiles than allocated");
-        break;
       default: fail(h, NLS_ERR_ARG, "nls_debug_knob: unknown knob");
     }
   });

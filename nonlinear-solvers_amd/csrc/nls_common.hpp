@@ -197,9 +197,12 @@ __device__ __forceinline__ cplx nl_half(cplx u, double mval, double dt, int nonl
 // first by the double-angle identities instead of a second sin/cos evaluation (one
 // rounding away from applying N twice, far below every parity tolerance).  The
 // complex-sigma cubic-quintic (nonlin 1) changes |u| and applies N twice.
+#ifndef NLS_NL_HALF2
+#define NLS_NL_HALF2 1
+#endif
 __device__ __forceinline__ void nl_half2(cplx y, double mval, double dt, int nonlin, cplx s1, cplx s2, cplx &u,
                                          cplx &u2) {
-  if (nonlin == 1) {
+  if (nonlin == 1 || !NLS_NL_HALF2) {
     u = nl_half(y, mval, dt, nonlin, s1, s2);
     u2 = nl_half(u, mval, dt, nonlin, s1, s2);
     return;

@@ -76,26 +76,7 @@ struct Geo {
                      // done; both back to 0 when the launch ends), else a static tile stride
   const double *cf;  // G2 anisotropic operator: c field at local plane 0 (ghost planes at
                      // -P and nzl*P, like a basis vector); unused by the isotropic operator
-  int32_t kz2;       // k_p2d only: > 0 -- after the first zbig chunks of kz planes, the rest
-  int32_t zbig;      //   of the range in chunks of kz2 (short tiles last: the launch's end
-                     //   waits on one short tile instead of one long one); 0: kz throughout
 };
-
-// z chunks of a k_p2d plane range of `span` planes (Geo kz / kz2 / zbig)
-__host__ __device__ inline int p2_nchunks(int span, int kz, int kz2, int zbig) {
-  if (kz2 <= 0 || zbig * kz >= span) return (span + kz - 1) / kz;
-  return zbig + (span - zbig * kz + kz2 - 1) / kz2;
-}
-__host__ __device__ inline void p2_chunk(int span, int kz, int kz2, int zbig, int zc, int &off, int &len) {
-  if (kz2 <= 0 || zbig * kz >= span || zc < zbig) {
-    off = zc * kz;
-    len = kz;
-  } else {
-    off = zbig * kz + (zc - zbig) * kz2;
-    len = kz2;
-  }
-  if (len > span - off) len = span - off;
-}
 
 // Device-resident Lanczos state of one Krylov basis (no host round trip in
 // the j-loop; the reference reads every dot back to the host,

@@ -73,6 +73,9 @@ constexpr int P2D_CSB = P2D_SR * P2D_CRB + P2D_SR * 32;
 #ifndef NLS_P2D_NP_MAX
 #define NLS_P2D_NP_MAX 5      // J-ring depth cap in planes
 #endif
+#ifndef NLS_P2D_PRE_LA
+#define NLS_P2D_PRE_LA 1      // issue the look-ahead before the prologue's wait (p2d_dspre)
+#endif
 // Workgroups per CU: two where the registers (<= 256 per lane) and the rings
 // (<= 80 KiB) allow, so the second workgroup's waves cover the first's barriers
 // and LDS latencies; one for the long passes.
@@ -147,11 +150,21 @@ static_assert(p2d_rings_ok(0, true) && p2d_rings_ok(2, true) && p2d_rings_ok(4, 
 // (early) or after it, the late J group k+1 after the J rows are read, then the STW
 // stores.  Step i needs S(k+2) and J plane k.
 __host__ __device__ constexpr int p2d_nsd(bool A) { return A ? 6 : 4; }
+// look-ahead S groups issued, with the J groups, before the prologue's wait (their slots
+// (4 + d) % NSL are clear of the prologue's slots 0..3: the one-workgroup-per-CU passes
+// with early issue); 0: every look-ahead group after the wait, S before J (the round-3
+// order; also the order with NLS_P2D_PRE_LA = 0)
+__host__ __device__ constexpr int p2d_dspre(int J, bool A = false) {
+  return NLS_P2D_PRE_LA ? (p2d_ds(J, A) < p2d_nsl(J, A) - 4 ? p2d_ds(J, A) : p2d_nsl(J, A) - 4) : 0;
+}
 __host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = false) {
   const int DS = p2d_ds(J, A), NP = p2d_np(J, A), NSD = p2d_nsd(A);
   const bool early = p2d_early(J, A), late = p2d_late(J, A);
+  // the issue order ahead of the loop: [S groups d < DSPRE][J groups][S groups d >= DSPRE]
+  // (DSPRE = 0: every S group first, as the round-3 kernel issued them)
+  const int dspre = p2d_dspre(J, A) > 0 ? p2d_dspre(J, A) : DS;
   int n = 0, lastS = 0, lastJ = 0;
-  for (int d = 0; d < DS; ++d) {
+  for (int d = 0; d < dspre; ++d) {
     n += NSD;
     if (d == i) lastS = n;
   }
@@ -161,6 +174,10 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = fals
       n += J;
       if (d == i) lastJ = n;
     }
+  }
+  for (int d = dspre; d < DS; ++d) {
+    n += NSD;
+    if (d == i) lastS = n;
   }
   for (int s = 0;; ++s) {
     if (early) {
@@ -308,9 +325,8 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   const int nzl = (int)g.nzl, z0 = (int)g.z0;
   const int ntx = (nx + P2D_XO - 1) / P2D_XO, nty = ny / P2D_TR;
   const int qa = g.qa, qb = g.qb;
-  // z chunks of [qa, qb) (kz planes, the last ones kz2 with Geo::kz2), and with g.q2 > 0
-  // as many again of [q2, q2 + qb - qa)
-  const int nz1 = p2_nchunks(qb - qa, g.kz, g.kz2, g.zbig);
+  // z chunks of [qa, qb), and with g.q2 > 0 as many again of [q2, q2 + qb - qa)
+  const int nz1 = (qb - qa + g.kz - 1) / g.kz;
   const int nzc = g.q2 > 0 ? 2 * nz1 : nz1;
   const int ntiles = ntx * nty * nzc;
   // XCD-banded order: the 8 XCDs take contiguous tile ranges, so the y-adjacent
@@ -335,9 +351,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   const int x0 = xt * P2D_XO, y0 = yt * P2D_TR;
   const bool hi = g.q2 > 0 && zc >= nz1;  // uniform
   const int za = hi ? g.q2 : qa, zb = hi ? g.q2 + (qb - qa) : qb;
-  int zoff, zlen;
-  p2_chunk(qb - qa, g.kz, g.kz2, g.zbig, hi ? zc - nz1 : zc, zoff, zlen);
-  const int k0 = za + zoff, k1 = min(k0 + zlen, zb);
+  const int k0 = za + (hi ? zc - nz1 : zc) * g.kz, k1 = min(k0 + g.kz, zb);
   const int x = x0 + lane;
   const bool xin = x < nx;
   const bool full = x0 + P2D_XO <= nx;                    // uniform
@@ -509,7 +523,21 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   // register) and k0 (own row + halo values; L ring slot 0); then the look-ahead
   // S planes and J planes
   for (int p = k0 - 2; p <= k0 + 1; ++p) P2D_ISSUE_S(p, p - k0 + 2);
-  wait_vm<0>();
+  // the look-ahead S planes whose ring slots are clear of the prologue's, and the J
+  // planes, go out before the prologue's wait (p2d_dspre): a tile then starts after
+  // one memory latency, not two
+  constexpr int DSPRE = p2d_dspre(J, A), PJ = J == 0 ? 0 : (LATE ? 1 : NP - 1);
+#pragma unroll
+  for (int d = 0; d < DSPRE; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
+  if constexpr (DSPRE > 0) {
+    if constexpr (LATE) {
+      P2D_ISSUE_J(k0, 0);
+    } else if constexpr (J > 0) {
+#pragma unroll
+      for (int d = 0; d + 1 < NP; ++d) P2D_ISSUE_J(k0 + d, d);
+    }
+  }
+  wait_vm<DSPRE * p2d_nsd(A) + (DSPRE > 0 ? PJ * J : 0)>();
   raw_barrier();
   cplx lq0, lq1, le1;  // L S_J of planes k-1 and k (own row), halo values of plane k
   P2D_LAP(lq0, k0 - 1, w + 2, 0, 1, 2, x, lane, mi, pi);
@@ -519,12 +547,14 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   P2D_LROWS(k0, 1, 2, 3, 0, lq1, le1);
   raw_barrier();  // L ring slot 0 published; every wave is done with S slot 0 (plane k0-2)
 #pragma unroll
-  for (int d = 0; d < DS; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
-  if constexpr (LATE) {
-    P2D_ISSUE_J(k0, 0);
-  } else if constexpr (J > 0) {
+  for (int d = DSPRE; d < DS; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
+  if constexpr (DSPRE == 0) {
+    if constexpr (LATE) {
+      P2D_ISSUE_J(k0, 0);
+    } else if constexpr (J > 0) {
 #pragma unroll
-    for (int d = 0; d + 1 < NP; ++d) P2D_ISSUE_J(k0 + d, d);
+      for (int d = 0; d + 1 < NP; ++d) P2D_ISSUE_J(k0 + d, d);
+    }
   }
   // ring slots as running counters (no divisions in the loop)
   int sk = 2;                  // S slot of plane k (k+1, k+2 follow cyclically)

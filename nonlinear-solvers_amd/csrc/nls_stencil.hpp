@@ -272,130 +272,6 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
   if (tq) tq_done(tq);
 }
 
-// The fused tail's 3D march with software pipelining (one row per wave).  Per plane the
-// tail reads the stencil vector and M-2 streamed vectors at every cell; with the loads
-// of a plane issued only when that plane is computed, each wave alternates between a
-// full memory latency and its arithmetic, and two waves per SIMD do not cover it.  Here
-// every load plane q+1 needs -- the stencil plane q+2, the y / x-edge neighbours of
-// plane q+1 and the streamed cells Ld(p, Buf) of plane q+1 -- is issued BEFORE plane q
-// is computed, into the second of two register buffers, so a wave keeps a plane of loads
-// in flight while it computes (the compiler counts the vmcnt of the older plane).  Loads
-// are unconditional: lanes past a ragged x tile load the row's last cell, ghost planes
-// (two per side) absorb the plane q+2 / y-wrap addresses, and zeros are selected after
-// the load, so no load sits behind an exec-masked branch.  Same operator and the same
-// arithmetic as march (laplacians.hpp:55-105 / 158-218): bitwise the same lap.
-// Fn(p, cur, lap, Buf &, ok): p the (clamped) local cell, ok = the lane's x is in the grid.
-template <class S, bool ANI, class Buf, class Ld, class Fn>
-__device__ __forceinline__ void march_pf(const S *__restrict__ V, const Geo &g, Ld &&ld, Fn &&fn) {
-  const double *__restrict__ C = g.cf;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int64_t ntx64, nty64, ntz64;
-  tile_counts<3, 1>(g, ntx64, nty64, ntz64);
-  const int ntx = (int)ntx64, nty = (int)nty64;
-  const int tiles = (int)(ntx64 * nty64 * ntz64);
-  const int T8 = tiles / 8;
-  const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, qa = g.qa, qb = g.qb, kz = g.kz;
-  const int z0 = (int)g.z0, npl = (int)g.npl;
-  const double s = g.s, sdb = g.sd_bd, sdi = g.sd_in;
-  int32_t *const tq = g.tq;
-  for (int t0 = tq ? tq_next(tq) : (int)blockIdx.x; t0 < tiles; t0 = tq ? tq_next(tq) : t0 + (int)gridDim.x) {
-    const int t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
-    const int it = t % ntx, rest = t / ntx, jt = rest % nty, kt = rest / nty;
-    const int y = jt * 4 + w;
-    if (y < nyp) {  // wave-uniform; the tile queue's barrier stays outside, in uniform flow
-      const int x = it * 64 + lane;
-      const bool xin = x < nx;
-      const int xc = xin ? x : nx - 1;
-      const int off = y * nx + xc;
-      const int q0 = qa + kt * kz, q1 = q0 + kz < qb ? q0 + kz : qb;
-      // the x neighbour outside the wave: lane 0 reads x-1, lane 63 x+1 (else its own cell)
-      const int dxe = lane == 0 ? (x > 0 ? -1 : 0) : (lane == 63 && xc + 1 < nx ? 1 : 0);
-      const bool bxy = x == 0 || x == nx - 1 || y == 0 || y == nyp - 1;
-      // register queue: stencil planes q-1, q, q+1 (c field alike), neighbours of plane q
-      S prev = V[(q0 - 1) * P + off], cur = V[q0 * P + off], nxt = V[(q0 + 1) * P + off];
-      S ym = V[q0 * P + off - nx], yp = V[q0 * P + off + nx], xe = V[q0 * P + off + dxe];
-      double cprv = 0.0, ccur = 0.0, cnxt = 0.0, cym = 0.0, cyp = 0.0, cxe = 0.0;
-      if constexpr (ANI) {
-        cprv = C[(q0 - 1) * P + off];
-        ccur = C[q0 * P + off];
-        cnxt = C[(q0 + 1) * P + off];
-        cym = C[q0 * P + off - nx];
-        cyp = C[q0 * P + off + nx];
-        cxe = C[q0 * P + off + dxe];
-      }
-      Buf bA, bB;
-      ld(q0 * P + off, bA);
-      auto plane = [&](int q, Buf &bc, Buf &bn) {
-        const bool more = q + 1 < q1;  // uniform
-        S nn = zero<S>(), ym1 = zero<S>(), yp1 = zero<S>(), xe1 = zero<S>();
-        double cnn = 0.0, cym1 = 0.0, cyp1 = 0.0, cxe1 = 0.0;
-        if (more) {
-          const int p1 = (q + 1) * P + off;
-          nn = V[p1 + P];
-          ym1 = V[p1 - nx];
-          yp1 = V[p1 + nx];
-          xe1 = V[p1 + dxe];
-          if constexpr (ANI) {
-            cnn = C[p1 + P];
-            cym1 = C[p1 - nx];
-            cyp1 = C[p1 + nx];
-            cxe1 = C[p1 + dxe];
-          }
-          ld(p1, bn);
-        }
-        asm volatile("" ::: "memory");  // the prefetch stays ahead of the plane's arithmetic
-        const int gq = z0 + q;
-        const bool eym = gq > 0 || y > 0, eyp = gq < npl - 1 || y < nyp - 1;
-        const bool hasp = gq > 0, hasn = gq + 1 < npl;
-        const S zp = hasp ? prev : zero<S>(), zn = hasn ? nxt : zero<S>();
-        const S yv0 = eym ? ym : zero<S>(), yv1 = eyp ? yp : zero<S>();
-        S xm = shfl_up1(cur), xp = shfl_dn1(cur);
-        if (lane == 0) xm = xe;
-        if (lane == 63) xp = xe;
-        if (!(x > 0)) xm = zero<S>();
-        if (!(x + 1 < nx)) xp = zero<S>();
-        S lap;
-        if constexpr (ANI) {
-          const double cc = ccur;
-          double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
-          if (lane == 0) cxm = cxe;
-          if (lane == 63) cxp = cxe;
-          const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
-          const double wym = face_w(eym, cc, cym), wyp = face_w(eyp, cc, cyp);
-          const double wzm = face_w(hasp, cc, cprv), wzp = face_w(hasn, cc, cnxt);
-          lap = s * ((((wzm * zp + wzp * zn) + (wxm * xm + wxp * xp)) + (wym * yv0 + wyp * yv1)) -
-                     (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * cur);
-        } else {
-          const bool bnd = bxy || gq == 0 || gq == npl - 1;
-          lap = s * (((zp + zn) + (xm + xp)) + (yv0 + yv1)) + (bnd ? sdb : sdi) * cur;
-        }
-        fn(q * P + off, cur, lap, bc, xin);
-        prev = cur;
-        cur = nxt;
-        nxt = nn;
-        ym = ym1;
-        yp = yp1;
-        xe = xe1;
-        if constexpr (ANI) {
-          cprv = ccur;
-          ccur = cnxt;
-          cnxt = cnn;
-          cym = cym1;
-          cyp = cyp1;
-          cxe = cxe1;
-        }
-      };
-      int q = q0;
-      for (; q + 1 < q1; q += 2) {  // two planes per trip: the buffers swap roles without copies
-        plane(q, bA, bB);
-        plane(q + 1, bB, bA);
-      }
-      if (q < q1) plane(q, bA, bB);
-    }
-  }
-  if (tq) tq_done(tq);
-}
-
 #include "nls_march_q.hpp"
 
 #ifndef NLS_UPD_RB_MODE
@@ -426,25 +302,11 @@ constexpr int RB_ALPHA = 4;
 #define NLS_RB_L2 1  // measured at 512^3: RB 1 / kz 32 0.50 ms vs RB 4 / kz 8 0.58 ms (tools/exp_l2.sh)
 #endif
 constexpr int RB_L2 = NLS_RB_L2;  // rows per thread of k_alpha_l2
-#ifndef NLS_L2_PF
-#define NLS_L2_PF 1  // 3D k_alpha_l2 through the pipelined march (march_pf)
-#endif
 #ifndef NLS_FUSED_RB
 #define NLS_FUSED_RB 1
 #endif
 constexpr int FUSED_RB = NLS_FUSED_RB;  // rows per thread of k_tail
-#ifndef NLS_TAIL_PF
-#define NLS_TAIL_PF 1  // 3D tails through the software-pipelined march (march_pf)
-#endif
-#ifndef NLS_TAIL_NACC
-#define NLS_TAIL_NACC 4  // partial sums of the tail's combination (plain march)
-#endif
-#ifndef NLS_TAIL_NACC_PF
-#define NLS_TAIL_NACC_PF 2  // the same with the pipelined march (registers: two planes of loads)
-#endif
-#ifndef NLS_TAIL_OCC
-#define NLS_TAIL_OCC 2  // k_tail's __launch_bounds__ minimum waves per SIMD (2: <= 256 VGPRs)
-#endif
+
 
 // y = L x  (DeviceSpMV::multiply, device/spmv.hpp:65-73)
 template <class S, int DIM, bool ANI>
@@ -742,22 +604,11 @@ template <class S, int DIM, bool ANI>
 __global__ __launch_bounds__(NTHREADS) void k_alpha_l2(const S *__restrict__ V, Geo g,
                                                        cplx *__restrict__ part) {
   double a = 0.0, n2 = 0.0, l2 = 0.0;
-  auto acc = [&](const S &c, const S &lap) {
+  march<S, DIM, RB_L2, false, ANI>(V, g, [&](int, const S &c, const S &lap) {
     a += to_c(cj_mul(c, lap)).re;
     n2 += abs2(c);
     l2 += abs2(lap);
-  };
-  if constexpr (DIM == 3 && RB_L2 == 1 && NLS_L2_PF) {
-    // the pipelined march (march_pf: the neighbours of plane q+1 and the stencil plane
-    // q+2 in flight while plane q is reduced); the same cells in the same order, so the
-    // same partial sums bit for bit
-    struct NoBuf {};
-    march_pf<S, ANI, NoBuf>(V, g, [](int, NoBuf &) {}, [&](int, const S &c, const S &lap, const NoBuf &, bool ok) {
-      if (ok) acc(c, lap);
-    });
-  } else {
-    march<S, DIM, RB_L2, false, ANI>(V, g, [&](int, const S &c, const S &lap) { acc(c, lap); });
-  }
+  });
   cplx v[3] = {{a, 0.0}, {n2, 0.0}, {l2, 0.0}};
   block_store<3>(v, part, gridDim.x, 0);
 }
@@ -785,7 +636,7 @@ __device__ __forceinline__ double sin_rl(double x) {
 }
 
 template <class S, int DIM, int M, bool ANI, int MODE>
-__global__ __launch_bounds__(NTHREADS, NLS_TAIL_OCC) void k_tail(TailArgs ta, Geo g) {
+__global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
   static_assert(M >= 3, "the stencil vector must not be W_0 (updated in place)");
   constexpr int J = M - 2;
   constexpr int NF = tail_nf(MODE);
@@ -820,11 +671,6 @@ __global__ __launch_bounds__(NTHREADS, NLS_TAIL_OCC) void k_tail(TailArgs ta, Ge
     S e0, e1;
     double d0;
   };
-  // the pipelined 3D march holds two planes of streamed cells in registers: where they fit
-  // beside the epilogue at two waves per SIMD (<= 256 VGPRs: c128 J <= 14 isotropic, 12
-  // anisotropic; f64 J + M2 <= 18), else the plain march
-  constexpr bool PF = NLS_TAIL_PF && DIM == 3 && (std::is_same<S, cplx>::value ? J <= (ANI ? 12 : 14) : J + M2 <= 18);
-  constexpr int NACC = PF ? NLS_TAIL_NACC_PF : NLS_TAIL_NACC;
   auto load = [&](int q, TBuf &b) {
     const S *__restrict__ src = W + q;
 #pragma unroll
@@ -858,19 +704,19 @@ __global__ __launch_bounds__(NTHREADS, NLS_TAIL_OCC) void k_tail(TailArgs ta, Ge
     }
   };
   // y_f = sum_k cf[f][k] W_k + cf[f][J+1] L W_J, then the step's epilogue at cell q.
-  // NACC partial sums (term k into sum k mod NACC): a single chain of 2(J+2) dependent
-  // f64 FMAs per component left the waves issue-stalled (SQ_WAIT_INST_ANY 0.55 of the
-  // wave cycles at 512^3, m = 16); shorter chains overlap
+  // Four partial sums (term k into sum k mod 4): one chain of 2(J+2) dependent f64 FMAs
+  // per component left the waves stalled on the chain (512^3, m = 16: tail 6.02 ->
+  // 5.92 ms with four, same box, profiles/r04/ab_tail.txt)
   auto finish = [&](int q, const S &cur, const S &lap, const TBuf &b) {
     S y[NF];
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       S a4[4] = {zero<S>(), zero<S>(), zero<S>(), zero<S>()};
 #pragma unroll
-      for (int k = 0; k < J; ++k) smac(a4[k % NACC], cf[f][k], b.wk[k]);
-      smac(a4[J % NACC], cf[f][J], cur);
-      smac(a4[(J + 1) % NACC], cf[f][J + 1], lap);
-      y[f] = NACC == 4 ? (a4[0] + a4[1]) + (a4[2] + a4[3]) : (NACC == 2 ? a4[0] + a4[1] : a4[0]);
+      for (int k = 0; k < J; ++k) smac(a4[k & 3], cf[f][k], b.wk[k]);
+      smac(a4[J & 3], cf[f][J], cur);
+      smac(a4[(J + 1) & 3], cf[f][J + 1], lap);
+      y[f] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
     }
     if constexpr (MODE == TAIL_NLSE) {
       cplx un, w0;
@@ -905,27 +751,19 @@ __global__ __launch_bounds__(NTHREADS, NLS_TAIL_OCC) void k_tail(TailArgs ta, Ge
       static_cast<cplx *>(ta.up)[q] = to_c(b.e0);
     }
   };
-  if constexpr (PF) {
-    // software-pipelined march (march_pf): plane q+1's reads in flight while plane q computes
-    march_pf<S, ANI, TBuf>(VJ, g, load, [&](int q, const S &cur, const S &lap, const TBuf &b, bool ok) {
-      asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
-      if (ok) finish(q, cur, lap, b);
-    });
-  } else {
-    // one row per thread: with the epilogue at the end of the combination, two
-    // rows no longer fit in the 256 registers of two waves per SIMD
-    constexpr int RB = FUSED_RB;
-    march<S, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
-      TBuf b[RB];
+  // one row per thread: with the epilogue at the end of the combination, two
+  // rows no longer fit in the 256 registers of two waves per SIMD
+  constexpr int RB = FUSED_RB;
+  march<S, DIM, RB, true, ANI>(VJ, g, [&](const int *p, const S *cur, const S *lap, const bool *ok) {
+    TBuf b[RB];
 #pragma unroll
-      for (int r = 0; r < RB; ++r)
-        if (ok[r]) load(p[r], b[r]);
-      asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
+    for (int r = 0; r < RB; ++r)
+      if (ok[r]) load(p[r], b[r]);
+    asm volatile("" ::: "memory");  // keep the coefficient reads in LDS
 #pragma unroll
-      for (int r = 0; r < RB; ++r)
-        if (ok[r]) finish(p[r], cur[r], lap[r], b[r]);
-    });
-  }
+    for (int r = 0; r < RB; ++r)
+      if (ok[r]) finish(p[r], cur[r], lap[r], b[r]);
+  });
 }
 
 #define NLS_J_LIST(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \

@@ -154,6 +154,7 @@ class P2dSchedule:
         self.OCC2A, self.EARLYA, self.DS1A = define("NLS_P2A_OCC2_MAXJ"), define("NLS_P2A_EARLY"), define("NLS_P2A_DS1")
         self.DS2, self.DS3 = define("NLS_P2D_DS2_MAXJ"), define("NLS_P2D_DS3_MAXJ")
         self.EARLY, self.NPMAX = define("NLS_P2D_EARLY"), define("NLS_P2D_NP_MAX")
+        self.PRE_LA = define("NLS_P2D_PRE_LA")
         self.SR, self.SRB, self.LR = const("P2D_SR"), const("P2D_SRB"), const("P2D_LR")
         self.CSB = const("P2D_CSB")
         self.LDS = 160 * 1024
@@ -191,11 +192,20 @@ class P2dSchedule:
     def late(self, J, A=0):
         return J > 0 and self.np(J, A) == 1
 
+    def nsl(self, J, A=0):
+        return self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
+
+    def dspre(self, J, A=0):
+        """Look-ahead S groups issued ahead of the J groups and the prologue's wait."""
+        pre = min(self.ds(J, A), self.nsl(J, A) - 4) if self.PRE_LA else 0
+        return pre if pre > 0 else self.ds(J, A)
+
     def after(self, J, stw, i, A=0):
         DS, NP, NSD = self.ds(J, A), self.np(J, A), 6 if A else 4
         early, late = self.early(J, A), self.late(J, A)
         n = lastS = lastJ = 0
-        for d in range(DS):
+        pre = self.dspre(J, A)
+        for d in range(pre):
             n += NSD
             if d == i:
                 lastS = n
@@ -204,6 +214,10 @@ class P2dSchedule:
                 n += J
                 if d == i:
                     lastJ = n
+        for d in range(pre, DS):
+            n += NSD
+            if d == i:
+                lastS = n
         s = 0
         while True:
             if early:

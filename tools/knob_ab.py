@@ -4,7 +4,9 @@ to handle on one box, more than the effects measured here, so every variant runs
 the SAME handle, rounds interleaved.  Prints per variant and round the per-pass times,
 the tail and the step's kernel classes.
 usage: python tools/knob_ab.py n m steps rounds "knob=v,knob=v" ...
-knobs: tail_dyn (1), kz_fused (2), p2_order (3), p2_kz2 (4), p2_zbig (5); "" = as created.  (Tiles of k_p2d by
+knobs: tail_dyn (1), kz_fused (2), p2_order (3); "" = as created.  (Round 4: shorter k_p2d tiles at the
+end of each launch, chunks of 128 / 64 / 32 planes after the first 256, measured no gain or a loss,
+profiles/r04/knob_ab_512.txt; removed.)  (Tiles of k_p2d by
 ticket of a global counter measured +1.8 % pass time, and the tail's queue on the full
 tile grid +50 %: removed, profiles/r03/knob_ab_dyn.txt.)"""
 import os
@@ -16,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "nonlinear-solvers_amd"))
 import nls_amd  # noqa: E402
 
-KNOB = {"tail_dyn": 1, "kz_fused": 2, "p2_order": 3, "p2_kz2": 4, "p2_zbig": 5}
+KNOB = {"tail_dyn": 1, "kz_fused": 2, "p2_order": 3}
 n, m, steps, rounds = (int(a) for a in sys.argv[1:5])
 variants = sys.argv[5:] or [""]
 dx = 20.0 / (n - 1)
