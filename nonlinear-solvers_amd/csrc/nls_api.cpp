@@ -114,6 +114,7 @@ struct nls_handle {
   void *p2 = nullptr;          // P2State
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
+  int p2kzj = 32;              // tile depth of the register-row passes (pass2_jreg)
   bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
   bool p2_split_on = true;     // collective handles: boundary/interior split (NLS_P2_SPLIT=0: off)
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
@@ -734,11 +735,18 @@ bool p2_split(const nls_handle *h) {
          !h->p2_ani;
 }
 int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
+// tile depth of pass J: the register-row passes (J rows loaded straight into
+// registers, no J-ring prologue) stream faster from shorter tiles (512^3 J = 10: 4.77 ms
+// at kz 32 vs 4.89 at 256; the J-ring passes lose: J = 12 6.45 vs 5.80; round 4,
+// profiles/r04/p2ab_512.txt)
+int p2_kz(const nls_handle *h, int J) {
+  return !h->p2_ani && h->cfg.dim == 3 && pass2_jreg(J) ? std::min(h->p2kz, h->p2kzj) : h->p2kz;
+}
 int p2_grid(const nls_handle *h, int J = 0) {
   if (h->p2reg) return h->p2mgrid[J];
   const int64_t nzl = p2_geo(h).nzl;
-  if (!p2_split(h)) return p2_tiles(h, 0, nzl, h->p2kz);
-  return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, h->p2kz);
+  if (!p2_split(h)) return p2_tiles(h, 0, nzl, p2_kz(h, J));
+  return p2_bnd_tiles(h) + p2_tiles(h, 2, nzl - 2, p2_kz(h, J));
 }
 
 // Two new vectors per pass (nls_pass2.hpp): the alpha pass + reduction of W_0
@@ -794,6 +802,7 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
     int J = sched[si].first, ns = sched[si].second;
     const int out = J + ns;  // the pass's last vector: the next stencil vector
     int nb = p2_grid(h, J);
+    g.kz = p2_kz(h, J);
     const void *fn = h->p2reg ? nullptr
                      : h->p2_ani ? kernel_pass2a(J, ns == 2)
                                  : kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
@@ -1042,11 +1051,13 @@ void alloc_all(nls_handle *h) {
     const int64_t span = p2_split(h) ? gm.nzl - 4 : gm.nzl;
     h->p2kz = (int)std::max<int64_t>(std::min<int64_t>(16, span), std::min<int64_t>(256, (span + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("NLS_P2_KZJ")) h->p2kzj = std::max(1, std::atoi(e));
     // tile order (round 3, tools/order_sweep.py, tools/wl_ab.sh): 3D x-fastest without XCD
     // bands (512^3 passes 25.6 -> 25.1 ms per step; 256^3 -0.5 %); 2D keeps the bands
     // (4096^2 passes 3.14 -> 3.34 ms without them)
     h->p2order = dim == 3 ? 6 : 0;
-    h->p2grid = p2_grid(h);
+    h->p2grid = 0;
+    for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
     if (h->p2reg)
       for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, h->p2mgrid[J]);
     hip_check(h, hipMalloc(&h->p2, p2state_bytes() * h->nbasis), "hipMalloc(p2)");  // one per basis

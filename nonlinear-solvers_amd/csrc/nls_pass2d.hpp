@@ -76,6 +76,28 @@ constexpr int P2D_CSB = P2D_SR * P2D_CRB + P2D_SR * 32;
 #ifndef NLS_P2D_PRE_LA
 #define NLS_P2D_PRE_LA 1      // issue the look-ahead before the prologue's wait (p2d_dspre)
 #endif
+#ifndef NLS_P2D_JREG
+#define NLS_P2D_JREG 1        // isotropic passes from J = NLS_P2D_JREG_MINJ: J rows in registers (p2d_jreg)
+#endif
+#ifndef NLS_P2D_JREG_MINJ
+#define NLS_P2D_JREG_MINJ 8
+#endif
+#ifndef NLS_P2D_JREG_MAXJ
+#define NLS_P2D_JREG_MAXJ 10
+#endif
+// The isotropic passes at J = 8, 10 read their J stored rows straight into registers
+// (one non-temporal load per row at the top of each step, awaited by the compiler's own
+// counted vmcnt before the first use) instead of through an LDS ring: without the J
+// ring the rings take ~47 KiB, so two workgroups fit per CU and the second covers the
+// first's barriers and waits, and short tiles (no J-ring prologue) stream from a
+// compact address window (512^3, same box: J = 10 5.17 ms at kz 32 vs 5.36 at 256 and
+// 5.22 through the ring).  J = 12 with Z does not fit: all rows live across the step
+// took 256 VGPRs and scratch; half of them loaded after the S issue (SGPR-walked
+// addresses) fit but ran slower than the ring (6.16 vs 6.06 ms; round 4,
+// profiles/r04/p2ab_512.txt).
+__host__ __device__ constexpr bool p2d_jreg(int J, bool A = false) {
+  return NLS_P2D_JREG && !A && J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ;
+}
 // Workgroups per CU: two where the registers (<= 256 per lane) and the rings
 // (<= 80 KiB) allow, so the second workgroup's waves cover the first's barriers
 // and LDS latencies; one for the long passes.
@@ -89,7 +111,8 @@ constexpr int P2D_CSB = P2D_SR * P2D_CRB + P2D_SR * 32;
 #define NLS_P2D_OCC0 3  // workgroups per CU of the J = 0 pass (S look-ahead 1; 512^3: 1.40 vs 1.61 ms at 2)
 #endif
 __host__ __device__ constexpr int p2d_occ(int J, bool A = false) {
-  return A ? (J <= NLS_P2A_OCC2_MAXJ ? 2 : 1) : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ ? 2 : 1));
+  return A ? (J <= NLS_P2A_OCC2_MAXJ ? 2 : 1)
+           : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ || p2d_jreg(J) ? 2 : 1));
 }
 // S ring: the planes k .. k+2 being read, DS planes of look-ahead and the slot of
 // plane k-2 (free since the previous step's barrier), into which a step issues
@@ -120,7 +143,7 @@ __host__ __device__ constexpr int p2d_avail(int J, bool A = false) {
 // anisotropic passes): the wave reads its J rows of plane k into registers and then
 // DMAs plane k+1 into the same slot, so the look-ahead is one step
 __host__ __device__ constexpr int p2d_np(int J, bool A = false) {
-  return J == 0 ? 0
+  return J == 0 || p2d_jreg(J, A) ? 0
                 : (p2d_avail(J, A) / (P2D_TR * 1024 * J) < NLS_P2D_NP_MAX ? p2d_avail(J, A) / (P2D_TR * 1024 * J)
                                                                           : NLS_P2D_NP_MAX);
 }
@@ -131,7 +154,7 @@ __host__ __device__ constexpr int p2d_off_c(int J, bool A = false) {
 __host__ __device__ constexpr int p2d_lds_bytes(int J, bool A = false) { return p2d_off_c(J, A) + 2 * (J + 1) * 16; }
 __host__ __device__ constexpr bool p2d_rings_ok(int J, bool A = false) {
   return J == 0 ? p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS
-                : (J <= (A ? P2D_JMAX_A : P2D_JMAX) && p2d_np(J, A) >= 1 &&
+                : (J <= (A ? P2D_JMAX_A : P2D_JMAX) && (p2d_np(J, A) >= 1 || p2d_jreg(J, A)) &&
                    p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS);
 }
 static_assert(p2d_rings_ok(2) && p2d_rings_ok(4) && p2d_rings_ok(6) && p2d_rings_ok(8) && p2d_rings_ok(10) &&
@@ -159,7 +182,7 @@ __host__ __device__ constexpr int p2d_dspre(int J, bool A = false) {
 }
 __host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = false) {
   const int DS = p2d_ds(J, A), NP = p2d_np(J, A), NSD = p2d_nsd(A);
-  const bool early = p2d_early(J, A), late = p2d_late(J, A);
+  const bool early = p2d_early(J, A), late = p2d_late(J, A), jreg = p2d_jreg(J, A);
   // the issue order ahead of the loop: [S groups d < DSPRE][J groups][S groups d >= DSPRE]
   // (DSPRE = 0: every S group first, as the round-3 kernel issued them)
   const int dspre = p2d_dspre(J, A) > 0 ? p2d_dspre(J, A) : DS;
@@ -168,7 +191,7 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = fals
     n += NSD;
     if (d == i) lastS = n;
   }
-  if (J > 0) {
+  if (J > 0 && !jreg) {
     const int pj = late ? 1 : NP - 1;
     for (int d = 0; d < pj; ++d) {
       n += J;
@@ -180,10 +203,11 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = fals
     if (d == i) lastS = n;
   }
   for (int s = 0;; ++s) {
+    if (jreg) n += J;  // the step's J row loads at its top (the compiler awaits them)
     if (early) {
       n += NSD;
       if (s + DS == i) lastS = n;
-      if (J > 0 && !late) {
+      if (J > 0 && !late && !jreg) {
         n += J;
         if (s + NP - 1 == i) lastJ = n;
       }
@@ -192,7 +216,7 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = fals
     if (!early) {
       n += NSD;
       if (s + DS == i) lastS = n;
-      if (J > 0 && !late) {
+      if (J > 0 && !late && !jreg) {
         n += J;
         if (s + NP - 1 == i) lastJ = n;
       }
@@ -203,7 +227,7 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = fals
     }
     n += STW;
   }
-  const int aS = n - lastS, aJ = J > 0 ? n - lastJ : 1 << 20;
+  const int aS = n - lastS, aJ = J > 0 && !jreg ? n - lastJ : 1 << 20;
   return aS < aJ ? aS : aJ;
 }
 // from this step on every wait is the same (a safe bound of the replay's warm-up)
@@ -303,7 +327,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   static_assert(p2d_rings_ok(J, A), "rings exceed LDS");
   static_assert(!(A && (D2 || PR)), "the anisotropic pass is 3D complex");
   constexpr int DS = p2d_ds(J, A), NSL = p2d_nsl(J, A), NP = p2d_np(J, A);
-  constexpr bool LATE = p2d_late(J, A);
+  constexpr bool LATE = p2d_late(J, A), JREG = p2d_jreg(J, A);
   constexpr int STW = HZ ? 2 : 1;            // stores per step
   // columns: gX[0..J], (HZ: gZ[0..J], xx, xz, zz | xx); J = 0 also ||S_0||^2 (the
   // blind start, k_p2coef mode 2)
@@ -563,27 +587,35 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   int jis = NP > 0 ? NP - 1 : 0;  // J slot of the next issued plane k+NP-1
   int lsl = 0;                 // L ring slot of plane k
 
+  // JREG: this lane's cell of plane k in the stored vectors (a ragged tile's extra lanes
+  // read the row's last cell)
+  const cplx *__restrict__ jrow = W + ((int64_t)y * nx + x0 + src_lane);
   for (int k = k0; k < k1; ++k) {
     const int i = k - k0;
+    cplx sv[J + 1];
+    if constexpr (JREG) {
+      const cplx *__restrict__ src = jrow + (int64_t)k * P;
+#pragma unroll
+      for (int l = 0; l < J; ++l) sv[l] = ld_nt(src + (int64_t)l * vs);
+    }
     // NLS_P2D_EARLY: issue first (the slots are free: S plane k-2 since the last
     // barrier, the wave's own J plane k-1 since its last step), then wait
     if constexpr (p2d_early(J, A)) {
       P2D_ISSUE_S(k + DS + 2, sis);
-      if constexpr (J > 0 && !LATE) P2D_ISSUE_J(k + NP - 1, jis);
+      if constexpr (J > 0 && !LATE && !JREG) P2D_ISSUE_J(k + NP - 1, jis);
     }
     wait_step<J, STW, A>(i);
     raw_barrier();
     if constexpr (!p2d_early(J, A)) {
       P2D_ISSUE_S(k + DS + 2, sis);
-      if constexpr (J > 0 && !LATE) P2D_ISSUE_J(k + NP - 1, jis);
+      if constexpr (J > 0 && !LATE && !JREG) P2D_ISSUE_J(k + NP - 1, jis);
     }
     const int s1 = sk + 1 == NSL ? 0 : sk + 1, s2 = s1 + 1 == NSL ? 0 : s1 + 1;
     // L S_J of plane k+1: own row (register) + halo values, shared rows into L slot lsl^1
     cplx ln, lne;
     P2D_LROWS(k + 1, sk, s1, s2, lsl ^ 1, ln, lne);
     // the J stored vectors of this cell and S_J itself
-    cplx sv[J + 1];
-    if constexpr (J > 0) {
+    if constexpr (J > 0 && !JREG) {
       const cplx *jv = reinterpret_cast<const cplx *>(smem + p2d_off_j(J, A) + ((jr * J) * P2D_TR + w) * 1024);
 #pragma unroll
       for (int l = 0; l < J; ++l) sv[l] = jv[l * P2D_TR * 64 + lane];

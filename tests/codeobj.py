@@ -129,11 +129,14 @@ def vmem_counts(ins) -> dict[str, int]:
     return c
 
 
-def p2d_loop_loads(J: int, A: int = 0) -> dict[str, int]:
+def p2d_loop_loads(J: int, A: int = 0, jreg: bool = False) -> dict[str, int]:
     """VMEM loads of one march step as the source issues them: 2 S rows (1 KiB each
     + a 4-byte halo piece on 16 lanes), with A the two c rows (one 16-B DMA + one
-    4-byte halo piece), and the J J-ring rows."""
-    return {"global_load_lds_dwordx4": 2 + J + (1 if A else 0), "global_load_lds_dword": 2 + (1 if A else 0)}
+    4-byte halo piece), and the J rows (J-ring DMAs, or with jreg register loads)."""
+    d = {"global_load_lds_dwordx4": 2 + (0 if jreg else J) + (1 if A else 0), "global_load_lds_dword": 2 + (1 if A else 0)}
+    if jreg:
+        d["global_load_dwordx4"] = J
+    return d
 
 
 class P2dSchedule:
@@ -155,16 +158,22 @@ class P2dSchedule:
         self.DS2, self.DS3 = define("NLS_P2D_DS2_MAXJ"), define("NLS_P2D_DS3_MAXJ")
         self.EARLY, self.NPMAX = define("NLS_P2D_EARLY"), define("NLS_P2D_NP_MAX")
         self.PRE_LA = define("NLS_P2D_PRE_LA")
+        self.JREG = define("NLS_P2D_JREG")
+        self.JREG_MINJ, self.JREG_MAXJ = define("NLS_P2D_JREG_MINJ"), define("NLS_P2D_JREG_MAXJ")
         self.SR, self.SRB, self.LR = const("P2D_SR"), const("P2D_SRB"), const("P2D_LR")
         self.CSB = const("P2D_CSB")
         self.LDS = 160 * 1024
 
     TR = 4
 
+    def jreg(self, J, A=0):
+        """J rows loaded into registers (no J ring)."""
+        return bool(self.JREG) and not A and self.JREG_MINJ <= J <= self.JREG_MAXJ
+
     def occ(self, J, A=0):
         if A:
             return 2 if J <= self.OCC2A else 1
-        return self.OCC0 if J == 0 else (2 if J <= self.OCC2 else 1)
+        return self.OCC0 if J == 0 else (2 if J <= self.OCC2 or self.jreg(J) else 1)
 
     def ds(self, J, A=0):
         o = self.occ(J, A)
@@ -182,7 +191,7 @@ class P2dSchedule:
         return bool(self.EARLY) and self.occ(J, A) == 1
 
     def np(self, J, A=0):
-        if J == 0:
+        if J == 0 or self.jreg(J, A):
             return 0
         nsl = self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
         off_j = nsl * self.SR * self.SRB + (nsl * self.CSB if A else 0) + 2 * self.LR * 1024
@@ -202,14 +211,14 @@ class P2dSchedule:
 
     def after(self, J, stw, i, A=0):
         DS, NP, NSD = self.ds(J, A), self.np(J, A), 6 if A else 4
-        early, late = self.early(J, A), self.late(J, A)
+        early, late, jreg = self.early(J, A), self.late(J, A), self.jreg(J, A)
         n = lastS = lastJ = 0
         pre = self.dspre(J, A)
         for d in range(pre):
             n += NSD
             if d == i:
                 lastS = n
-        if J > 0:
+        if J > 0 and not jreg:
             for d in range(1 if late else NP - 1):
                 n += J
                 if d == i:
@@ -220,11 +229,13 @@ class P2dSchedule:
                 lastS = n
         s = 0
         while True:
+            if jreg:
+                n += J  # the step's J row loads at its top
             if early:
                 n += NSD
                 if s + DS == i:
                     lastS = n
-                if J > 0 and not late:
+                if J > 0 and not late and not jreg:
                     n += J
                     if s + NP - 1 == i:
                         lastJ = n
@@ -234,7 +245,7 @@ class P2dSchedule:
                 n += NSD
                 if s + DS == i:
                     lastS = n
-                if J > 0 and not late:
+                if J > 0 and not late and not jreg:
                     n += J
                     if s + NP - 1 == i:
                         lastJ = n
@@ -244,7 +255,7 @@ class P2dSchedule:
                     lastJ = n
             n += stw
             s += 1
-        return min(n - lastS, n - lastJ if J > 0 else 1 << 20)
+        return min(n - lastS, n - lastJ if J > 0 and not jreg else 1 << 20)
 
     def waits(self, J, stw, A=0):
         """The vmcnt values wait_step<J, STW, A> can emit (steps 0 .. p2d_i0)."""
@@ -280,13 +291,15 @@ def check_p2d(funcs, meta, sched: P2dSchedule):
         got = vmem_counts(loop)
         stw = 1 + hz
         loads = {k: v for k, v in got.items() if k != "global_store_dwordx4"}
-        if loads != p2d_loop_loads(J, A):
-            probs.append(f"march loop loads {loads} != the source's {p2d_loop_loads(J, A)}")
+        jreg = sched.jreg(J, A)
+        if loads != p2d_loop_loads(J, A, jreg):
+            probs.append(f"march loop loads {loads} != the source's {p2d_loop_loads(J, A, jreg)}")
         if got.get("global_store_dwordx4", 0) not in (stw, 2 * stw):
             probs.append(f"march loop stores {got.get('global_store_dwordx4', 0)} (STW = {stw})")
         waits = sorted({int(re.search(r"vmcnt\((\d+)\)", o).group(1)) for _a, mn, o in loop
                         if mn == "s_waitcnt" and "vmcnt" in o})
-        if waits != sched.waits(J, stw, A):
+        # jreg: the compiler adds its own counted waits for the J register loads
+        if (not set(sched.waits(J, stw, A)) <= set(waits)) if jreg else waits != sched.waits(J, stw, A):
             probs.append(f"march loop vmcnt waits {waits} != p2d_after {sched.waits(J, stw, A)}")
         rec = {"J": J, "HZ": hz, "D2": d2, "PR": pr, "A": A, "vgpr": md.get("vgpr_count"), "agpr": md.get("agpr_count"),
                "sgpr": md.get("sgpr_count"), "sgpr_spill": md.get("sgpr_spill_count"),

@@ -97,6 +97,23 @@ print(f\"$v rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} domina
             | tee -a "$OUT/ab_$wl.txt"
         done
       done ;;
+    p2ab)
+      # per-pass times (tools/p2_probe.py, 512^3 m=16) of every lib_v* variant and lib,
+      # once per environment setting of the comma list ARG ("-" = none, e.g.
+      # "-,NLS_P2_KZJ=16") -> p2ab.txt
+      vars=$(cd nonlinear-solvers_amd && ls -d lib_v* 2>/dev/null | tr '\n' ' ')
+      for ev in $(echo "${arg:--}" | tr ',' ' '); do
+        for rep in 1 2; do
+          for v in $vars lib; do
+            echo "== $v $ev rep$rep" >> "$OUT/p2ab.txt"
+            [ "$ev" != "-" ] && export "${ev?}"
+            NLS_AMD_LIB=$PWD/nonlinear-solvers_amd/$v/libnls_amd.so run 300 "$OUT/p2ab_cur.txt" python -u tools/p2_probe.py 512 16 4
+            [ "$ev" != "-" ] && unset "${ev%%=*}"
+            cat "$OUT/p2ab_cur.txt" >> "$OUT/p2ab.txt"
+          done
+        done
+      done
+      cat "$OUT/p2ab.txt" ;;
     probe6)
       # pure-stream rates of the tail / pass access patterns (tools/bw_probe6.hip, prebuilt)
       run 300 "$OUT/bw_probe6_512.txt" tools/bw_probe6
