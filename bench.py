@@ -100,8 +100,18 @@ def moved_bytes_per_cell_step(w, m, sched, pass2, u_frac, tm, steps):
         (+ c), the tail (m-1 reads + c + m(x), u and W_0 written);
       one-vector G2 NLSE (div(c grad), m(x)): alpha passes j = 0..m-3 (W_j + c), the
         tail's alpha (W_{m-2} + c), updates J = 0..m-3 ((J+2) vectors + c), tail (m-1
-        reads + c + m(x), u and W_0 written)."""
+        reads + c + m(x), u and W_0 written);
+      two-vector Klein-Gordon (f64 cell pairs, div(c grad)): g = -m u^3 (u, m in, g out);
+        per basis (g, then u) alpha_0 (W_0 + c; blind start: first step only), the passes
+        (S_0..S_J + c in, ns out), the tail's alpha (S_{m-2} + c); the g basis's tail
+        (m-1 reads + c, its W_0 written), the Gautschi tail (m-1 reads + c + that W_0 +
+        u_past; u, u_past, v written)."""
     eq = w["eq"]
+    if pass2 and eq == 4 and not w.get("sewi"):
+        a0 = tm["class_count"].get("alpha", 0) - tm["class_count"].get("final", 0)  # alpha_0 launches
+        a0 = max(0, a0) / max(1, tm["steps"])  # per step, both bases
+        per_basis = sum((j + 1 + ns) * 8 + 8 for j, ns in sched) + 16
+        return 24 + a0 * 16 + 2 * per_basis + ((m - 1) * 8 + 16) + ((m - 1) * 8 + 8 + 16 + 24)
     if w.get("sewi") or eq == 4:
         return None
     if pass2 and eq in (0, 1):

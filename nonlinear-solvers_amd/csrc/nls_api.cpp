@@ -25,6 +25,10 @@
 #include "nls_device.hpp"
 #include "nls_kernels.hpp"
 
+#ifndef NLS_KZ_L2
+#define NLS_KZ_L2 32  // tile depth of k_alpha_l2 (with NLS_RB_L2 rows per thread, nls_stencil.hpp)
+#endif
+
 using namespace nls;
 
 namespace {
@@ -134,9 +138,9 @@ struct nls_handle {
   bool p2_fresh = true;
   bool p2_pr = false;
   bool p2_ani = false;         // k_p2d with the G2 operator (nls_pass2a.hip)          // real field marched as cell pairs by k_p2d (p2_geo)
-  int grid_alpha2 = 1, kz_alpha2 = 32, kz_fused = 0;  // kz_fused 0: geo.kz
-  int tail_grid[8] = {};  // per TailMode; 0: no such kernel (unfused path)
-  int tail_dyn_grid[8] = {};  // resident workgroups of each tail kernel (dynamic tile queue)
+  int grid_alpha2 = 1, kz_alpha2 = NLS_KZ_L2, kz_fused = 0;  // kz_fused 0: geo.kz
+  int tail_grid[TAIL_NMODES] = {};  // per TailMode; 0: no such kernel (unfused path)
+  int tail_dyn_grid[TAIL_NMODES] = {};  // resident workgroups of each tail kernel (dynamic tile queue)
   bool tail_dyn = false;      // fused tail through the dynamic tile queue (debug knob 1)
   bool tail_one_tile = false; // one tile per workgroup for the static tail grids
   int32_t *tailq = nullptr;   // its counters (Geo::tq)
@@ -804,7 +808,7 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
     int nb = p2_grid(h, J);
     g.kz = p2_kz(h, J);
     const void *fn = h->p2reg ? nullptr
-                     : h->p2_ani ? kernel_pass2a(J, ns == 2)
+                     : h->p2_ani ? kernel_pass2a(J, ns == 2, h->p2_pr)
                                  : kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
     if (h->p2reg) {
@@ -961,7 +965,7 @@ void tail_grids(nls_handle *h, bool one_tile) {
   const int64_t tt = stencil_tiles(gf, dim, fused_rows_per_thread());
   int ncu = 0;
   hip_check(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev), "hipDeviceGetAttribute");
-  for (int mode = 0; mode < 8; ++mode) {
+  for (int mode = 0; mode < TAIL_NMODES; ++mode) {
     const void *ft = kernel_tail(tail_is_cplx(h, mode), dim, mode, h->m, h->ani);
     h->tail_grid[mode] = h->tail_dyn_grid[mode] = 0;
     if (!ft) continue;
@@ -1011,8 +1015,13 @@ void alloc_all(nls_handle *h) {
                       g.nyp >= P2D_ROWS && g.nx % 2 == 0 && g.nx >= 4 && maxj <= P2D_MAXJ_A &&
                       (!h->collective || min_slab_planes(h) >= 4) && g.nloc + 2 * g.P < (int64_t(1) << 31) &&
                       !(std::getenv("NLS_P2_REG") && std::atoi(std::getenv("NLS_P2_REG")));
-    h->pass2 = want && ((base && dma) || adma || reg);
-    h->p2reg = h->pass2 && !(base && dma) && !adma;
+    // the Klein-Gordon Gautschi step (3D, real, div(c grad)): k_p2d with the G2 operator
+    // on pairs of cells (nx even), J <= P2D_MAXJ_A2; both bases end in fused tails
+    const bool kdma = h->kg && dim == 3 && h->m >= 3 && g.nyp % P2D_ROWS == 0 && g.nyp >= P2D_ROWS &&
+                      g.nx % 2 == 0 && g.nx >= 4 && maxj <= P2D_MAXJ_A2 &&
+                      (!h->collective || min_slab_planes(h) >= 4) && g.nloc + 2 * g.P < (int64_t(1) << 31);
+    h->pass2 = want && ((base && dma) || adma || reg || kdma);
+    h->p2reg = h->pass2 && !(base && dma) && !adma && !kdma;
     h->p2_ani = h->pass2 && !h->p2reg && ani;
     h->p2_d2 = h->pass2 && !h->p2reg && dim == 2;
     h->p2_pr = h->pass2 && !h->p2reg && !c;
@@ -1110,6 +1119,11 @@ void alloc_all(nls_handle *h) {
       bool ok = has(TAIL_NLSE) && has(TAIL_COMBINE);
       if (ani) ok = ok && has(TAIL_COMBINE_W0) && has(TAIL_SEWI_END);
       if (ok) h->nvec[0] = h->m - 1;
+    } else if (h->kg && h->pass2) {
+      // the s-step passes store m-1 vectors of each basis: the sinc^2 basis ends in a
+      // combining tail into its own W_0, the cos basis in the Gautschi update
+      if (!has(TAIL_COMBINE_W0) || !has(TAIL_KG_END1)) fail(h, NLS_ERR_STATE, "KG s-step tails missing");
+      h->nvec[0] = h->nvec[1] = h->m - 1;
     } else if (h->kg) {
       if (has(TAIL_KG_END)) h->nvec[0] = h->m - 1;  // the sinc^2 basis is stored in full
     } else if (has(h->gfun >= 0 ? TAIL_GG_MID : TAIL_SG_MID) && has(TAIL_SG_END) && has(TAIL_COMBINE)) {
@@ -1725,6 +1739,23 @@ void issue_step(nls_handle *h, double dt) {
       void *args[] = {&u, &h->mf, &g0, (void *)&n};
       pw_launch(h, 3, kernel_kg_g(), args);
       halo(h, 1, 0);
+    }
+    if (h->pass2) {
+      // s-step passes (k_p2d on cell pairs): the sinc^2 action into the g basis's own
+      // W_0 (TAIL_COMBINE_W0), then the cos basis ends in the Gautschi update that reads
+      // that one vector (TAIL_KG_END1)
+      run_lanczos2(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
+      tail_launch(h, TAIL_COMBINE_W0, tail_args(h, 1));
+      run_lanczos2(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0);
+      TailArgs ta = tail_args(h, 0);
+      ta.W2 = vec_ptr(h, 1, 0);
+      ta.up = h->up;
+      ta.v = h->vel;
+      ta.dt = dt;
+      tail_launch(h, TAIL_KG_END1, ta);
+      halo(h, 0, 0);
+      h->vel_valid = true;
+      return;
     }
     // the sinc^2 basis is stored in full; the cos basis may end in the fused tail
     const bool tail = use_tail(h, TAIL_KG_END);

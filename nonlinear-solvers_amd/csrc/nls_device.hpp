@@ -107,7 +107,11 @@ enum TailMode {
   TAIL_SEWI_END = 6,    // u <- y - 2 tau e; up <- old u             (k_sewi_end; nlse_dev.hpp:52-63)
   TAIL_GG_MID = 7,      // g_0 = -m F(y_id) (F by TailArgs::nonlin, gg_force); up <- 2 y_cos - up
                         //   (G2 Gautschi family, e.g. phi4_single.cuh:33-47)
+  TAIL_KG_END1 = 8,     // TAIL_KG_END with the sinc^2 action already combined into W2 (one
+                        //   vector: the s-step passes' KG step, whose sinc^2 basis ends in
+                        //   its own TAIL_COMBINE_W0 tail)
 };
+constexpr int TAIL_NMODES = 9;
 constexpr int tail_nf(int mode) { return (mode == TAIL_SG_MID || mode == TAIL_GG_MID) ? 2 : 1; }
 
 // Nonlinearity F of the G2 Gautschi family (g = -m F(id u)):

@@ -62,12 +62,12 @@ const void *kernel_colsum();
 //   pass2 : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* zbuf, int poff)
 const void *kernel_pass2(int J, bool hz, bool d2 = false, bool pr = false);  // hz: also Z (k_p2d)
 bool pass2_jreg(int J);  // k_p2d<J> reads its J rows into registers (p2d_jreg): shorter tiles pay
-constexpr int P2D_WAVE_XO = 64, P2D_ROWS = 4, P2D_MAXJ = 14, P2D_MAXJ_A = 22;  // == P2D_XO, P2D_TR, P2D_JMAX, P2D_JMAX_A
+constexpr int P2D_WAVE_XO = 64, P2D_ROWS = 4, P2D_MAXJ = 14, P2D_MAXJ_A = 22, P2D_MAXJ_A2 = 14;  // == P2D_XO, P2D_TR, P2D_JMAX, P2D_JMAX_A, P2D_JMAX_A2
 //   p2m    : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* lbuf, int poff)
 //            -- the register two-vector pass (nls_pass2g.hpp; lbuf = y = L S_J at local planes
 //            [-1, nzl], local plane 0 at lbuf + P, from k_lap); J even <= 28
 const void *kernel_p2m(int dim, int J, bool hz, bool ani);
-const void *kernel_pass2a(int J, bool hz);  // k_p2d of the G2 operator div(c grad) (3D, J <= P2D_MAXJ_A)
+const void *kernel_pass2a(int J, bool hz, bool pr = false);  // k_p2d of the G2 operator div(c grad) (3D; pr: real cell pairs)
 int p2m_rows_per_thread(int J);
 //   p2tail: (P2State*, KState*, const cplx* sums, int m);  p2tfin: (const P2State*, KState*, int m, int nf)
 const void *kernel_p2tail();

@@ -48,6 +48,7 @@ constexpr int P2D_SRB = 1024 + 64;    // bytes per staged S_J row: x0..x0+63, th
 constexpr int P2D_LR = P2D_TR + 2;    // L S_J rows shared per plane (y0-1 .. y0+4)
 constexpr int P2D_JMAX = 14;          // largest J of the isotropic passes (m <= 18)
 constexpr int P2D_JMAX_A = 22;        // largest J of the anisotropic passes (G2: m = 25 -> J <= 22)
+constexpr int P2D_JMAX_A2 = 14;       // largest J of the anisotropic cell-pair passes (Klein-Gordon, m <= 18)
 constexpr int P2D_GHOST = 2;          // ghost planes per side of a stored vector (radius-2 march)
 constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
 // A (the G2 operator div(c grad)): the c field staged beside S_J, same rows and
@@ -55,6 +56,13 @@ constexpr int P2D_LDS = 160 * 1024;   // LDS per CU
 // (x0-2, x0-1, x0+64, x0+65; 32 B each)
 constexpr int P2D_CRB = 512;
 constexpr int P2D_CSB = P2D_SR * P2D_CRB + P2D_SR * 32;
+// Anisotropic kinds (the A argument of the ring functions): 0 isotropic, 1 the G2
+// operator on a complex field, 2 the G2 operator on a real field as pairs of cells
+// (Klein-Gordon): c is then one f64 per cell, so a row of 64 pairs is 128 c values =
+// the same 1 KiB + 4 halo pairs as an S_J row, and its c ring is staged exactly like
+// the S ring (P2D_SRB per row; c of cell 2P + h at double index 2P + h of the row,
+// halo pairs P = 64..67 as in S)
+__host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_SRB : (A ? P2D_CSB : 0); }
 #ifndef NLS_P2D_OCC2_MAXJ
 #define NLS_P2D_OCC2_MAXJ 6   // two workgroups per CU up to this J (J = 6: late J ring, 512^3 4.08 -> 3.64 ms; J = 8 no gain)
 #endif
@@ -95,7 +103,7 @@ constexpr int P2D_CSB = P2D_SR * P2D_CRB + P2D_SR * 32;
 // took 256 VGPRs and scratch; half of them loaded after the S issue (SGPR-walked
 // addresses) fit but ran slower than the ring (6.16 vs 6.06 ms; round 4,
 // profiles/r04/p2ab_512.txt).
-__host__ __device__ constexpr bool p2d_jreg(int J, bool A = false) {
+__host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
   return NLS_P2D_JREG && !A && J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ;
 }
 // Workgroups per CU: two where the registers (<= 256 per lane) and the rings
@@ -110,14 +118,14 @@ __host__ __device__ constexpr bool p2d_jreg(int J, bool A = false) {
 #ifndef NLS_P2D_OCC0
 #define NLS_P2D_OCC0 3  // workgroups per CU of the J = 0 pass (S look-ahead 1; 512^3: 1.40 vs 1.61 ms at 2)
 #endif
-__host__ __device__ constexpr int p2d_occ(int J, bool A = false) {
-  return A ? (J <= NLS_P2A_OCC2_MAXJ ? 2 : 1)
+__host__ __device__ constexpr int p2d_occ(int J, int A = 0) {
+  return A ? (A == 1 && J <= NLS_P2A_OCC2_MAXJ ? 2 : 1)  // pairs: the c ring as large as S's
            : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ || p2d_jreg(J) ? 2 : 1));
 }
 // S ring: the planes k .. k+2 being read, DS planes of look-ahead and the slot of
 // plane k-2 (free since the previous step's barrier), into which a step issues
 // before its own wait and barrier
-__host__ __device__ constexpr int p2d_ds(int J, bool A = false) {
+__host__ __device__ constexpr int p2d_ds(int J, int A = 0) {
   return A ? (p2d_occ(J, A) == 2 ? (J == 0 ? 2 : 1) : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J >= 22 ? 1 : NLS_P2A_DS1)))
            : (p2d_occ(J) >= 3 ? 1
                                 : (p2d_occ(J) == 2
@@ -126,35 +134,35 @@ __host__ __device__ constexpr int p2d_ds(int J, bool A = false) {
 }
 // early issue only at one workgroup per CU (two: the other workgroup covers the wait,
 // and the LDS is short); not where the anisotropic rings leave no slot for it
-__host__ __device__ constexpr bool p2d_early(int J, bool A = false) {
+__host__ __device__ constexpr bool p2d_early(int J, int A = 0) {
   return A ? NLS_P2A_EARLY && p2d_occ(J, A) == 1 && J < 22 : NLS_P2D_EARLY && p2d_occ(J) == 1;
 }
-__host__ __device__ constexpr int p2d_nsl(int J, bool A = false) { return p2d_ds(J, A) + 3 + (p2d_early(J, A) ? 1 : 0); }
-__host__ __device__ constexpr int p2d_off_c_ring(int J, bool A = false) { return p2d_nsl(J, A) * P2D_SR * P2D_SRB; }
-__host__ __device__ constexpr int p2d_off_l(int J, bool A = false) {
-  return p2d_off_c_ring(J, A) + (A ? p2d_nsl(J, A) * P2D_CSB : 0);
+__host__ __device__ constexpr int p2d_nsl(int J, int A = 0) { return p2d_ds(J, A) + 3 + (p2d_early(J, A) ? 1 : 0); }
+__host__ __device__ constexpr int p2d_off_c_ring(int J, int A = 0) { return p2d_nsl(J, A) * P2D_SR * P2D_SRB; }
+__host__ __device__ constexpr int p2d_off_l(int J, int A = 0) {
+  return p2d_off_c_ring(J, A) + p2d_nsl(J, A) * p2d_csb(A);
 }
-__host__ __device__ constexpr int p2d_off_j(int J, bool A = false) { return p2d_off_l(J, A) + 2 * P2D_LR * 1024; }
-__host__ __device__ constexpr int p2d_avail(int J, bool A = false) {
+__host__ __device__ constexpr int p2d_off_j(int J, int A = 0) { return p2d_off_l(J, A) + 2 * P2D_LR * 1024; }
+__host__ __device__ constexpr int p2d_avail(int J, int A = 0) {
   return P2D_LDS / p2d_occ(J, A) - p2d_off_j(J, A) - 2 * (J + 1) * 16;
 }
 // J ring: NP whole planes of the J stored vectors of the wave's row (1 KiB each),
 // the plane being read + NP-1 planes of look-ahead.  NP = 1 ("late" J ring, the long
 // anisotropic passes): the wave reads its J rows of plane k into registers and then
 // DMAs plane k+1 into the same slot, so the look-ahead is one step
-__host__ __device__ constexpr int p2d_np(int J, bool A = false) {
+__host__ __device__ constexpr int p2d_np(int J, int A = 0) {
   return J == 0 || p2d_jreg(J, A) ? 0
                 : (p2d_avail(J, A) / (P2D_TR * 1024 * J) < NLS_P2D_NP_MAX ? p2d_avail(J, A) / (P2D_TR * 1024 * J)
                                                                           : NLS_P2D_NP_MAX);
 }
-__host__ __device__ constexpr bool p2d_late(int J, bool A = false) { return J > 0 && p2d_np(J, A) == 1; }
-__host__ __device__ constexpr int p2d_off_c(int J, bool A = false) {
+__host__ __device__ constexpr bool p2d_late(int J, int A = 0) { return J > 0 && p2d_np(J, A) == 1; }
+__host__ __device__ constexpr int p2d_off_c(int J, int A = 0) {
   return p2d_off_j(J, A) + p2d_np(J, A) * J * P2D_TR * 1024;
 }
-__host__ __device__ constexpr int p2d_lds_bytes(int J, bool A = false) { return p2d_off_c(J, A) + 2 * (J + 1) * 16; }
-__host__ __device__ constexpr bool p2d_rings_ok(int J, bool A = false) {
+__host__ __device__ constexpr int p2d_lds_bytes(int J, int A = 0) { return p2d_off_c(J, A) + 2 * (J + 1) * 16; }
+__host__ __device__ constexpr bool p2d_rings_ok(int J, int A = 0) {
   return J == 0 ? p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS
-                : (J <= (A ? P2D_JMAX_A : P2D_JMAX) && (p2d_np(J, A) >= 1 || p2d_jreg(J, A)) &&
+                : (J <= (A == 2 ? P2D_JMAX_A2 : (A ? P2D_JMAX_A : P2D_JMAX)) && (p2d_np(J, A) >= 1 || p2d_jreg(J, A)) &&
                    p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS);
 }
 static_assert(p2d_rings_ok(2) && p2d_rings_ok(4) && p2d_rings_ok(6) && p2d_rings_ok(8) && p2d_rings_ok(10) &&
@@ -164,6 +172,9 @@ static_assert(p2d_rings_ok(0, true) && p2d_rings_ok(2, true) && p2d_rings_ok(4, 
               p2d_rings_ok(14, true) && p2d_rings_ok(16, true) && p2d_rings_ok(18, true) &&
               p2d_rings_ok(20, true) && p2d_rings_ok(22, true),
               "anisotropic rings do not fit the LDS");
+static_assert(p2d_rings_ok(0, 2) && p2d_rings_ok(2, 2) && p2d_rings_ok(4, 2) && p2d_rings_ok(6, 2) &&
+              p2d_rings_ok(8, 2) && p2d_rings_ok(10, 2) && p2d_rings_ok(12, 2) && p2d_rings_ok(14, 2),
+              "anisotropic cell-pair rings do not fit the LDS");
 
 // VMEM ops issued after the last one step i needs, up to its wait (see k_p2d): a
 // replay of the wave's issue order.  After the prologue's full wait the wave issues
@@ -172,15 +183,15 @@ static_assert(p2d_rings_ok(0, true) && p2d_rings_ok(2, true) && p2d_rings_ok(4, 
 // plane k0); then per step: [S group k+DS+2 and J group k+NP-1] before the wait
 // (early) or after it, the late J group k+1 after the J rows are read, then the STW
 // stores.  Step i needs S(k+2) and J plane k.
-__host__ __device__ constexpr int p2d_nsd(bool A) { return A ? 6 : 4; }
+__host__ __device__ constexpr int p2d_nsd(int A) { return A == 2 ? 8 : (A ? 6 : 4); }
 // look-ahead S groups issued, with the J groups, before the prologue's wait (their slots
 // (4 + d) % NSL are clear of the prologue's slots 0..3: the one-workgroup-per-CU passes
 // with early issue); 0: every look-ahead group after the wait, S before J (the round-3
 // order; also the order with NLS_P2D_PRE_LA = 0)
-__host__ __device__ constexpr int p2d_dspre(int J, bool A = false) {
+__host__ __device__ constexpr int p2d_dspre(int J, int A = 0) {
   return NLS_P2D_PRE_LA ? (p2d_ds(J, A) < p2d_nsl(J, A) - 4 ? p2d_ds(J, A) : p2d_nsl(J, A) - 4) : 0;
 }
-__host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = false) {
+__host__ __device__ constexpr int p2d_after(int J, int STW, int i, int A = 0) {
   const int DS = p2d_ds(J, A), NP = p2d_np(J, A), NSD = p2d_nsd(A);
   const bool early = p2d_early(J, A), late = p2d_late(J, A), jreg = p2d_jreg(J, A);
   // the issue order ahead of the loop: [S groups d < DSPRE][J groups][S groups d >= DSPRE]
@@ -231,11 +242,11 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, bool A = fals
   return aS < aJ ? aS : aJ;
 }
 // from this step on every wait is the same (a safe bound of the replay's warm-up)
-__host__ __device__ constexpr int p2d_i0(int J, bool A = false) { return p2d_ds(J, A) + p2d_np(J, A) + 1; }
+__host__ __device__ constexpr int p2d_i0(int J, int A = 0) { return p2d_ds(J, A) + p2d_np(J, A) + 1; }
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 0 ? 0 : (N > 63 ? 63 : N)) : "memory");
 }
-template <int J, int STW, bool A, int I = 0> __device__ __forceinline__ void wait_step(int i) {
+template <int J, int STW, int A, int I = 0> __device__ __forceinline__ void wait_step(int i) {
   if constexpr (I >= p2d_i0(J, A)) {
     wait_vm<p2d_after(J, STW, I, A)>();
   } else {
@@ -320,25 +331,27 @@ __device__ __forceinline__ cplx pr_lap(cplx c, cplx xm, cplx xp, cplx yz, double
 }
 
 template <int J, bool HZ, bool D2 = false, bool PR = false, bool A = false>
-__global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
+__global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
                                                               const P2State *__restrict__ ps,
                                                               cplx *__restrict__ part, int nb,
                                                               const cplx *__restrict__ zbuf, int poff) {
-  static_assert(p2d_rings_ok(J, A), "rings exceed LDS");
-  static_assert(!(A && (D2 || PR)), "the anisotropic pass is 3D complex");
-  constexpr int DS = p2d_ds(J, A), NSL = p2d_nsl(J, A), NP = p2d_np(J, A);
-  constexpr bool LATE = p2d_late(J, A), JREG = p2d_jreg(J, A);
+  // the anisotropic kind of the ring functions (p2d_csb): 1 complex, 2 real cell pairs
+  constexpr int AK = A ? (PR ? 2 : 1) : 0;
+  static_assert(p2d_rings_ok(J, AK), "rings exceed LDS");
+  static_assert(!(A && D2), "the anisotropic pass is 3D");
+  constexpr int DS = p2d_ds(J, AK), NSL = p2d_nsl(J, AK), NP = p2d_np(J, AK);
+  constexpr bool LATE = p2d_late(J, AK), JREG = p2d_jreg(J, AK);
   constexpr int STW = HZ ? 2 : 1;            // stores per step
   // columns: gX[0..J], (HZ: gZ[0..J], xx, xz, zz | xx); J = 0 also ||S_0||^2 (the
   // blind start, k_p2coef mode 2)
   constexpr int NC = (HZ ? 2 * (J + 1) + 3 : J + 2) + (J == 0 ? 1 : 0);
   constexpr int NPD = NP > 0 ? NP : 1;
   constexpr int RW = P2D_SRB / 16;           // cplx per staged S row (68)
-  __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J, A)];
+  __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J, AK)];
   const cplx *Sr = reinterpret_cast<const cplx *>(smem);             // [NSL][P2D_SR][RW]
-  const double *Cr = reinterpret_cast<const double *>(smem + p2d_off_c_ring(J, A));  // A: [NSL][P2D_CSB/8]
-  cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J, A));       // [2][P2D_LR][64]
-  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J, A));       // [J+1]
+  const double *Cr = reinterpret_cast<const double *>(smem + p2d_off_c_ring(J, AK));  // A: [NSL][p2d_csb/8]
+  cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J, AK));       // [2][P2D_LR][64]
+  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J, AK));       // [J+1]
   cplx *cZ = cX + (J + 1);                                           // [J+1]
   // w through readfirstlane: wave-uniform for the compiler too, so row and plane
   // logic stays scalar
@@ -443,10 +456,22 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
       dma16(b_, xoff, dst_ + r_ * P2D_SRB, 0);                                          \
       if (lane < 16) dma4(b_, hoff, dst_ + r_ * P2D_SRB + 1024);                        \
     }                                                                                   \
-    if constexpr (A) {                                                                  \
+    if constexpr (AK == 2) {                                                            \
+      /* cell pairs: the c rows of the same two S rows, staged as S rows are */       \
+      char *cd_ = smem + p2d_off_c_ring(J, AK) + ((sl) * P2D_SR + 2 * w) * P2D_SRB;     \
+      _Pragma("unroll") for (int r_ = 0; r_ < 2; ++r_) {                                \
+        const int yy_ = y0 - 2 + 2 * w + r_, kk_ = P2D_PLANE(p_, yy_), lp_ = kk_ - z0;  \
+        const bool ok_ = kk_ >= 0 && kk_ < nz && lp_ >= -P2D_GHOST && lp_ < nzl + P2D_GHOST && \
+                         p_ <= k1 + 1;                                                  \
+        const char *b_ = ok_ ? Cg + (p_ * P16 + (int64_t)yy_ * nx * 16)                 \
+                             : reinterpret_cast<const char *>(zbuf);                    \
+        dma16(b_, xoff, cd_ + r_ * P2D_SRB, 0);                                         \
+        if (lane < 16) dma4(b_, hoff, cd_ + r_ * P2D_SRB + 1024);                       \
+      }                                                                                 \
+    } else if constexpr (A) {                                                           \
       /* the c rows of the same two S rows: lanes 0..31 / 32..63 two cells each of   \
          row 2w / 2w+1, then their halo cells on lanes 0..15 (8 lanes x 4 B a row) */ \
-      char *cd_ = smem + p2d_off_c_ring(J, A) + (sl) * P2D_CSB;                         \
+      char *cd_ = smem + p2d_off_c_ring(J, AK) + (sl) * P2D_CSB;                        \
       const int yc_ = y0 - 2 + 2 * w + (lane >> 5), kc_ = P2D_PLANE(p_, yc_), lc_ = kc_ - z0; \
       const bool okc_ = kc_ >= 0 && kc_ < nz && lc_ >= -P2D_GHOST && lc_ < nzl + P2D_GHOST && \
                         p_ <= k1 + 1;                                                   \
@@ -471,7 +496,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
 #define P2D_ISSUE_J(p, sl)                                                              \
   do {                                                                                  \
     const char *b_ = jb0 + (int64_t)min((p), k1 - 1) * P16;                             \
-    char *dst_ = smem + p2d_off_j(J, A) + (((sl) * J) * P2D_TR + w) * 1024;             \
+    char *dst_ = smem + p2d_off_j(J, AK) + (((sl) * J) * P2D_TR + w) * 1024;             \
     _Pragma("unroll") for (int l_ = 0; l_ < J; ++l_) {                                  \
       asm volatile("" : "+s"(b_));  /* keep the walk: no J loop-invariant pointers */   \
       dma16(b_, xoff, dst_ + l_ * P2D_TR * 1024, 1);                                    \
@@ -482,6 +507,8 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   // cells x0-2, x0-1, x0+64, x0+65)
 #define P2D_CV(sl, tr, i)                                                                \
   Cr[(sl) * (P2D_CSB / 8) + ((i) < 64 ? (tr) * 64 + (i) : P2D_SR * 64 + (tr) * 4 + (i) - 64)]
+  // cell pairs: c of cell h (0: 2P, 1: 2P + 1) of pair row index P (0..67, as S_J's)
+#define P2D_CV2(sl, tr, P, h) Cr[((sl) * P2D_SR + (tr)) * (P2D_SRB / 8) + 2 * (P) + (h)]
   // L S_J at plane p, S tile row tr (yy = y0 - 2 + tr), x position xx with row
   // indices ci (centre), mi_ / pi_ (x - 1 / x + 1), from ring slots sm, sc, sp
   // (planes p-1, p, p+1)
@@ -499,7 +526,31 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
     const cplx zm_ = D2 ? cplx{0.0, 0.0} : Sm_[(ci)], zp_ = D2 ? cplx{0.0, 0.0} : Sp_[(ci)]; \
     const bool ok_ = xx_ >= 0 && xx_ < nx && kk_ >= 0 && kk_ < nz;                      \
     cplx v_;                                                                            \
-    if constexpr (A) {                                                                  \
+    if constexpr (AK == 2) {                                                            \
+      /* div(c grad) per cell of the pair (a = 2 xx, b = 2 xx + 1): the a|b face     \
+         always exists, a's x - 1 is the previous pair's b, b's x + 1 the next      \
+         pair's a; y, z faces per cell as in the complex form */                     \
+      const int jj_ = P2D_ROW(yy_);                                                     \
+      const double ca_ = P2D_CV2(sc, tr_, ci, 0), cb_ = P2D_CV2(sc, tr_, ci, 1);        \
+      const double wab_ = 0.5 * (ca_ + cb_);                                            \
+      const double wam_ = p2d_face(xx_ > 0, ca_, P2D_CV2(sc, tr_, mi_, 1));             \
+      const double wbp_ = p2d_face(xx_ + 1 < nx, cb_, P2D_CV2(sc, tr_, pi_, 0));        \
+      const bool ym_ok_ = kk_ > 0 || jj_ > 0, yp_ok_ = kk_ < nz - 1 || jj_ < ny - 1;    \
+      const double wyam_ = p2d_face(ym_ok_, ca_, P2D_CV2(sc, tr_ - 1, ci, 0));          \
+      const double wyap_ = p2d_face(yp_ok_, ca_, P2D_CV2(sc, tr_ + 1, ci, 0));          \
+      const double wybm_ = p2d_face(ym_ok_, cb_, P2D_CV2(sc, tr_ - 1, ci, 1));          \
+      const double wybp_ = p2d_face(yp_ok_, cb_, P2D_CV2(sc, tr_ + 1, ci, 1));          \
+      const double wzam_ = p2d_face(kk_ > 0, ca_, P2D_CV2(sm, tr_, ci, 0));             \
+      const double wzap_ = p2d_face(kk_ < nz - 1, ca_, P2D_CV2(sp, tr_, ci, 0));        \
+      const double wzbm_ = p2d_face(kk_ > 0, cb_, P2D_CV2(sm, tr_, ci, 1));             \
+      const double wzbp_ = p2d_face(kk_ < nz - 1, cb_, P2D_CV2(sp, tr_, ci, 1));        \
+      v_.re = s * ((((wzam_ * zm_.re + wzap_ * zp_.re) + (wam_ * xm_.im + wab_ * c_.im)) + \
+                    (wyam_ * ym_.re + wyap_ * yp_.re)) -                                \
+                   (((wzam_ + wzap_) + (wam_ + wab_)) + (wyam_ + wyap_)) * c_.re);      \
+      v_.im = s * ((((wzbm_ * zm_.im + wzbp_ * zp_.im) + (wab_ * c_.re + wbp_ * xp_.re)) + \
+                    (wybm_ * ym_.im + wybp_ * yp_.im)) -                                \
+                   (((wzbm_ + wzbp_) + (wab_ + wbp_)) + (wybm_ + wybp_)) * c_.im);      \
+    } else if constexpr (A) {                                                           \
       /* div(c grad) (laplacians.hpp:158-218): face weights (c_a + c_b)/2 where the  \
          reference's flat-index neighbour exists, diagonal -sum of the weights */     \
       const int jj_ = P2D_ROW(yy_);                                                     \
@@ -550,7 +601,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
   // the look-ahead S planes whose ring slots are clear of the prologue's, and the J
   // planes, go out before the prologue's wait (p2d_dspre): a tile then starts after
   // one memory latency, not two
-  constexpr int DSPRE = p2d_dspre(J, A), PJ = J == 0 ? 0 : (LATE ? 1 : NP - 1);
+  constexpr int DSPRE = p2d_dspre(J, AK), PJ = J == 0 ? 0 : (LATE ? 1 : NP - 1);
 #pragma unroll
   for (int d = 0; d < DSPRE; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
   if constexpr (DSPRE > 0) {
@@ -561,13 +612,17 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
       for (int d = 0; d + 1 < NP; ++d) P2D_ISSUE_J(k0 + d, d);
     }
   }
-  wait_vm<DSPRE * p2d_nsd(A) + (DSPRE > 0 ? PJ * J : 0)>();
+  wait_vm<DSPRE * p2d_nsd(AK) + (DSPRE > 0 ? PJ * J : 0)>();
   raw_barrier();
   cplx lq0, lq1, le1;  // L S_J of planes k-1 and k (own row), halo values of plane k
   P2D_LAP(lq0, k0 - 1, w + 2, 0, 1, 2, x, lane, mi, pi);
   // A: c of the own cell at plane k-1 (its slot is reused before L^2 S_J of plane k needs it)
-  double cq0 = 0.0;
-  if constexpr (A && HZ) cq0 = P2D_CV(1, w + 2, lane);
+  double cq0 = 0.0, cq0b = 0.0;  // (pairs: cells a, b)
+  if constexpr (AK == 1 && HZ) cq0 = P2D_CV(1, w + 2, lane);
+  if constexpr (AK == 2 && HZ) {
+    cq0 = P2D_CV2(1, w + 2, lane, 0);
+    cq0b = P2D_CV2(1, w + 2, lane, 1);
+  }
   P2D_LROWS(k0, 1, 2, 3, 0, lq1, le1);
   raw_barrier();  // L ring slot 0 published; every wave is done with S slot 0 (plane k0-2)
 #pragma unroll
@@ -600,13 +655,13 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
     }
     // NLS_P2D_EARLY: issue first (the slots are free: S plane k-2 since the last
     // barrier, the wave's own J plane k-1 since its last step), then wait
-    if constexpr (p2d_early(J, A)) {
+    if constexpr (p2d_early(J, AK)) {
       P2D_ISSUE_S(k + DS + 2, sis);
       if constexpr (J > 0 && !LATE && !JREG) P2D_ISSUE_J(k + NP - 1, jis);
     }
-    wait_step<J, STW, A>(i);
+    wait_step<J, STW, AK>(i);
     raw_barrier();
-    if constexpr (!p2d_early(J, A)) {
+    if constexpr (!p2d_early(J, AK)) {
       P2D_ISSUE_S(k + DS + 2, sis);
       if constexpr (J > 0 && !LATE && !JREG) P2D_ISSUE_J(k + NP - 1, jis);
     }
@@ -616,7 +671,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
     P2D_LROWS(k + 1, sk, s1, s2, lsl ^ 1, ln, lne);
     // the J stored vectors of this cell and S_J itself
     if constexpr (J > 0 && !JREG) {
-      const cplx *jv = reinterpret_cast<const cplx *>(smem + p2d_off_j(J, A) + ((jr * J) * P2D_TR + w) * 1024);
+      const cplx *jv = reinterpret_cast<const cplx *>(smem + p2d_off_j(J, AK) + ((jr * J) * P2D_TR + w) * 1024);
 #pragma unroll
       for (int l = 0; l < J; ++l) sv[l] = jv[l * P2D_TR * 64 + lane];
       if constexpr (LATE) {
@@ -646,7 +701,29 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
       const cplx ym = Lr[(lsl * P2D_LR + w) * 64 + lane], yp = Lr[(lsl * P2D_LR + w + 2) * 64 + lane];
       const cplx zz = D2 ? cplx{0.0, 0.0} : lq0 + ln;
       cplx l2;
-      if constexpr (A) {
+      if constexpr (AK == 2) {
+        // cell pairs: per cell as in LROWS (a's x - 1 is xm's b, b's x + 1 is xp's a),
+        // z faces from c of planes k-1 (registers) and k+1
+        const int gk = z0 + k;
+        const double ca = P2D_CV2(sk, w + 2, lane, 0), cb = P2D_CV2(sk, w + 2, lane, 1);
+        const double wab = 0.5 * (ca + cb);
+        const double wam = p2d_face(x > 0, ca, P2D_CV2(sk, w + 2, mi, 1));
+        const double wbp = p2d_face(x + 1 < nx, cb, P2D_CV2(sk, w + 2, pi, 0));
+        const bool ymk = gk > 0 || y > 0, ypk = gk < nz - 1 || y < ny - 1;
+        const double wyam = p2d_face(ymk, ca, P2D_CV2(sk, w + 1, lane, 0));
+        const double wyap = p2d_face(ypk, ca, P2D_CV2(sk, w + 3, lane, 0));
+        const double wybm = p2d_face(ymk, cb, P2D_CV2(sk, w + 1, lane, 1));
+        const double wybp = p2d_face(ypk, cb, P2D_CV2(sk, w + 3, lane, 1));
+        const double wzam = p2d_face(gk > 0, ca, cq0), wzbm = p2d_face(gk > 0, cb, cq0b);
+        const double wzap = p2d_face(gk < nz - 1, ca, P2D_CV2(s1, w + 2, lane, 0));
+        const double wzbp = p2d_face(gk < nz - 1, cb, P2D_CV2(s1, w + 2, lane, 1));
+        l2.re = s * ((((wzam * lq0.re + wzap * ln.re) + (wam * xm.im + wab * l1.im)) + (wyam * ym.re + wyap * yp.re)) -
+                     (((wzam + wzap) + (wam + wab)) + (wyam + wyap)) * l1.re);
+        l2.im = s * ((((wzbm * lq0.im + wzbp * ln.im) + (wab * l1.re + wbp * xp.re)) + (wybm * ym.im + wybp * yp.im)) -
+                     (((wzbm + wzbp) + (wab + wbp)) + (wybm + wybp)) * l1.im);
+        cq0 = ca;
+        cq0b = cb;
+      } else if constexpr (A) {
         // the same operator at the same cell: c of the own row at planes k-1 (register),
         // k (x, y neighbours from the ring) and k+1
         const int gk = z0 + k;
@@ -713,6 +790,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A)) void k_p2d(cplx *__restric
 #undef P2D_ISSUE_J
 #undef P2D_LAP
 #undef P2D_CV
+#undef P2D_CV2
 #undef P2D_LROWS
   wait_vm<0>();  // the look-ahead DMAs land before the LDS is reused
   raw_barrier();

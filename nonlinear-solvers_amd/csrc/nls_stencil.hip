@@ -63,6 +63,8 @@ const void *tail_fn(bool complex_, int code) {
   switch (mode) {
 #if NLS_ANI
     case TAIL_KG_END: return tail_m<double, TAIL_KG_END>(M);
+    case TAIL_KG_END1: return tail_m<double, TAIL_KG_END1>(M);
+    case TAIL_COMBINE_W0: return tail_m<double, TAIL_COMBINE_W0>(M);
 #else
     case TAIL_SG_MID: return tail_m<double, TAIL_SG_MID>(M);
     case TAIL_GG_MID: return tail_m<double, TAIL_GG_MID>(M);

@@ -640,8 +640,8 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
   static_assert(M >= 3, "the stencil vector must not be W_0 (updated in place)");
   constexpr int J = M - 2;
   constexpr int NF = tail_nf(MODE);
-  constexpr bool KG = MODE == TAIL_KG_END;
-  constexpr int M2 = KG ? M : 1;
+  constexpr bool KG = MODE == TAIL_KG_END || MODE == TAIL_KG_END1;
+  constexpr int M2 = MODE == TAIL_KG_END ? M : 1;
   __shared__ S cf[NF][MMAX + 1];  // cf[f][k] for W_k (k <= J), cf[f][J+1] for L W_J
   __shared__ double c2[MMAX];     // KG: combination of the stored basis
   const KState *__restrict__ st = ta.st;
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
       else cf[f][k] = c.re;
     }
   }
-  if constexpr (KG) {
+  if constexpr (MODE == TAIL_KG_END) {
     for (int k = threadIdx.x; k < M; k += NTHREADS) c2[k] = ta.st2->fin[0][k].re;
   }
   __syncthreads();
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
     if constexpr (KG) {
       const double *__restrict__ s2 = W2 + q;
 #pragma unroll
-      for (int k = 0; k < M; ++k) {
+      for (int k = 0; k < M2; ++k) {
         b.w2[k] = ld_nt(s2);
         s2 += vs;
       }
@@ -696,7 +696,7 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
     } else if constexpr (MODE == TAIL_SG_END) {
       b.e0 = static_cast<const S *>(ta.u)[q];
       b.e1 = static_cast<const S *>(ta.up)[q];
-    } else if constexpr (MODE == TAIL_KG_END) {
+    } else if constexpr (KG) {
       b.e0 = static_cast<const S *>(ta.up)[q];
     } else if constexpr (MODE == TAIL_SEWI_END) {
       b.e0 = static_cast<const S *>(ta.u)[q];
@@ -733,10 +733,14 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
       const double uo = to_c(b.e0).re;
       static_cast<double *>(ta.u)[q] = to_c(b.e1).re + (ta.dt * ta.dt) * to_c(y[0]).re;
       static_cast<double *>(ta.up)[q] = uo;
-    } else if constexpr (MODE == TAIL_KG_END) {
+    } else if constexpr (KG) {
       double ys = 0.0;
+      if constexpr (MODE == TAIL_KG_END1) {
+        ys = b.w2[0];
+      } else {
 #pragma unroll
-      for (int k = 0; k < M2; ++k) ys += c2[k] * b.w2[k];
+        for (int k = 0; k < M2; ++k) ys += c2[k] * b.w2[k];
+      }
       const double uo = to_c(b.wk[0]).re;  // u is W_0 of the tail (cos) basis
       const double un = (to_c(y[0]).re * 2.0 - to_c(b.e0).re) + ys * (ta.dt * ta.dt);
       reinterpret_cast<double *>(W)[q] = un;

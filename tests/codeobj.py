@@ -131,9 +131,11 @@ def vmem_counts(ins) -> dict[str, int]:
 
 def p2d_loop_loads(J: int, A: int = 0, jreg: bool = False) -> dict[str, int]:
     """VMEM loads of one march step as the source issues them: 2 S rows (1 KiB each
-    + a 4-byte halo piece on 16 lanes), with A the two c rows (one 16-B DMA + one
-    4-byte halo piece), and the J rows (J-ring DMAs, or with jreg register loads)."""
-    d = {"global_load_lds_dwordx4": 2 + (0 if jreg else J) + (1 if A else 0), "global_load_lds_dword": 2 + (1 if A else 0)}
+    + a 4-byte halo piece on 16 lanes), with A = 1 the two c rows (one 16-B DMA + one
+    4-byte halo piece), with A = 2 (cell pairs) two c rows staged as S rows are, and
+    the J rows (J-ring DMAs, or with jreg register loads)."""
+    ca = {0: (0, 0), 1: (1, 1), 2: (2, 2)}[A]
+    d = {"global_load_lds_dwordx4": 2 + (0 if jreg else J) + ca[0], "global_load_lds_dword": 2 + ca[1]}
     if jreg:
         d["global_load_dwordx4"] = J
     return d
@@ -172,7 +174,7 @@ class P2dSchedule:
 
     def occ(self, J, A=0):
         if A:
-            return 2 if J <= self.OCC2A else 1
+            return 2 if A == 1 and J <= self.OCC2A else 1
         return self.OCC0 if J == 0 else (2 if J <= self.OCC2 or self.jreg(J) else 1)
 
     def ds(self, J, A=0):
@@ -194,7 +196,8 @@ class P2dSchedule:
         if J == 0 or self.jreg(J, A):
             return 0
         nsl = self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
-        off_j = nsl * self.SR * self.SRB + (nsl * self.CSB if A else 0) + 2 * self.LR * 1024
+        csb = self.SR * self.SRB if A == 2 else (self.CSB if A else 0)
+        off_j = nsl * self.SR * self.SRB + nsl * csb + 2 * self.LR * 1024
         avail = self.LDS // self.occ(J, A) - off_j - 2 * (J + 1) * 16
         return min(avail // (self.TR * 1024 * J), self.NPMAX)
 
@@ -210,7 +213,7 @@ class P2dSchedule:
         return pre if pre > 0 else self.ds(J, A)
 
     def after(self, J, stw, i, A=0):
-        DS, NP, NSD = self.ds(J, A), self.np(J, A), 6 if A else 4
+        DS, NP, NSD = self.ds(J, A), self.np(J, A), {0: 4, 1: 6, 2: 8}[A]
         early, late, jreg = self.early(J, A), self.late(J, A), self.jreg(J, A)
         n = lastS = lastJ = 0
         pre = self.dspre(J, A)
@@ -277,6 +280,7 @@ def check_p2d(funcs, meta, sched: P2dSchedule):
         if prm is None or name.endswith(".kd"):
             continue
         J, hz, d2, pr, A = prm
+        A = (2 if pr else 1) if A else 0  # the ring functions' anisotropic kind
         probs = []
         allv = vmem_counts(ins)
         bad = {k: v for k, v in allv.items() if k.startswith(("scratch_", "buffer_", "flat_"))}

@@ -32,6 +32,7 @@ def test_every_p2d_instantiation_found(p2d_results):
     got = {(r["J"], r["HZ"], r["D2"], r["PR"], r["A"]) for _n, _p, r in p2d_results}
     want = {(J, hz, d2, pr, 0) for J in range(0, 16, 2) for hz in (0, 1) for d2, pr in ((0, 0), (1, 0), (1, 1))}
     want |= {(J, hz, 0, 0, 1) for J in range(0, 24, 2) for hz in (0, 1)}  # the G2 operator (nls_pass2a.hip)
+    want |= {(J, hz, 0, 1, 2) for J in range(0, 16, 2) for hz in (0, 1)}  # G2 on real cell pairs (Klein-Gordon)
     assert got == want
 
 

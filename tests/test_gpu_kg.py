@@ -166,3 +166,79 @@ def test_kg_driver_matches_oracle(tmp_path, dim):
     for k in range(1, ns):
         assert rel_l2(tu[k].ravel(), eu[k]) <= TOL_TRAJ, k
         assert rel_l2(tv[k].ravel(), ev[k]) <= TOL_V, k
+
+
+def _ran_pass2(s):
+    """The s-step passes time their launches at J = 0, 2, ...; the one-vector path at every j."""
+    cnt = s.timing()["update_count"]
+    return cnt[0] > 0 and cnt[1] == 0
+
+
+@pytest.mark.parametrize("nx,ny,nz,m,kz", [(12, 12, 12, 10, None), (140, 8, 9, 10, None), (22, 20, 16, 10, "4"),
+                                           (64, 16, 10, 16, None), (18, 4, 7, 6, "2"), (30, 12, 8, 3, None)])
+def test_kg_pair_passes_match_oracle(monkeypatch, nx, ny, nz, m, kz):
+    """3D KG on the s-step passes k_p2d<.., PR, A> (real cells as pairs, div(c grad)):
+    ragged x tiles (140 = 70 pairs), one and several z chunks, m = 3 .. 16; against the
+    oracle and against the one-vector path (NLS_PASS2=0) of the same handle shape."""
+    if kz:
+        monkeypatch.setenv("NLS_P2_KZ", kz)
+    L, dt, steps = 3.0, 5e-3, 8
+    dx = 2 * L / (nx - 1)
+    u0, v0, mf, c = kg_fields(3, nx, ny, nz, L, seed=4)
+    up0 = u0 - dt * v0
+    ru, _, rv = O.kg_steps(O.grid(3, nx, ny, nz, dx, dx), c, mf, u0, up0, dt, steps, m, bc=True)
+    res = {}
+    for p2 in ("1", "0"):
+        monkeypatch.setenv("NLS_PASS2", p2)
+        with kg_solver(3, nx, ny, nz, dx, m=m) as s:
+            s.set_coefficients(mf, c)
+            s.set_sg_state(u0, up0)
+            s.set_timing(True)
+            for _ in range(steps):
+                s.step(dt, 1)
+                s.apply_bc()
+            assert _ran_pass2(s) == (p2 == "1")
+            res[p2] = (s.get_field(), s.get_sg_velocity(dt))
+    for u, v in res.values():
+        assert rel_l2(u, ru) <= TOL_TRAJ
+        assert rel_l2(v, rv) <= TOL_V
+    assert rel_l2(res["1"][0], res["0"][0]) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("n,nranks", [(16, 2), (16, 3)])
+def test_kg_pair_passes_slabs_match_single_rank(n, nranks):
+    """The cell-pair passes on z-slabs (two ghost planes; in-process local transport)."""
+    L, dt, steps = 3.0, 5e-3, 5
+    dx = 2 * L / (n - 1)
+    u0, v0, mf, c = kg_fields(3, n, n, n, L, seed=5)
+    up0 = u0 - dt * v0
+    P = n * n
+    ref = O.kg_steps(O.grid(3, n, n, n, dx, dx), c, mf, u0, up0, dt, steps, 10, bc=True)[0]
+    grp = nls_amd.Group(nranks)
+    out = [None] * nranks
+    ran = [None] * nranks
+    err = []
+
+    def work(r):
+        try:
+            s = kg_solver(3, n, n, n, dx, device=0, nranks=nranks, rank=r, group=grp)
+            sl = slice(s.z0 * P, (s.z0 + s.nzl) * P)
+            s.set_coefficients(mf[sl], c[sl])
+            s.set_sg_state(u0[sl], up0[sl])
+            s.set_timing(True)
+            for _ in range(steps):
+                s.step(dt, 1)
+                s.apply_bc()
+            out[r] = s.get_field()
+            ran[r] = _ran_pass2(s)
+            s.close()
+        except Exception as e:  # noqa: BLE001
+            err.append((r, e))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    grp.close()
+    assert not err, err
+    assert all(ran)
+    assert rel_l2(np.concatenate(out), ref) <= TOL_TRAJ
