@@ -744,7 +744,9 @@ int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
 // at kz 32 vs 4.89 at 256; the J-ring passes lose: J = 12 6.45 vs 5.80; round 4,
 // profiles/r04/p2ab_512.txt)
 int p2_kz(const nls_handle *h, int J) {
-  return !h->p2_ani && h->cfg.dim == 3 && pass2_jreg(J) ? std::min(h->p2kz, h->p2kzj) : h->p2kz;
+  // (the G2 register-row pass at J = 6 keeps the general depth: 256^3 0.473 ms at kz 128
+  // vs 0.491 at 32, profiles/r04/g2_probe_jreg.txt)
+  return h->cfg.dim == 3 && !h->p2_ani && pass2_jreg(J, 0) ? std::min(h->p2kz, h->p2kzj) : h->p2kz;
 }
 int p2_grid(const nls_handle *h, int J = 0) {
   if (h->p2reg) return h->p2mgrid[J];

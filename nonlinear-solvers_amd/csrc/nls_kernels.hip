@@ -822,7 +822,7 @@ const void *kernel_sg_end(int M) {
 // two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp): the LDS-DMA pass
 // k_p2d at even J <= P2D_JMAX; d2: a 2D grid as planes of 4 rows; pr: a real 2D
 // field as pairs of cells
-bool pass2_jreg(int J) { return p2d_jreg(J); }
+bool pass2_jreg(int J, int akind) { return p2d_jreg(J, akind); }
 const void *kernel_pass2(int J, bool hz, bool d2, bool pr) {
   switch (J) {
 #define X(J)                                                                                       \

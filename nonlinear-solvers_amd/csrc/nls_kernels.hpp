@@ -61,7 +61,7 @@ const void *kernel_colsum();
 // two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp; 3D isotropic complex, single rank)
 //   pass2 : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* zbuf, int poff)
 const void *kernel_pass2(int J, bool hz, bool d2 = false, bool pr = false);  // hz: also Z (k_p2d)
-bool pass2_jreg(int J);  // k_p2d<J> reads its J rows into registers (p2d_jreg): shorter tiles pay
+bool pass2_jreg(int J, int akind = 0);  // k_p2d<J> reads its J rows into registers (p2d_jreg; akind: 1 G2, 2 G2 pairs)
 constexpr int P2D_WAVE_XO = 64, P2D_ROWS = 4, P2D_MAXJ = 14, P2D_MAXJ_A = 22, P2D_MAXJ_A2 = 14;  // == P2D_XO, P2D_TR, P2D_JMAX, P2D_JMAX_A, P2D_JMAX_A2
 //   p2m    : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* lbuf, int poff)
 //            -- the register two-vector pass (nls_pass2g.hpp; lbuf = y = L S_J at local planes

@@ -103,8 +103,15 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 // took 256 VGPRs and scratch; half of them loaded after the S issue (SGPR-walked
 // addresses) fit but ran slower than the ring (6.16 vs 6.06 ms; round 4,
 // profiles/r04/p2ab_512.txt).
+#ifndef NLS_P2A_JREG_MINJ
+#define NLS_P2A_JREG_MINJ 6  // the complex anisotropic passes (G2): register rows, two workgroups per CU
+#endif
+#ifndef NLS_P2A_JREG_MAXJ
+#define NLS_P2A_JREG_MAXJ 6  // J = 8 with Z: 256 VGPRs and scratch
+#endif
 __host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
-  return NLS_P2D_JREG && !A && J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ;
+  return NLS_P2D_JREG && (A == 0 ? J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ
+                                 : A == 1 && J >= NLS_P2A_JREG_MINJ && J <= NLS_P2A_JREG_MAXJ);
 }
 // Workgroups per CU: two where the registers (<= 256 per lane) and the rings
 // (<= 80 KiB) allow, so the second workgroup's waves cover the first's barriers
@@ -119,7 +126,7 @@ __host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
 #define NLS_P2D_OCC0 3  // workgroups per CU of the J = 0 pass (S look-ahead 1; 512^3: 1.40 vs 1.61 ms at 2)
 #endif
 __host__ __device__ constexpr int p2d_occ(int J, int A = 0) {
-  return A ? (A == 1 && J <= NLS_P2A_OCC2_MAXJ ? 2 : 1)  // pairs: the c ring as large as S's
+  return A ? (A == 1 && (J <= NLS_P2A_OCC2_MAXJ || p2d_jreg(J, A)) ? 2 : 1)  // pairs: the c ring as large as S's
            : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ || p2d_jreg(J) ? 2 : 1));
 }
 // S ring: the planes k .. k+2 being read, DS planes of look-ahead and the slot of

@@ -162,6 +162,7 @@ class P2dSchedule:
         self.PRE_LA = define("NLS_P2D_PRE_LA")
         self.JREG = define("NLS_P2D_JREG")
         self.JREG_MINJ, self.JREG_MAXJ = define("NLS_P2D_JREG_MINJ"), define("NLS_P2D_JREG_MAXJ")
+        self.JREGA_MINJ, self.JREGA_MAXJ = define("NLS_P2A_JREG_MINJ"), define("NLS_P2A_JREG_MAXJ")
         self.SR, self.SRB, self.LR = const("P2D_SR"), const("P2D_SRB"), const("P2D_LR")
         self.CSB = const("P2D_CSB")
         self.LDS = 160 * 1024
@@ -170,11 +171,15 @@ class P2dSchedule:
 
     def jreg(self, J, A=0):
         """J rows loaded into registers (no J ring)."""
-        return bool(self.JREG) and not A and self.JREG_MINJ <= J <= self.JREG_MAXJ
+        if not self.JREG:
+            return False
+        if A == 0:
+            return self.JREG_MINJ <= J <= self.JREG_MAXJ
+        return A == 1 and self.JREGA_MINJ <= J <= self.JREGA_MAXJ
 
     def occ(self, J, A=0):
         if A:
-            return 2 if A == 1 and J <= self.OCC2A else 1
+            return 2 if A == 1 and (J <= self.OCC2A or self.jreg(J, A)) else 1
         return self.OCC0 if J == 0 else (2 if J <= self.OCC2 or self.jreg(J) else 1)
 
     def ds(self, J, A=0):
