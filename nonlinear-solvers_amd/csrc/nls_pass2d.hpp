@@ -84,6 +84,9 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 #ifndef NLS_P2D_PRE_LA
 #define NLS_P2D_PRE_LA 1      // issue the look-ahead before the prologue's wait (p2d_dspre)
 #endif
+#ifndef NLS_P2D_EXT1
+#define NLS_P2D_EXT1 1        // the tile's 8 x-halo L values computed by one wave (P2D_LROWS)
+#endif
 #ifndef NLS_P2D_JREG
 #define NLS_P2D_JREG 1        // isotropic passes from J = NLS_P2D_JREG_MINJ: J rows in registers (p2d_jreg)
 #endif
@@ -149,7 +152,9 @@ __host__ __device__ constexpr int p2d_off_c_ring(int J, int A = 0) { return p2d_
 __host__ __device__ constexpr int p2d_off_l(int J, int A = 0) {
   return p2d_off_c_ring(J, A) + p2d_nsl(J, A) * p2d_csb(A);
 }
-__host__ __device__ constexpr int p2d_off_j(int J, int A = 0) { return p2d_off_l(J, A) + 2 * P2D_LR * 1024; }
+// the L ring: [2][P2D_LR] rows of 64, then [2][P2D_TR][2] x-halo values (x0-1, x0+64)
+constexpr int P2D_LXB = 2 * P2D_TR * 2 * 16;
+__host__ __device__ constexpr int p2d_off_j(int J, int A = 0) { return p2d_off_l(J, A) + 2 * P2D_LR * 1024 + P2D_LXB; }
 __host__ __device__ constexpr int p2d_avail(int J, int A = 0) {
   return P2D_LDS / p2d_occ(J, A) - p2d_off_j(J, A) - 2 * (J + 1) * 16;
 }
@@ -358,6 +363,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   const cplx *Sr = reinterpret_cast<const cplx *>(smem);             // [NSL][P2D_SR][RW]
   const double *Cr = reinterpret_cast<const double *>(smem + p2d_off_c_ring(J, AK));  // A: [NSL][p2d_csb/8]
   cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J, AK));       // [2][P2D_LR][64]
+  cplx *Lx = Lr + 2 * P2D_LR * 64;                                     // [2][P2D_TR][2]
   cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J, AK));       // [J+1]
   cplx *cZ = cX + (J + 1);                                           // [J+1]
   // w through readfirstlane: wave-uniform for the compiler too, so row and plane
@@ -431,8 +437,10 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // the halo cells 65 / 66 at the tile edges); extra pass lane 0 -> x0-1, lane 1
   // -> x0+64 (row indices 65 / 66, neighbours 64,0 / 63,67)
   const int mi = lane > 0 ? lane - 1 : 65, pi = lane < 63 ? lane + 1 : 66;
-  const int xe = lane == 1 ? x0 + 64 : x0 - 1;
-  const int eci = lane == 1 ? 66 : 65, emi = lane == 1 ? 63 : 64, epi = lane == 1 ? 67 : 0;
+  // (EXT1: lane 2r + h -> tile row r, h as above)
+  const int xe = (lane & 1) ? x0 + 64 : x0 - 1;
+  const int eci = (lane & 1) ? 66 : 65, emi = (lane & 1) ? 63 : 64, epi = (lane & 1) ? 67 : 0;
+  const int xr = 2 + ((lane >> 1) & (P2D_TR - 1));
   // (macros, not lambdas capturing by reference: hipcc kept such captures on the
   // stack, and every scratch access is a VMEM op that breaks the vmcnt counting)
 #define P2D_PLANE(p, yy) (z0 + ((yy) < 0 ? (p) - 1 : ((yy) >= ny ? (p) + 1 : (p))))  // global
@@ -581,16 +589,25 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     dst = ok_ ? v_ : cplx{0.0, 0.0};                                                    \
   } while (0)
   // per plane a wave computes L S_J of its own row (main lanes, kept in a
-  // register; extra pass: the two x-halo values, lanes 0 / 1), and on the edge
-  // waves the tile's halo row (L row 0 on wave 0, P2D_LR-1 on wave 3); the main
-  // rows go to the L ring for the y neighbours of the other waves' L^2 S_J
+  // register); the tile's halo rows (L rows 0 and P2D_LR-1) and its 8 x-halo values
+  // (x0-1, x0+64 of each row) are spread over the waves, one extra stencil each
+  // (EXT1: wave 0 the x-halo values on lanes 0..7 into Lx, waves 1 / 2 the halo
+  // rows, wave 3 none: at most two stencils per wave and step instead of three;
+  // NLS_P2D_EXT1 = 0: every wave its own two x-halo values in a register, the halo
+  // rows on waves 0 / 3); the main rows go to the L ring for the y neighbours of
+  // the other waves' L^2 S_J
 #define P2D_LROWS(p, sm, sc, sp, slot, own, ext)                                        \
   do {                                                                                  \
     P2D_LAP(own, p, w + 2, sm, sc, sp, x, lane, mi, pi);                                \
-    P2D_LAP(ext, p, w + 2, sm, sc, sp, xe, eci, emi, epi);                              \
+    if constexpr (!NLS_P2D_EXT1) P2D_LAP(ext, p, w + 2, sm, sc, sp, xe, eci, emi, epi); \
     Lr[((slot) * P2D_LR + w + 1) * 64 + lane] = own;                                    \
-    if (w == 0 || w == P2D_TR - 1) {                                                    \
-      const int er_ = w == 0 ? 0 : P2D_LR - 1;                                          \
+    if (NLS_P2D_EXT1 && w == 0) {                                                       \
+      cplx e_;                                                                          \
+      P2D_LAP(e_, p, xr, sm, sc, sp, xe, eci, emi, epi);                                \
+      if (lane < 2 * P2D_TR) Lx[(slot) * 2 * P2D_TR + lane] = e_;                       \
+    }                                                                                   \
+    if (NLS_P2D_EXT1 ? (w == 1 || w == 2) : (w == 0 || w == P2D_TR - 1)) {              \
+      const int er_ = (NLS_P2D_EXT1 ? w == 1 : w == 0) ? 0 : P2D_LR - 1;                \
       cplx e_;                                                                          \
       P2D_LAP(e_, p, er_ + 1, sm, sc, sp, x, lane, mi, pi);                             \
       Lr[((slot) * P2D_LR + er_) * 64 + lane] = e_;                                     \
@@ -621,7 +638,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   }
   wait_vm<DSPRE * p2d_nsd(AK) + (DSPRE > 0 ? PJ * J : 0)>();
   raw_barrier();
-  cplx lq0, lq1, le1;  // L S_J of planes k-1 and k (own row), halo values of plane k
+  cplx lq0, lq1, le1 = {0.0, 0.0};  // L S_J of planes k-1 and k (own row), (!EXT1) halo values of plane k
   P2D_LAP(lq0, k0 - 1, w + 2, 0, 1, 2, x, lane, mi, pi);
   // A: c of the own cell at plane k-1 (its slot is reused before L^2 S_J of plane k needs it)
   double cq0 = 0.0, cq0b = 0.0;  // (pairs: cells a, b)
@@ -674,7 +691,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     }
     const int s1 = sk + 1 == NSL ? 0 : sk + 1, s2 = s1 + 1 == NSL ? 0 : s1 + 1;
     // L S_J of plane k+1: own row (register) + halo values, shared rows into L slot lsl^1
-    cplx ln, lne;
+    cplx ln, lne = {0.0, 0.0};
     P2D_LROWS(k + 1, sk, s1, s2, lsl ^ 1, ln, lne);
     // the J stored vectors of this cell and S_J itself
     if constexpr (J > 0 && !JREG) {
@@ -697,14 +714,20 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     cplx Z = {0.0, 0.0};
     if constexpr (HZ) {
       // x neighbours: lanes i-1 / i+1 by DPP, the tile-edge ones from the halo values
-      // (x0-1 on lane 0 of le1, x0+64 on its lane 1)
+      // (EXT1: Lx of the wave's row; else x0-1 on lane 0 of le1, x0+64 on its lane 1)
       cplx xm = lane_prev(l1), xp = lane_next(l1);
-      const cplx er = {__hiloint2double(__builtin_amdgcn_readlane(__double2hiint(le1.re), 1),
-                                        __builtin_amdgcn_readlane(__double2loint(le1.re), 1)),
-                       __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(le1.im), 1),
-                                        __builtin_amdgcn_readlane(__double2loint(le1.im), 1))};
-      if (lane == 0) xm = le1;
-      if (lane == 63) xp = er;
+      if constexpr (NLS_P2D_EXT1) {
+        const cplx hm = Lx[lsl * 2 * P2D_TR + 2 * w], hp = Lx[lsl * 2 * P2D_TR + 2 * w + 1];
+        if (lane == 0) xm = hm;
+        if (lane == 63) xp = hp;
+      } else {
+        const cplx er = {__hiloint2double(__builtin_amdgcn_readlane(__double2hiint(le1.re), 1),
+                                          __builtin_amdgcn_readlane(__double2loint(le1.re), 1)),
+                         __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(le1.im), 1),
+                                          __builtin_amdgcn_readlane(__double2loint(le1.im), 1))};
+        if (lane == 0) xm = le1;
+        if (lane == 63) xp = er;
+      }
       const cplx ym = Lr[(lsl * P2D_LR + w) * 64 + lane], yp = Lr[(lsl * P2D_LR + w + 2) * 64 + lane];
       const cplx zz = D2 ? cplx{0.0, 0.0} : lq0 + ln;
       cplx l2;

@@ -202,7 +202,7 @@ class P2dSchedule:
             return 0
         nsl = self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
         csb = self.SR * self.SRB if A == 2 else (self.CSB if A else 0)
-        off_j = nsl * self.SR * self.SRB + nsl * csb + 2 * self.LR * 1024
+        off_j = nsl * self.SR * self.SRB + nsl * csb + 2 * self.LR * 1024 + 2 * self.TR * 2 * 16  # + P2D_LXB
         avail = self.LDS // self.occ(J, A) - off_j - 2 * (J + 1) * 16
         return min(avail // (self.TR * 1024 * J), self.NPMAX)
 
