@@ -110,7 +110,7 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 #define NLS_P2A_JREG_MINJ 6  // the complex anisotropic passes (G2): register rows, two workgroups per CU
 #endif
 #ifndef NLS_P2A_JREG_MAXJ
-#define NLS_P2A_JREG_MAXJ 6  // J = 8 with Z: 256 VGPRs and scratch
+#define NLS_P2A_JREG_MAXJ 8  // J = 10 with Z: 255 VGPRs and scratch
 #endif
 __host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
   return NLS_P2D_JREG && (A == 0 ? J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ
