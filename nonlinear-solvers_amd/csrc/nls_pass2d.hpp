@@ -87,6 +87,9 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 #ifndef NLS_P2D_EXT1
 #define NLS_P2D_EXT1 1        // the tile's 8 x-halo L values computed by one wave (P2D_LROWS)
 #endif
+#ifndef NLS_P2D_VCOEF_MAXJ
+#define NLS_P2D_VCOEF_MAXJ 8  // the march's uniform f64 operands in VGPRs up to this J
+#endif
 #ifndef NLS_P2D_JREG
 #define NLS_P2D_JREG 1        // isotropic passes from J = NLS_P2D_JREG_MINJ: J rows in registers (p2d_jreg)
 #endif
@@ -411,8 +414,18 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     cX[l] = ps->aX[l];
     cZ[l] = ps->aZ[l];
   }
-  const cplx bX1 = ps->bX1, bZ1 = ps->bZ1, bZ2 = ps->bZ2;
-  const double s = g.s, sdi = g.sd_in, sdb = g.sd_bd;
+  cplx bX1 = ps->bX1, bZ1 = ps->bZ1, bZ2 = ps->bZ2;
+  double s = g.s, sdi = g.sd_in, sdb = g.sd_bd;
+  // the anisotropic passes up to J = NLS_P2D_VCOEF_MAXJ keep the uniform f64 operands
+  // of the march in VGPRs: as SGPRs (18 of them) they were among the values spilled to
+  // VGPR lanes, a v_readlane / v_writelane per use (KG 256^3 passes 2.38 -> 2.26 ms per
+  // step, G2 neutral; above J = 8 the VGPRs are the scarcer).  The isotropic passes
+  // lost with it (512^3: 24.3 -> 25.3 ms of passes, fewer instructions notwithstanding;
+  // profiles/r04/ab_vcoef.txt)
+  if constexpr (AK > 0 && J <= NLS_P2D_VCOEF_MAXJ) {
+    asm volatile("" : "+v"(bX1.re), "+v"(bX1.im), "+v"(bZ1.re), "+v"(bZ1.im), "+v"(bZ2.re), "+v"(bZ2.im));
+    asm volatile("" : "+v"(s), "+v"(sdi), "+v"(sdb));
+  }
   const int64_t P16 = (int64_t)P * 16;
   const char *__restrict__ SJb = reinterpret_cast<const char *>(W + (int64_t)J * vs);
   cplx *__restrict__ Xo = W + (int64_t)(J + 1) * vs;
@@ -453,37 +466,43 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
 // PR: the diagonals of the pair's first / second cell
 #define P2D_DIAGA(xx, j, kk) ((((xx) == 0) | P2D_BYZ(j, kk)) ? sdb : sdi)
 #define P2D_DIAGB(xx, j, kk) ((((xx) == nx - 1) | P2D_BYZ(j, kk)) ? sdb : sdi)
+  // this wave's two staged S rows yy = y0 - 2 + 2w + r (r = 0, 1): the plane shift of
+  // the y-wrap (rows -2, -1 are the previous plane's last, ny, ny+1 the next plane's
+  // first), the issue planes p for which the row's global plane lies in the grid, its
+  // local plane in the allocation (ghosts) and p <= k1 + 1 (not past the tile's last
+  // needed plane), and the row's byte offset: computed once per tile, not per DMA
+  const int s_yy0 = y0 - 2 + 2 * w, s_yy1 = s_yy0 + 1;
+  const int s_dr0 = s_yy0 < 0 ? -1 : (s_yy0 >= ny ? 1 : 0), s_dr1 = s_yy1 < 0 ? -1 : (s_yy1 >= ny ? 1 : 0);
+  const int s_lo0 = max(-z0 - s_dr0, -P2D_GHOST - s_dr0), s_lo1 = max(-z0 - s_dr1, -P2D_GHOST - s_dr1);
+  const int s_hi0 = min(min(nz - z0 - s_dr0, nzl + P2D_GHOST - s_dr0) - 1, k1 + 1);
+  const int s_hi1 = min(min(nz - z0 - s_dr1, nzl + P2D_GHOST - s_dr1) - 1, k1 + 1);
+  const int64_t s_yo0 = (int64_t)s_yy0 * nx * 16, s_yo1 = s_yo0 + (int64_t)nx * 16;
   // DMA this wave's two S_J rows of plane p into ring slot sl: the 64 aligned
   // cells and the 4 halo cells (the zero row outside the grid and past the
   // tile's last needed plane)
 #define P2D_ISSUE_S(p, sl)                                                              \
   do {                                                                                  \
     const int p_ = (p);                                                                 \
+    const int64_t pb_ = (int64_t)p_ * P16;                                              \
     char *dst_ = smem + ((sl) * P2D_SR + 2 * w) * P2D_SRB;                              \
     _Pragma("unroll") for (int r_ = 0; r_ < 2; ++r_) {                                  \
-      const int yy_ = y0 - 2 + 2 * w + r_, kk_ = P2D_PLANE(p_, yy_), lp_ = kk_ - z0;    \
-      /* global plane in the grid, local plane inside the allocation (ghosts), and   \
-         not past the tile's last needed plane */                                     \
-      const bool ok_ = kk_ >= 0 && kk_ < nz && lp_ >= -P2D_GHOST && lp_ < nzl + P2D_GHOST && \
-                       p_ <= k1 + 1;                                                    \
-      const char *b_ = ok_ ? SJb + (p_ * P16 + (int64_t)yy_ * nx * 16)                  \
-                           : reinterpret_cast<const char *>(zbuf);                      \
+      /* the row inside the grid and the allocation and needed (s_lo / s_hi) */       \
+      const bool ok_ = p_ >= (r_ ? s_lo1 : s_lo0) && p_ <= (r_ ? s_hi1 : s_hi0);        \
+      const int64_t o_ = pb_ + (r_ ? s_yo1 : s_yo0);                                    \
+      const char *b_ = ok_ ? SJb + o_ : reinterpret_cast<const char *>(zbuf);           \
+      asm volatile("" : "+s"(b_)); /* one select, not a DMA per branch */               \
       dma16(b_, xoff, dst_ + r_ * P2D_SRB, 0);                                          \
       if (lane < 16) dma4(b_, hoff, dst_ + r_ * P2D_SRB + 1024);                        \
-    }                                                                                   \
-    if constexpr (AK == 2) {                                                            \
-      /* cell pairs: the c rows of the same two S rows, staged as S rows are */       \
-      char *cd_ = smem + p2d_off_c_ring(J, AK) + ((sl) * P2D_SR + 2 * w) * P2D_SRB;     \
-      _Pragma("unroll") for (int r_ = 0; r_ < 2; ++r_) {                                \
-        const int yy_ = y0 - 2 + 2 * w + r_, kk_ = P2D_PLANE(p_, yy_), lp_ = kk_ - z0;  \
-        const bool ok_ = kk_ >= 0 && kk_ < nz && lp_ >= -P2D_GHOST && lp_ < nzl + P2D_GHOST && \
-                         p_ <= k1 + 1;                                                  \
-        const char *b_ = ok_ ? Cg + (p_ * P16 + (int64_t)yy_ * nx * 16)                 \
-                             : reinterpret_cast<const char *>(zbuf);                    \
-        dma16(b_, xoff, cd_ + r_ * P2D_SRB, 0);                                         \
-        if (lane < 16) dma4(b_, hoff, cd_ + r_ * P2D_SRB + 1024);                       \
+      if constexpr (AK == 2) {                                                          \
+        /* cell pairs: the c row of the same S row, staged as S rows are */           \
+        char *cd_ = smem + p2d_off_c_ring(J, AK) + ((sl) * P2D_SR + 2 * w + r_) * P2D_SRB; \
+        const char *c_ = ok_ ? Cg + o_ : reinterpret_cast<const char *>(zbuf);          \
+        asm volatile("" : "+s"(c_));                                                    \
+        dma16(c_, xoff, cd_, 0);                                                        \
+        if (lane < 16) dma4(c_, hoff, cd_ + 1024);                                      \
       }                                                                                 \
-    } else if constexpr (A) {                                                           \
+    }                                                                                   \
+    if constexpr (AK == 1) {                                                           \
       /* the c rows of the same two S rows: lanes 0..31 / 32..63 two cells each of   \
          row 2w / 2w+1, then their halo cells on lanes 0..15 (8 lanes x 4 B a row) */ \
       char *cd_ = smem + p2d_off_c_ring(J, AK) + (sl) * P2D_CSB;                        \
