@@ -87,6 +87,9 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 #ifndef NLS_P2D_EXT1
 #define NLS_P2D_EXT1 1        // the tile's 8 x-halo L values computed by one wave (P2D_LROWS)
 #endif
+#ifndef NLS_P2D_WCACHE
+#define NLS_P2D_WCACHE 1      // anisotropic passes: L^2's face weights from the L S_J of the step before
+#endif
 #ifndef NLS_P2D_VCOEF_MAXJ
 #define NLS_P2D_VCOEF_MAXJ 8  // the march's uniform f64 operands in VGPRs up to this J
 #endif
@@ -356,6 +359,12 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   static_assert(!(A && D2), "the anisotropic pass is 3D");
   constexpr int DS = p2d_ds(J, AK), NSL = p2d_nsl(J, AK), NP = p2d_np(J, AK);
   constexpr bool LATE = p2d_late(J, AK), JREG = p2d_jreg(J, AK);
+  // WC: the own row's face weights div(c grad) needs at plane k were computed with its
+  // L S_J one step earlier (same c, same conditions, so the same bits): kept in
+  // registers (nwc -> cwc) instead of recomputed from the c ring by L^2 S_J
+  constexpr bool WC = NLS_P2D_WCACHE && A && HZ && (p2d_occ(J, AK) == 1 || J <= 6);  // (J = 8 at two per CU: scratch)
+  constexpr int NWC = AK == 2 ? 13 : 7;
+  double nwc[NWC], cwc[NWC];
   constexpr int STW = HZ ? 2 : 1;            // stores per step
   // columns: gX[0..J], (HZ: gZ[0..J], xx, xz, zz | xx); J = 0 also ||S_0||^2 (the
   // blind start, k_p2coef mode 2)
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // L S_J at plane p, S tile row tr (yy = y0 - 2 + tr), x position xx with row
   // indices ci (centre), mi_ / pi_ (x - 1 / x + 1), from ring slots sm, sc, sp
   // (planes p-1, p, p+1)
-#define P2D_LAP(dst, p, tr, sm, sc, sp, xx, ci, mi_, pi_)                               \
+#define P2D_LAP(dst, p, tr, sm, sc, sp, xx, ci, mi_, pi_, ws)                           \
   do {                                                                                  \
     const int p_ = (p), tr_ = (tr), xx_ = (xx);                                         \
     const cplx *Sm_ = Sr + ((sm) * P2D_SR + tr_) * RW;                                  \
@@ -584,6 +593,13 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
       v_.im = s * ((((wzbm_ * zm_.im + wzbp_ * zp_.im) + (wab_ * c_.re + wbp_ * xp_.re)) + \
                     (wybm_ * ym_.im + wybp_ * yp_.im)) -                                \
                    (((wzbm_ + wzbp_) + (wab_ + wbp_)) + (wybm_ + wybp_)) * c_.im);      \
+      if constexpr (ws && WC) {                                                         \
+        nwc[0] = wab_; nwc[1] = wam_; nwc[2] = wbp_; nwc[3] = wyam_; nwc[4] = wyap_;    \
+        nwc[5] = wybm_; nwc[6] = wybp_; nwc[7] = wzam_; nwc[8] = wzap_; nwc[9] = wzbm_; \
+        nwc[10] = wzbp_;                                                                \
+        nwc[11] = ((wzam_ + wzap_) + (wam_ + wab_)) + (wyam_ + wyap_);                  \
+        nwc[12] = ((wzbm_ + wzbp_) + (wab_ + wbp_)) + (wybm_ + wybp_);                  \
+      }                                                                                 \
     } else if constexpr (A) {                                                           \
       /* div(c grad) (laplacians.hpp:158-218): face weights (c_a + c_b)/2 where the  \
          reference's flat-index neighbour exists, diagonal -sum of the weights */     \
@@ -595,6 +611,10 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
       const double wyp_ = p2d_face(kk_ < nz - 1 || jj_ < ny - 1, cc_, P2D_CV(sc, tr_ + 1, ci)); \
       const double wzm_ = p2d_face(kk_ > 0, cc_, P2D_CV(sm, tr_, ci));                    \
       const double wzp_ = p2d_face(kk_ < nz - 1, cc_, P2D_CV(sp, tr_, ci));               \
+      if constexpr (ws && WC) {                                                         \
+        nwc[0] = wxm_; nwc[1] = wxp_; nwc[2] = wym_; nwc[3] = wyp_; nwc[4] = wzm_;      \
+        nwc[5] = wzp_; nwc[6] = ((wzm_ + wzp_) + (wxm_ + wxp_)) + (wym_ + wyp_);         \
+      }                                                                                 \
       v_ = s * ((((wzm_ * zm_ + wzp_ * zp_) + (wxm_ * xm_ + wxp_ * xp_)) + (wym_ * ym_ + wyp_ * yp_)) - \
                 (((wzm_ + wzp_) + (wxm_ + wxp_)) + (wym_ + wyp_)) * c_);                 \
     } else if constexpr (PR) {                                                          \
@@ -617,18 +637,18 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // the other waves' L^2 S_J
 #define P2D_LROWS(p, sm, sc, sp, slot, own, ext)                                        \
   do {                                                                                  \
-    P2D_LAP(own, p, w + 2, sm, sc, sp, x, lane, mi, pi);                                \
-    if constexpr (!NLS_P2D_EXT1) P2D_LAP(ext, p, w + 2, sm, sc, sp, xe, eci, emi, epi); \
+    P2D_LAP(own, p, w + 2, sm, sc, sp, x, lane, mi, pi, 1);                             \
+    if constexpr (!NLS_P2D_EXT1) P2D_LAP(ext, p, w + 2, sm, sc, sp, xe, eci, emi, epi, 0); \
     Lr[((slot) * P2D_LR + w + 1) * 64 + lane] = own;                                    \
     if (NLS_P2D_EXT1 && w == 0) {                                                       \
       cplx e_;                                                                          \
-      P2D_LAP(e_, p, xr, sm, sc, sp, xe, eci, emi, epi);                                \
+      P2D_LAP(e_, p, xr, sm, sc, sp, xe, eci, emi, epi, 0);                             \
       if (lane < 2 * P2D_TR) Lx[(slot) * 2 * P2D_TR + lane] = e_;                       \
     }                                                                                   \
     if (NLS_P2D_EXT1 ? (w == 1 || w == 2) : (w == 0 || w == P2D_TR - 1)) {              \
       const int er_ = (NLS_P2D_EXT1 ? w == 1 : w == 0) ? 0 : P2D_LR - 1;                \
       cplx e_;                                                                          \
-      P2D_LAP(e_, p, er_ + 1, sm, sc, sp, x, lane, mi, pi);                             \
+      P2D_LAP(e_, p, er_ + 1, sm, sc, sp, x, lane, mi, pi, 0);                          \
       Lr[((slot) * P2D_LR + er_) * 64 + lane] = e_;                                     \
     }                                                                                   \
   } while (0)
@@ -658,7 +678,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   wait_vm<DSPRE * p2d_nsd(AK) + (DSPRE > 0 ? PJ * J : 0)>();
   raw_barrier();
   cplx lq0, lq1, le1 = {0.0, 0.0};  // L S_J of planes k-1 and k (own row), (!EXT1) halo values of plane k
-  P2D_LAP(lq0, k0 - 1, w + 2, 0, 1, 2, x, lane, mi, pi);
+  P2D_LAP(lq0, k0 - 1, w + 2, 0, 1, 2, x, lane, mi, pi, 0);
   // A: c of the own cell at plane k-1 (its slot is reused before L^2 S_J of plane k needs it)
   double cq0 = 0.0, cq0b = 0.0;  // (pairs: cells a, b)
   if constexpr (AK == 1 && HZ) cq0 = P2D_CV(1, w + 2, lane);
@@ -667,6 +687,10 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     cq0b = P2D_CV2(1, w + 2, lane, 1);
   }
   P2D_LROWS(k0, 1, 2, 3, 0, lq1, le1);
+  if constexpr (WC) {
+#pragma unroll
+    for (int q = 0; q < NWC; ++q) cwc[q] = nwc[q];
+  }
   raw_barrier();  // L ring slot 0 published; every wave is done with S slot 0 (plane k0-2)
 #pragma unroll
   for (int d = DSPRE; d < DS; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
@@ -750,7 +774,15 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
       const cplx ym = Lr[(lsl * P2D_LR + w) * 64 + lane], yp = Lr[(lsl * P2D_LR + w + 2) * 64 + lane];
       const cplx zz = D2 ? cplx{0.0, 0.0} : lq0 + ln;
       cplx l2;
-      if constexpr (AK == 2) {
+      if constexpr (AK == 2 && WC) {
+        l2.re = s * ((((cwc[7] * lq0.re + cwc[8] * ln.re) + (cwc[1] * xm.im + cwc[0] * l1.im)) +
+                      (cwc[3] * ym.re + cwc[4] * yp.re)) - cwc[11] * l1.re);
+        l2.im = s * ((((cwc[9] * lq0.im + cwc[10] * ln.im) + (cwc[0] * l1.re + cwc[2] * xp.re)) +
+                      (cwc[5] * ym.im + cwc[6] * yp.im)) - cwc[12] * l1.im);
+      } else if constexpr (A && WC) {
+        l2 = s * ((((cwc[4] * lq0 + cwc[5] * ln) + (cwc[0] * xm + cwc[1] * xp)) + (cwc[2] * ym + cwc[3] * yp)) -
+                  cwc[6] * l1);
+      } else if constexpr (AK == 2) {
         // cell pairs: per cell as in LROWS (a's x - 1 is xm's b, b's x + 1 is xp's a),
         // z faces from c of planes k-1 (registers) and k+1
         const int gk = z0 + k;
@@ -820,6 +852,10 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     }
     lq0 = lq1;
     lq1 = ln;
+    if constexpr (WC) {
+#pragma unroll
+      for (int q = 0; q < NWC; ++q) cwc[q] = nwc[q];
+    }
     le1 = lne;
     sk = s1;
     sis = sis + 1 == NSL ? 0 : sis + 1;
