@@ -8,7 +8,7 @@
 #   smoke          __graft_entry__.smoke()                 -> smoke.txt
 #   bench          python bench.py (headline, cpu baseline) -> bench_nlse3d_512.json
 #   bench:WL       python bench.py --workload WL            -> bench_WL.json
-#   set            bench of every BASELINE workload + KG    -> bench_*.json
+#   set            bench of every BASELINE workload + KG    -> bench_*_set.json
 #   prof[:WL]      bench under rocprofv3 --kernel-trace --stats -> prof_WL/, bench_WL_under_rocprof.json
 #   pmc[:WL]       FETCH_SIZE / WRITE_SIZE / TCC hit passes, one counter group per run -> pmc_WL/
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (a probe)           -> py_<name>.txt
@@ -55,8 +55,8 @@ for st in "$@"; do
       fi ;;
     set)
       for w in nlse2d_4096 sg2d_8192 g2_3d_256 kg_3d_256 cq3d_1024 nlse3d_512; do
-        run 300 "$OUT/bench_$w.json" python bench.py --workload "$w" --steps 10 --warmup 2 --no-cpu-baseline
-        cat "$OUT/bench_$w.json"
+        run 300 "$OUT/bench_${w}_set.json" python bench.py --workload "$w" --steps 10 --warmup 2 --no-cpu-baseline
+        cat "$OUT/bench_${w}_set.json"
       done ;;
     prof)
       wl=${arg:-nlse3d_512}
