@@ -746,7 +746,13 @@ int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
 int p2_kz(const nls_handle *h, int J) {
   // (the G2 register-row pass at J = 6 keeps the general depth: 256^3 0.473 ms at kz 128
   // vs 0.491 at 32, profiles/r04/g2_probe_jreg.txt)
-  return h->cfg.dim == 3 && !h->p2_ani && pass2_jreg(J, 0) ? std::min(h->p2kz, h->p2kzj) : h->p2kz;
+  if (h->cfg.dim != 3 || h->p2_ani) return h->p2kz;
+  if (pass2_jreg(J, 0)) return std::min(h->p2kz, h->p2kzj);
+  // the J = 0 pass (one read, two writes, three workgroups per CU) also streams faster
+  // from 64-plane tiles: 512^3 1.29-1.30 vs 1.33-1.34 ms on two boxes; the ring passes at
+  // J = 2..6, 12 lose at 64 (profiles/r04/p2ab_512.txt, calls r4g and r4w)
+  if (J == 0) return std::min(h->p2kz, 64);
+  return h->p2kz;
 }
 int p2_grid(const nls_handle *h, int J = 0) {
   if (h->p2reg) return h->p2mgrid[J];
