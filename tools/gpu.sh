@@ -114,6 +114,21 @@ print(f\"$v rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} domina
         done
       done
       cat "$OUT/p2ab.txt" ;;
+    envab)
+      # same-box A/B of environment settings on one workload: ARG = WL:SET,SET,... ("-" =
+      # none), two interleaved rounds -> envab_WL.txt
+      wl=${arg%%:*}
+      sets=${arg#*:}
+      for rep in 1 2; do
+        for ev in $(echo "$sets" | tr ',' ' '); do
+          [ "$ev" != "-" ] && export "${ev?}"
+          run 300 "$OUT/envab_cur.json" python bench.py --workload "$wl" --steps 10 --warmup 2 --no-cpu-baseline
+          [ "$ev" != "-" ] && unset "${ev%%=*}"
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['step_roofline']['gpu_kernel_ms_per_step']; \
+print(f\"$ev rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} \" + ' '.join(f'{a}:{b:.3f}' for a, b in k.items()))" \
+            "$OUT/envab_cur.json" | tee -a "$OUT/envab_$wl.txt"
+        done
+      done ;;
     probe6)
       # pure-stream rates of the tail / pass access patterns (tools/bw_probe6.hip, prebuilt)
       run 300 "$OUT/bw_probe6_512.txt" tools/bw_probe6

@@ -26,7 +26,13 @@ rng = np.random.default_rng(0)
 x = np.linspace(-10, 10, n)
 u0 = (np.exp(-(x[:, None, None] ** 2 + x[None, :, None] ** 2 + x[None, None, :] ** 2) / 8)
       + 1e-3 * rng.standard_normal((n, n, n))).astype(np.complex128).ravel()
-with nls_amd.Solver(3, n, n, n, dx, dx, m=m) as s:
+# KNOB_AB_G2=1: the G2 NLSE (m(x), div(c grad)) instead of the isotropic cubic NLSE
+g2 = os.environ.get("KNOB_AB_G2") == "1"
+kw = {"equation": nls_amd.NLSE_G2} if g2 else {}
+with nls_amd.Solver(3, n, n, n, dx, dx, m=m, **kw) as s:
+    if g2:
+        N = n ** 3
+        s.set_coefficients(1.0 + 0.5 * rng.random(N), 0.7 + 0.6 * rng.random(N))
     s.set_field(u0)
     s.step(1e-3, 2)
     for r in range(rounds):
