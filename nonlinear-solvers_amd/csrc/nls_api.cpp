@@ -25,6 +25,9 @@
 #include "nls_device.hpp"
 #include "nls_kernels.hpp"
 
+#ifndef NLS_VPAD
+#define NLS_VPAD 8192  // stride pad of a stored vector, elements (see the default's note in nls_create)
+#endif
 #ifndef NLS_KZ_L2
 #define NLS_KZ_L2 32  // tile depth of k_alpha_l2 (with NLS_RB_L2 rows per thread, nls_stencil.hpp)
 #endif
@@ -946,8 +949,11 @@ void setup_geometry(nls_handle *h) {
   // the same HBM channel (strides of 2^k * plane bytes camp on one channel).
   // 4096 elements (64 KiB of complex<double>): same-box A/B sweeps (tools/exp_pad3.sh,
   // exp_pad4.sh) gave 512^3 update passes -5 % (two boxes), 4096^2 +6 % vs the former
-  // 4 KiB pad, within 1 % elsewhere; no pad at all is ~15 % slower (tools/bw_probe.hip)
-  h->vpad = 4096;
+  // 4 KiB pad, within 1 % elsewhere; no pad at all is ~15 % slower (tools/bw_probe.hip).
+  // Round 4, with the s-step passes and the tail: 8192 elements, 512^3 passes 24.39-24.57
+  // -> 24.15-24.27 ms per step on two boxes (2048: +0.1; 4160: +0.3; 16384: +0.0), 4096^2
+  // and G2 256^3 within 1 % (profiles/r04/ab_vpad.txt)
+  h->vpad = NLS_VPAD;
   // (the vector stride h->vs follows in alloc_all, once the ghost depth is known)
 }
 
