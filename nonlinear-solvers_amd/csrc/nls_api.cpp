@@ -133,6 +133,7 @@ struct nls_handle {
   int p2lapgrid = 0;           // k_lap grid over planes [-1, nzl]
   int p2mkz = 16;              // tile depth of k_lap / k_p2m (G2 256^3 m=25: 13.36 ms/step vs 13.76 at 32)
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm
+  bool large = false;          // large-slab launch shapes (setup_geometry)
   int p2order = 0;             // k_p2d tile order (Geo::remap bits: 2 x-fastest, 4 no XCD bands; debug knob 3)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
   // a new state was set (nls_set_*): the next step starts its bases cold, so it is
@@ -904,7 +905,7 @@ int occupancy_grid(nls_handle *h, const void *fn, int64_t work_items) {
   // update time at 512^3, -1 % at 8192^2 SG); the partials of such grids are
   // summed by k_colsum.  Small slabs (<= 32 M cells): a persistent grid, where
   // the extra reduction launch costs more than the balance gains (4096^2, 256^3).
-  int mult = h->geo.nloc > (int64_t(1) << 25) ? 16 : 1;
+  int mult = h->large ? 16 : 1;
   if (const char *e = std::getenv("NLS_GRID_MULT")) mult = std::max(1, std::atoi(e));
   int64_t grid = (int64_t)std::max(per_cu, 1) * std::max(ncu, 1) * mult;
   grid = std::min<int64_t>(grid, std::max<int64_t>(work_items, 1));
@@ -932,6 +933,12 @@ void setup_geometry(nls_handle *h) {
   g.qa = 0;
   g.qb = (int32_t)g.nzl;
   g.nloc = g.nzl * g.P;
+  // Large slabs (> 32 M cells) take their own launch shapes: 16x grids of one tile per
+  // workgroup, 4-plane alpha tiles, the one-tile / tile-queue fused tail.
+  // NLS_LARGE_SLAB=1 forces them on any grid, so the tests run the bench's code path on
+  // grids the oracle and the reference fixtures cover (tests/test_gpu_refpin.py).
+  h->large = g.nloc > (int64_t(1) << 25);
+  if (const char *e = std::getenv("NLS_LARGE_SLAB")) h->large = std::atoi(e) != 0;
   // laplacians.hpp:49 (2D 1/(dx*dy)) and :102 (3D 1/(dx*dx)); values -4/-3, -6/-5 times scale
   g.s = c.dim == 2 ? 1.0 / (c.dx * c.dy) : 1.0 / (c.dx * c.dx);
   g.sd_in = (c.dim == 2 ? -4.0 : -6.0) * g.s;
@@ -942,7 +949,7 @@ void setup_geometry(nls_handle *h) {
   // alpha pass on large 3D slabs (one-tile-per-workgroup grids, see
   // occupancy_grid): shallower tiles, -9 % alpha time at 512^3 with kz 4 vs
   // 16-32; on small slabs (persistent grids) it is slower (tools/exp_kz.sh)
-  h->kz_alpha = (c.dim == 3 && g.nloc > (int64_t(1) << 25)) ? 4 : g.kz;
+  h->kz_alpha = (c.dim == 3 && h->large) ? 4 : g.kz;
   if (const char *e = std::getenv("NLS_KZ_ALPHA")) h->kz_alpha = std::max(1, std::atoi(e));
   g.remap = 0;  // (march's XCD-banded order, Geo::remap, measured no gain for these kernels)
   // Pad the vector stride so the m streams of one update pass do not start on
@@ -1101,7 +1108,7 @@ void alloc_all(nls_handle *h) {
     // large slabs: one tile per workgroup (the tail reduces nothing, so the grid
     // size only sets the dispatch balance): 512^3 m=16 tail 6.64 -> 6.38 ms against
     // two tiles per workgroup (tools/tail_sweep.sh, same box, two rounds)
-    const bool one_tile = g.nloc > (int64_t(1) << 25) && !std::getenv("NLS_GRID_MULT");
+    const bool one_tile = h->large && !std::getenv("NLS_GRID_MULT");
     // shallow tail tiles there and in 2D (4 planes / rows per wave; round 3,
     // tools/order_sweep.py, tools/wl_ab.sh, same box): 512^3 6.25 -> 6.00 ms, 4096^2
     // 0.775 -> 0.74, SG 8192^2 2.62 -> 2.51; the persistent grids of small 3D slabs keep

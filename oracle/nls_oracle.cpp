@@ -466,6 +466,19 @@ int oracle_lanczos_c(const oracle_grid *g, const double *u, uint32_t m,
   return 0;
 }
 
+// real lanczos_L (eigen_krylov_real.hpp:5-51): V n*m, T m*m, both column-major f64
+int oracle_lanczos_r(const oracle_grid *g, const double *u, uint32_t m,
+                     double *V, double *T, double *beta) {
+  Grid G;
+  if (!make_grid(g, G) || m < 1) return -1;
+  StencilOp op{G};
+  std::vector<double> Vv, Tv;
+  lanczos(op, u, m, Vv, Tv, *beta);
+  std::memcpy(V, Vv.data(), Vv.size() * sizeof(double));
+  std::memcpy(T, Tv.data(), Tv.size() * sizeof(double));
+  return 0;
+}
+
 int oracle_krylov_c(const oracle_grid *g, const double *u, double t_re,
                     double t_im, uint32_t m, int func, double *out) {
   Grid G;

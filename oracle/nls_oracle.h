@@ -62,6 +62,10 @@ int oracle_laplacian_apply_r(const oracle_grid *g, const double *x, double *y);
 int oracle_lanczos_c(const oracle_grid *g, const double *u, uint32_t m,
                      double *V, double *T, double *beta);
 
+/* real lanczos_L (eigen_krylov_real.hpp:5-51): V n*m f64, T m*m f64, column-major */
+int oracle_lanczos_r(const oracle_grid *g, const double *u, uint32_t m,
+                     double *V, double *T, double *beta);
+
 /* out = f(L) u via m-dim Krylov; t complex for the complex path */
 int oracle_krylov_c(const oracle_grid *g, const double *u, double t_re,
                     double t_im, uint32_t m, int func, double *out);

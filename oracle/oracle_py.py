@@ -42,6 +42,7 @@ def lib():
         L.oracle_laplacian_apply_c.argtypes = [g, dp, dp]
         L.oracle_laplacian_apply_r.argtypes = [g, dp, dp]
         L.oracle_lanczos_c.argtypes = [g, dp, C.c_uint32, dp, dp, C.POINTER(C.c_double)]
+        L.oracle_lanczos_r.argtypes = [g, dp, C.c_uint32, dp, dp, C.POINTER(C.c_double)]
         L.oracle_krylov_c.argtypes = [g, dp, C.c_double, C.c_double, C.c_uint32, C.c_int, dp]
         L.oracle_krylov_r.argtypes = [g, dp, C.c_double, C.c_uint32, C.c_int, dp]
         ip = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
@@ -111,6 +112,17 @@ def lanczos_c(g, u, m):
     _check(lib().oracle_lanczos_c(C.byref(g), ui, m, V, T, C.byref(b)))
     # column-major n x m -> rows; column-major m x m -> T[r, c]
     return V.view(np.complex128).reshape(m, n), T.view(np.complex128).reshape(m, m).T.copy(), b.value
+
+
+def lanczos_r(g, u, m):
+    """real lanczos_L (eigen_krylov_real.hpp:5-51): V as m rows of n, T[r, c], beta0."""
+    ui = np.ascontiguousarray(u, dtype=np.float64).ravel()
+    n = ui.size
+    V = np.zeros(n * m)
+    T = np.zeros(m * m)
+    b = C.c_double(0.0)
+    _check(lib().oracle_lanczos_r(C.byref(g), ui, m, V, T, C.byref(b)))
+    return V.reshape(m, n), T.reshape(m, m).T.copy(), b.value
 
 
 def krylov_c(g, u, t, m, func=0):

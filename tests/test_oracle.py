@@ -442,34 +442,95 @@ def test_golden_gautschi_g2():
 
 # ---- pins from the reference's own executable code (tests/golden/make_ref_fixtures.py) ----
 # Measured differences (oracle MGS vs the reference's CGS step, fresh-dot T(j-1, j)):
-# T 1e-15 .. 4e-15 of max|T|, beta <= 1e-15, V <= 5e-15 per vector, action <= 3e-15.
-# The bounds below are ~25x that: a change of recurrence (a missing re-orthogonalisation
-# term, a wrong T write, another normalisation) moves these by orders of magnitude.
-REF_LANCZOS = ["ref_lanczos_2d_smooth", "ref_lanczos_2d_noise", "ref_lanczos_3d_smooth",
+# T 1e-15 .. 4.3e-15 of max|T|, beta <= 1e-15, V <= 9e-15 per vector, at every spacing
+# (the Lanczos basis of c L is that of L: the stiffness enters the recurrence only through
+# rounding).  The bounds below are ~25x that: a change of recurrence (a missing
+# re-orthogonalisation term, a wrong T write, another normalisation) moves these by orders
+# of magnitude.  The Krylov ACTION inherits the eigenvalues' relative rounding times the
+# argument of f: its error is ~ eps (1 + kappa) with kappa = |t| rho(T) (exp, sinc of
+# t lambda) or |t| sqrt(rho(T)) (the t sqrt|lambda| functions) -- observed at most
+# 38 eps (1 + kappa) over every fixture, spacing and function (sinc^2 at C4's spacing,
+# kappa = 38); TOL_REF_ACT_K = 200 eps.
+REF_COMPLEX = ["ref_lanczos_2d_smooth", "ref_lanczos_2d_noise", "ref_lanczos_3d_smooth",
                "ref_lanczos_3d_noise"]
-TOL_REF_T, TOL_REF_V, TOL_REF_ACT = 1e-13, 1e-13, 1e-13
+REF_REAL = [f"{n}_real" for n in REF_COMPLEX]
+# the same noise fields at the BASELINE workloads' spacings: hl = 20/511 (3D 512^3),
+# c2 = 20/4095 (2D 4096^2), c4 = 6/8191 (sine-Gordon 8192^2)
+REF_STIFF = [f"ref_lanczos_{d}d_noise{r}_{s}" for d in (2, 3) for r in ("", "_real")
+             for s in ("hl", "c2", "c4")]
+REF_LANCZOS = REF_COMPLEX + REF_REAL + REF_STIFF
+TOL_REF_T, TOL_REF_V = 1e-13, 2.5e-13
+TOL_REF_ACT_K = 200 * 2.22e-16
+REAL_FUNCS = (2, 3, 4, 5, 6)  # cos, sinc, sinc^2, id of t sqrt|lambda|, sinc^2(t/2 sqrt|lambda|)
+COMPLEX_FUNCS = (0, 1, 7)  # exp(t|lambda|) (G1), exp(t lambda) (G2), sinc(t lambda) (G2 sEWI)
 
 
-def ref_action(d, m, t, V=None):
-    """beta0 V Q f(Lambda) Q^H e1 from the reference's own V and T (the eigensolve reads
-    the lower triangle and the real diagonal, eigen_krylov_complex.hpp:69-83)."""
+def ref_sinc(x):  # eigen_krylov_real.hpp:95-97 (and matfunc_complex.hpp:293-300 for complex x)
+    small = np.abs(x) < 1e-8
+    return np.where(small, 1.0, np.sin(x) / np.where(small, 1.0, x))
+
+
+def ref_f(func, lam, t):
+    """f(lambda) of every convention (eigen_krylov_complex.hpp:71-77, eigen_krylov_real.hpp:53-201,
+    nlsolvers/host/include/eigen_krylov_complex.hpp:67-72, matfunc_complex.hpp:290-300)."""
+    if func == 0:
+        return np.exp(t * np.abs(lam))
+    if func == 1:
+        return np.exp(t * lam)
+    if func == 7:
+        return ref_sinc(t * lam.astype(complex))
+    t = float(np.real(t))
+    x = t * np.sqrt(np.abs(lam))
+    return {2: lambda: np.cos(x), 3: lambda: ref_sinc(x), 4: lambda: ref_sinc(x) ** 2,
+            5: lambda: x, 6: lambda: ref_sinc(t / 2 * np.sqrt(np.abs(lam))) ** 2}[func]()
+
+
+def ref_eig(d, m):
+    """The m x m matrix the eigensolver sees (lower triangle, real diagonal:
+    eigen_krylov_complex.hpp:69, eigen_krylov_real.hpp:69) and its eigenpairs."""
     T = d[f"T{m}"]
     H = np.tril(T, -1) + np.tril(T, -1).conj().T + np.diag(T.diagonal().real)
-    lam, Q = np.linalg.eigh(H)
+    return np.linalg.eigh(H)
+
+
+def ref_action(d, m, t, func=0, V=None):
+    """beta0 V Q f(Lambda) Q^H e1 from the reference's own V and T
+    (eigen_krylov_complex.hpp:69-83, eigen_krylov_real.hpp:69-84)."""
+    lam, Q = ref_eig(d, m)
     V = d["V16"][:m] if V is None else V
-    return float(d["beta0"]) * (V.T @ (Q @ (np.exp(t * np.abs(lam)) * Q[0].conj())))
+    y = float(d["beta0"]) * (V.T @ (Q @ (ref_f(func, lam, t) * Q[0].conj())))
+    return y.real if np.isrealobj(V) else y
+
+
+def ref_kappa(d, m, t, func):
+    """The argument scale of f: |t| rho(T), or |t| sqrt(rho(T)) for the sqrt functions."""
+    rho = np.abs(ref_eig(d, m)[0]).max()
+    return abs(t) * (np.sqrt(rho) if func in REAL_FUNCS else rho)
+
+
+def ref_cases(name):
+    """(t, func) pairs checked on a fixture: the real t sqrt|lambda| functions at the
+    Gautschi steps' dt (sg_driver_dev.cpp: 5/500) and 10x; the complex conventions at
+    t = -i dt (dt = 1e-3, the NLSE configs) and 10x; sinc(t lambda) of an imaginary
+    argument only where it is finite (sinh growth)."""
+    real = "_real" in name
+    ts = (1e-2, 1e-1) if real else (-1e-3j, -1e-2j)
+    return [(t, f) for t in ts for f in (REAL_FUNCS if real else COMPLEX_FUNCS)]
 
 
 @pytest.mark.parametrize("name", REF_LANCZOS)
 @pytest.mark.parametrize("m", [10, 16])
 def test_ref_lanczos_recurrence(name, m):
-    """The oracle's lanczos_L against the reference's LanczosStepTorch, driven with
+    """The oracle's lanczos_L (complex eigen_krylov_complex.hpp:10-53, real
+    eigen_krylov_real.hpp:5-51) against the reference's LanczosStepTorch, driven with
     buf1 = L V[j] from the triplet builder: every T entry, every beta, every V row."""
     d = np.load(os.path.join(GOLD, f"{name}.npz"))
     dim, n, dx = int(d["dim"]), int(d["n"]), float(d["dx"])
     g = O.grid(dim, n, n, n, dx, dx)
-    V, T, b0 = O.lanczos_c(g, d["u"], m)
+    real = "_real" in name
+    V, T, b0 = (O.lanczos_r if real else O.lanczos_c)(g, d["u"], m)
     Tr = d[f"T{m}"]
+    assert np.isrealobj(Tr) == real
     scale = np.abs(Tr).max()
     assert np.abs(np.tril(T) - np.tril(Tr)).max() <= TOL_REF_T * scale
     assert np.abs(T - Tr).max() <= TOL_REF_T * scale  # the fresh-dot upper entries too
@@ -484,13 +545,20 @@ def test_ref_lanczos_recurrence(name, m):
 @pytest.mark.parametrize("name", REF_LANCZOS)
 @pytest.mark.parametrize("m", [10, 16])
 def test_ref_krylov_action(name, m):
-    """krylov_apply built from the reference's V and T == the oracle's action (G1
-    exp(t|lambda|), t = -i dt and a 10x longer step)."""
+    """Krylov actions built from the reference's V and T == the oracle's (complex: G1
+    exp(t|lambda|), G2 exp(t lambda), sinc(t lambda); real: cos, sinc, sinc^2, id and
+    sinc^2-half of t sqrt|lambda|), within TOL_REF_ACT_K (1 + kappa)."""
     d = np.load(os.path.join(GOLD, f"{name}.npz"))
     dim, n, dx = int(d["dim"]), int(d["n"]), float(d["dx"])
     g = O.grid(dim, n, n, n, dx, dx)
-    for t in (-1e-3j, -1e-2j):
-        assert rel_l2(O.krylov_c(g, d["u"], t, m, 0), ref_action(d, m, t)) <= TOL_REF_ACT
+    real = "_real" in name
+    for t, func in ref_cases(name):
+        kap = ref_kappa(d, m, t, func)
+        if func == 7 and kap > 300:
+            continue
+        got = O.krylov_r(g, d["u"], t, m, func) if real else O.krylov_c(g, d["u"], t, m, func)
+        err = rel_l2(got, ref_action(d, m, t, func))
+        assert err <= TOL_REF_ACT_K * (1 + kap), (t, func, err, kap)
 
 
 def test_ref_neumann_bc_2d():
