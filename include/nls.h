@@ -257,7 +257,8 @@ int nls_reset_timing(nls_handle *h);
  * {kind, stream (0 compute, 1 halo), count (doubles), peer rank (-1: none)}.
  * Sets *n to the number recorded; with out != NULL also copies the oldest
  * min(*n, cap) entries into out and removes exactly those from the log (out ==
- * NULL: size query only).  The log keeps at most NLS_OPLOG_MAX entries (the newest).  The invariant the tests check: an operation
+ * NULL: size query only).  The log keeps at most NLS_OPLOG_MAX entries (the newest); once
+ * it has dropped any, its first entry is NLS_OP_DROPPED with the number dropped.  The invariant the tests check: an operation
  * on one stream is ordered after every earlier operation on the other stream
  * by a NLS_OP_WAIT_* entry in between (RCCL never sees one communicator's
  * operations in flight on two streams at once). */
@@ -266,7 +267,9 @@ enum nls_op_kind {
   NLS_OP_SEND = 2,           /* halo planes to peer */
   NLS_OP_RECV = 3,           /* halo planes from peer */
   NLS_OP_WAIT_HALO = 4,      /* compute stream waits for the halo stream */
-  NLS_OP_WAIT_COMPUTE = 5    /* halo stream waits for the compute stream */
+  NLS_OP_WAIT_COMPUTE = 5,   /* halo stream waits for the compute stream */
+  NLS_OP_ALLGATHER = 6,      /* ncclAllGather of the peer-store IPC handles (NLS_PEER=1, once) */
+  NLS_OP_DROPPED = 7         /* first entry of a truncated log: count = entries dropped before it */
 };
 #define NLS_OPLOG_MAX 65536
 int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n);

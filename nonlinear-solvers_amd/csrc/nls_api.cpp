@@ -10,6 +10,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
+#include <deque>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -140,8 +142,8 @@ struct nls_handle {
   // issued eagerly, never replayed from a graph captured warm (run-to-run bitwise
   // reproducibility of "set state; step" sequences)
   bool p2_fresh = true;
-  bool p2_pr = false;
-  bool p2_ani = false;         // k_p2d with the G2 operator (nls_pass2a.hip)          // real field marched as cell pairs by k_p2d (p2_geo)
+  bool p2_pr = false;          // real field marched as cell pairs by k_p2d (p2_geo)
+  bool p2_ani = false;         // k_p2d with the G2 operator (nls_pass2a.hip)
   int grid_alpha2 = 1, kz_alpha2 = NLS_KZ_L2, kz_fused = 0;  // kz_fused 0: geo.kz
   int tail_grid[TAIL_NMODES] = {};  // per TailMode; 0: no such kernel (unfused path)
   int tail_dyn_grid[TAIL_NMODES] = {};  // resident workgroups of each tail kernel (dynamic tile queue)
@@ -178,10 +180,18 @@ struct nls_handle {
   hipEvent_t ev_bnd = nullptr, ev_halo = nullptr, ev_bdone = nullptr;
   bool halo_pending = false;
   bool bnd_side = true;  // boundary-plane launches on cstream
+  // peer stores (NLS_PEER=1): k_p2d writes each pass's next stencil
+  // vector's boundary planes straight into the neighbours' ghost planes -- no exchange
+  // step, no split.  peer_W[side][b]: allocation base of basis b of the neighbour below
+  // (side 0) / above (side 1), nullptr where there is none; a 1-rank handle points both
+  // at itself (its out-of-grid ghost planes: a cost probe that changes no result)
+  bool peer = false, peer_ready = false, peer_ipc = false;
+  char *peer_W[2][2] = {};
+  int64_t peer_vs[2] = {}, peer_nzl[2] = {};
   // debug (NLS_OPLOG=1 at nls_create): the transport operations in issue order, with
   // the cross-stream waits between them (nls_debug_oplog; tests/test_gpu_oplog.py)
   bool oplog_on = false;
-  std::vector<int32_t> oplog;  // [kind, stream, count, peer] per entry (nls.h NLS_OP_*)
+  std::deque<std::array<int32_t, 4>> oplog;  // {kind, stream, count, peer} per entry (nls.h NLS_OP_*)
   // debug switches read once at nls_create (never on the per-reduction path)
   bool dbg_sums = false, dbg_alpha = false;
   // asynchronous snapshots: staging copy on the compute stream, D2H on xstream
@@ -246,10 +256,21 @@ char *vec_ptr(nls_handle *h, int b, int k) {  // local plane 0 of vector k of ba
 
 // debug op log (NLS_OPLOG=1): transport operations and cross-stream waits in issue order
 void oplog(nls_handle *h, int kind, int stream, int64_t count, int peer) {
-  // bounded (NLS_OPLOG_MAX entries): a long run with the log on keeps the newest ones
+  // bounded (NLS_OPLOG_MAX entries): a long run with the log on keeps the newest ones,
+  // and a leading NLS_OP_DROPPED entry counts the entries that went (a truncated log is
+  // never mistaken for a complete one by the ordering checks)
   if (!h->oplog_on) return;
-  if (h->oplog.size() >= 4 * (size_t)NLS_OPLOG_MAX) h->oplog.erase(h->oplog.begin(), h->oplog.begin() + 4);
-  h->oplog.insert(h->oplog.end(), {(int32_t)kind, (int32_t)stream, (int32_t)count, (int32_t)peer});
+  if (h->oplog.size() >= (size_t)NLS_OPLOG_MAX) {
+    int64_t dropped = 0;
+    if (h->oplog.front()[0] == NLS_OP_DROPPED) {
+      dropped = h->oplog.front()[2];
+      h->oplog.pop_front();
+    }
+    h->oplog.pop_front();
+    ++dropped;
+    h->oplog.push_front({NLS_OP_DROPPED, 0, (int32_t)std::min<int64_t>(dropped, INT32_MAX), -1});
+  }
+  h->oplog.push_back({(int32_t)kind, (int32_t)stream, (int32_t)count, (int32_t)peer});
 }
 int stream_id(const nls_handle *h, hipStream_t st) { return st && st == h->cstream ? 1 : 0; }
 // the halo stream (cstream) waits for the work enqueued so far on the compute stream
@@ -402,6 +423,99 @@ void halo_planes(nls_handle *h, char *v, int64_t es, hipStream_t st = nullptr, i
     hip_check(h, hipEventRecord(rec.b, st), "hipEventRecord");
     h->recs.push_back(rec);
   }
+}
+
+// ---- peer stores (NLS_PEER=1) ------------------------------------------------
+
+// The neighbours' basis allocations, once per handle (they never move): over the local
+// group's rendezvous (plain device pointers: the ranks share the device), or for RCCL
+// ranks by an all-gather of IPC handles (hipIpcOpenMemHandle maps the neighbour's HBM
+// over xGMI); a 1-rank handle points at itself.
+struct PeerMsg {
+  hipIpcMemHandle_t hd[2];
+  int64_t vs, nzl;
+};
+void peer_setup(nls_handle *h) {
+  if (h->peer_ready) return;
+  if (h->nranks == 1) {
+    for (int side = 0; side < 2; ++side) {
+      for (int b = 0; b < h->nbasis; ++b) h->peer_W[side][b] = static_cast<char *>(h->B[b].W);
+      h->peer_vs[side] = h->vs;
+      h->peer_nzl[side] = h->geo.nzl;
+    }
+  } else if (h->group) {
+    auto all = rendezvous(h, {(uint64_t)(uintptr_t)h->B[0].W, (uint64_t)(uintptr_t)h->B[1].W, (uint64_t)h->vs,
+                              (uint64_t)h->geo.nzl});
+    for (int side = 0; side < 2; ++side) {
+      const int nb = h->rank + (side ? 1 : -1);
+      if (nb < 0 || nb >= h->nranks) continue;
+      for (int b = 0; b < h->nbasis; ++b) h->peer_W[side][b] = reinterpret_cast<char *>((uintptr_t)all[nb][b]);
+      h->peer_vs[side] = (int64_t)all[nb][2];
+      h->peer_nzl[side] = (int64_t)all[nb][3];
+    }
+  } else {
+    PeerMsg mine{};
+    for (int b = 0; b < h->nbasis; ++b) hip_check(h, hipIpcGetMemHandle(&mine.hd[b], h->B[b].W), "hipIpcGetMemHandle");
+    mine.vs = h->vs;
+    mine.nzl = h->geo.nzl;
+    const size_t sz = sizeof(PeerMsg);
+    char *d = nullptr;
+    hip_check(h, hipMalloc(&d, sz * (h->nranks + 1)), "hipMalloc(peer msg)");
+    std::vector<PeerMsg> all(h->nranks);
+    try {
+      hip_check(h, hipMemcpyAsync(d + sz * h->nranks, &mine, sz, hipMemcpyHostToDevice, h->stream), "H2D");
+      oplog(h, NLS_OP_ALLGATHER, 0, (int64_t)(sz / 8), -1);
+      rccl_check(h, ncclAllGather(d + sz * h->nranks, d, sz, ncclChar, h->comm, h->stream), "ncclAllGather");
+      hip_check(h, hipMemcpyAsync(all.data(), d, sz * h->nranks, hipMemcpyDeviceToHost, h->stream), "D2H");
+      hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    } catch (...) {
+      (void)hipFree(d);
+      throw;
+    }
+    (void)hipFree(d);
+    h->peer_ipc = true;
+    for (int side = 0; side < 2; ++side) {
+      const int nb = h->rank + (side ? 1 : -1);
+      if (nb < 0 || nb >= h->nranks) continue;
+      for (int b = 0; b < h->nbasis; ++b) {
+        void *p = nullptr;
+        hip_check(h, hipIpcOpenMemHandle(&p, all[nb].hd[b], hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+        h->peer_W[side][b] = static_cast<char *>(p);
+      }
+      h->peer_vs[side] = all[nb].vs;
+      h->peer_nzl[side] = all[nb].nzl;
+    }
+  }
+  h->peer_ready = true;
+}
+void peer_close(nls_handle *h) {
+  if (h->peer_ipc)
+    for (auto &side : h->peer_W)
+      for (char *&p : side)
+        if (p) (void)hipIpcCloseMemHandle(p);
+  h->peer_ipc = h->peer_ready = false;
+  for (auto &side : h->peer_W)
+    for (char *&p : side) p = nullptr;
+}
+// k_p2d's peer targets of every stored vector k of each basis (P2State pdn / pup,
+// once): the neighbour below's upper ghost planes (its local planes nzl, nzl + 1) and
+// the neighbour above's lower ones (-2, -1)
+void peer_tables(nls_handle *h) {
+  if (h->peer_ready) return;
+  peer_setup(h);
+  const int64_t P = h->geo.P, es = (int64_t)h->esize;
+  const int NK = p2state_peer_slots();
+  for (int b = 0; b < h->nbasis; ++b) {
+    std::vector<void *> t(2 * NK, nullptr);
+    for (int k = 0; k < NK && k < h->nvec[b]; ++k) {
+      if (char *w = h->peer_W[0][b]) t[k] = w + (k * h->peer_vs[0] + (GHOST_MAX + h->peer_nzl[0]) * P) * es;
+      if (char *w = h->peer_W[1][b]) t[NK + k] = w + k * h->peer_vs[1] * es;
+    }
+    char *ps = static_cast<char *>(h->p2) + (size_t)b * p2state_bytes() + p2state_peer_offset();
+    hip_check(h, hipMemcpyAsync(ps, t.data(), t.size() * sizeof(void *), hipMemcpyHostToDevice, h->stream),
+              "hipMemcpy(peer tables)");
+  }
+  hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
 }
 
 // vector k of basis b (two planes on two-vector handles: every halo'd basis vector
@@ -739,8 +853,8 @@ int p2_tiles(const nls_handle *h, int64_t qa, int64_t qb, int64_t kz) {
 // exchange the new stencil vector's two boundary planes on the halo stream while
 // the interior planes run as k_p2d on the compute stream (run_lanczos2).
 bool p2_split(const nls_handle *h) {
-  return h->collective && min_slab_planes(h) >= 8 && h->p2_split_on && !h->p2_d2 && !h->p2_pr && !h->p2reg &&
-         !h->p2_ani;
+  return h->collective && min_slab_planes(h) >= 8 && h->p2_split_on && !h->peer && !h->p2_d2 && !h->p2_pr &&
+         !h->p2reg && !h->p2_ani;
 }
 int p2_bnd_tiles(const nls_handle *h) { return 2 * p2_tiles(h, 0, 2, 2); }
 // tile depth of pass J: the register-row passes (J rows loaded straight into
@@ -787,6 +901,7 @@ std::vector<std::pair<int, int>> p2_schedule(const nls_handle *, int nstore) {
 }
 
 void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, double ti) {
+  if (h->peer) peer_tables(h);
   const int m = h->m, nstore = m - 1;
   KState *st = h->B[b].st;
   void *ps = static_cast<char *>(h->p2) + (size_t)b * p2state_bytes();
@@ -821,7 +936,7 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
     g.kz = p2_kz(h, J);
     const void *fn = h->p2reg ? nullptr
                      : h->p2_ani ? kernel_pass2a(J, ns == 2, h->p2_pr)
-                                 : kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr);
+                                 : kernel_pass2(J, ns == 2, h->p2_d2, h->p2_pr, h->peer);
     halo_wait(h);  // the stencil vector S_J's ghost planes (previous pass's exchange)
     if (h->p2reg) {
       // y = L S_J over the slab and its neighbour planes, then the pass over y.  (Issuing
@@ -839,7 +954,8 @@ void run_lanczos2(nls_handle *h, int b, int nf, int f0, int f1, double tr, doubl
       int poff = 0;
       void *args[] = {&W, &vs, &g, &ps, &h->partP2, &nb, &h->zbuf, &poff};
       launch(h, 1, J, fn, nb, args);
-      if (h->collective) halo_begin(h, b, out);
+      // peer stores: the exchange is the pass's own stores (P2State peer tables)
+      if (h->collective && !h->peer) halo_begin(h, b, out);
     } else {
       // the boundary planes [0, 2) and [nzl-2, nzl) first, as k_p2d tiles of depth 2 in
       // one grid (Geo::q2), on the compute stream; the exchange of the new stencil
@@ -1047,6 +1163,13 @@ void alloc_all(nls_handle *h) {
     h->p2_d2 = h->pass2 && !h->p2reg && dim == 2;
     h->p2_pr = h->pass2 && !h->p2reg && !c;
   }
+  // peer stores (NLS_PEER=1): the 3D isotropic k_p2d passes of
+  // collective handles write their next stencil vector's boundary planes into the
+  // neighbours' ghost planes; a 1-rank handle into its own out-of-grid ghost planes (a
+  // cost probe).  (The anisotropic and cell-pair passes keep the RCCL exchange.)
+  if (const char *e = std::getenv("NLS_PEER"))
+    h->peer = std::atoi(e) != 0 && h->pass2 && !h->p2reg && !h->p2_d2 && !h->p2_ani && !h->p2_pr && dim == 3 &&
+              (h->collective || h->nranks == 1);
   // stored vectors: slab + ghost planes (two for the two-vector passes' radius-2
   // march) + the stride pad
   h->ghost = h->pass2 ? GHOST_MAX : 1;
@@ -1429,6 +1552,7 @@ int nls_destroy(nls_handle *h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->cstream) (void)hipStreamSynchronize(h->cstream);
   if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+  peer_close(h);  // the neighbours' IPC mappings before our own allocations go
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_bdone, h->ev_snap, h->ev_snap_done})
     if (e) (void)hipEventDestroy(e);
@@ -2102,14 +2226,16 @@ int nls_get_timing(nls_handle *h, nls_timing *out) {
 
 int nls_debug_oplog(nls_handle *h, int32_t *out, uint64_t cap, uint64_t *n) {
   if (!h || !n) return NLS_ERR_ARG;
-  const uint64_t cnt = h->oplog.size() / 4;
+  const uint64_t cnt = h->oplog.size();
   *n = cnt;
   if (!out) return NLS_OK;  // size query: the log is kept
   // copy the oldest min(n, cap) entries and drop only those: a short buffer drains the
   // log over several calls instead of losing the rest
   const uint64_t take = std::min(cnt, cap);
-  std::memcpy(out, h->oplog.data(), (size_t)take * 4 * sizeof(int32_t));
-  h->oplog.erase(h->oplog.begin(), h->oplog.begin() + (ptrdiff_t)(take * 4));
+  for (uint64_t i = 0; i < take; ++i) {
+    std::memcpy(out + 4 * i, h->oplog.front().data(), 4 * sizeof(int32_t));
+    h->oplog.pop_front();
+  }
   return NLS_OK;
 }
 

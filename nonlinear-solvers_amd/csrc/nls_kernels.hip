@@ -420,9 +420,12 @@ __global__ __launch_bounds__(NTHREADS) void k_final_nlse(cplx *__restrict__ W, i
 #pragma unroll
       for (int k = 0; k < M; ++k) y += cmul(cf[k], w[q][k]);
       const double mv = nonlin >= 2 ? mf[p] : 0.0;
-      const cplx un = nl_half(y, mv, dt, nonlin, s1, s2);
+      // the fused tail's N(1/2) . N(1/2) pair (nl_half2: the second phase by the
+      // double-angle identity), so that the fused and unfused steps round alike
+      cplx un, w0;
+      nl_half2(y, mv, dt, nonlin, s1, s2, un, w0);
       st_nt(u + p, un);
-      st_nt(W + p, nl_half(un, mv, dt, nonlin, s1, s2));
+      st_nt(W + p, w0);
     }
   }
 }
@@ -823,7 +826,8 @@ const void *kernel_sg_end(int M) {
 // k_p2d at even J <= P2D_JMAX; d2: a 2D grid as planes of 4 rows; pr: a real 2D
 // field as pairs of cells
 bool pass2_jreg(int J, int akind) { return p2d_jreg(J, akind); }
-const void *kernel_pass2(int J, bool hz, bool d2, bool pr) {
+const void *kernel_pass2(int J, bool hz, bool d2, bool pr, bool peer) {
+  if (peer) return (d2 || pr) ? nullptr : kernel_pass2_peer(J, hz);
   switch (J) {
 #define X(J)                                                                                       \
   case J:                                                                                          \
@@ -847,5 +851,7 @@ const void *kernel_p2tfin() { return reinterpret_cast<const void *>(&k_p2tfin); 
 const void *kernel_p2coef() { return reinterpret_cast<const void *>(&k_p2coef); }
 size_t p2state_bytes() { return sizeof(P2State); }
 size_t p2state_sums_offset() { return offsetof(P2State, sums); }
+size_t p2state_peer_offset() { return offsetof(P2State, pdn); }
+int p2state_peer_slots() { return P2M + 1; }
 
 }  // namespace nls

@@ -60,7 +60,8 @@ const void *kernel_reduce_final();
 const void *kernel_colsum();
 // two-vectors-per-pass Lanczos (nls_pass2.hpp, nls_pass2d.hpp; 3D isotropic complex, single rank)
 //   pass2 : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* zbuf, int poff)
-const void *kernel_pass2(int J, bool hz, bool d2 = false, bool pr = false);  // hz: also Z (k_p2d)
+const void *kernel_pass2(int J, bool hz, bool d2 = false, bool pr = false, bool peer = false);  // hz: also Z (k_p2d)
+const void *kernel_pass2_peer(int J, bool hz);  // 3D isotropic k_p2d with the peer-store epilogue (nls_pass2p.hip)
 bool pass2_jreg(int J, int akind = 0);  // k_p2d<J> reads its J rows into registers (p2d_jreg; akind: 1 G2, 2 G2 pairs)
 constexpr int P2D_WAVE_XO = 64, P2D_ROWS = 4, P2D_MAXJ = 14, P2D_MAXJ_A = 22, P2D_MAXJ_A2 = 14;  // == P2D_XO, P2D_TR, P2D_JMAX, P2D_JMAX_A, P2D_JMAX_A2
 //   p2m    : (cplx* W, int64_t vs, Geo g, const P2State*, cplx* part, int nb, const cplx* lbuf, int poff)
@@ -75,6 +76,8 @@ const void *kernel_p2tfin();
 const void *kernel_p2coef();  // (P2State*, KState*, int J, int mode, int ns, int nsn)
 size_t p2state_bytes();
 size_t p2state_sums_offset();
+size_t p2state_peer_offset();  // P2State::pdn, then pup (2 x p2state_peer_slots() pointers)
+int p2state_peer_slots();
 
 // pointwise (grid-stride):
 //   nl_init   : (const cplx* u, cplx* w0, const double* mf, int64_t n, double dt, int nonlin,

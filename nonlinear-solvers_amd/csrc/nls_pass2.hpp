@@ -29,6 +29,12 @@ struct P2State {
   cplx tk[P2M];   // fused tail: t_k = W_k^H L S_{m-2} (k_p2tail)
   double beta_t;  // fused tail: beta_{m-1}
   int32_t blind;  // the J = 0 pass ran on the raw start vector (mode 2), beta from its sums
+  // peer stores (NLS_PEER=1, multi-rank k_p2d): where stored vector k's local planes 0, 1
+  // (pdn: the neighbour below's upper ghost planes) and nzl-2, nzl-1 (pup: the neighbour
+  // above's lower ones) also go; written once by the host, nullptr = no such neighbour.
+  // Read by k_p2d after its march loop (a kernel argument would be loaded at entry and
+  // held in SGPRs across the loop)
+  void *pdn[P2M + 1], *pup[P2M + 1];
 };
 
 #ifndef NLS_NO_P2_KERNELS  // (defined by translation units that only need the types)

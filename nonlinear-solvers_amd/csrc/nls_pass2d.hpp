@@ -348,7 +348,9 @@ __device__ __forceinline__ cplx pr_lap(cplx c, cplx xm, cplx xp, cplx yz, double
   return {dga * c.re + s * (yz.re + (xm.im + c.im)), dgb * c.im + s * (yz.im + (c.re + xp.re))};
 }
 
-template <int J, bool HZ, bool D2 = false, bool PR = false, bool A = false>
+// PEER: the multi-rank peer-store variant (3D isotropic; NLS_PEER=1): after the march the
+// pass's last output's boundary planes also go to the neighbours' ghost planes
+template <int J, bool HZ, bool D2 = false, bool PR = false, bool A = false, bool PEER = false>
 __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
                                                               const P2State *__restrict__ ps,
                                                               cplx *__restrict__ part, int nb,
@@ -664,7 +666,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // the look-ahead S planes whose ring slots are clear of the prologue's, and the J
   // planes, go out before the prologue's wait (p2d_dspre): a tile then starts after
   // one memory latency, not two
-  constexpr int DSPRE = p2d_dspre(J, AK), PJ = J == 0 ? 0 : (LATE ? 1 : NP - 1);
+  // (the J groups the prologue issues: none for J = 0 and the register-row passes, which
+  // have no J ring -- as p2d_after's replay skips them)
+  constexpr int DSPRE = p2d_dspre(J, AK), PJ = (J == 0 || JREG) ? 0 : (LATE ? 1 : NP - 1);
 #pragma unroll
   for (int d = 0; d < DSPRE; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
   if constexpr (DSPRE > 0) {
@@ -877,8 +881,36 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
 #undef P2D_CV
 #undef P2D_CV2
 #undef P2D_LROWS
-  wait_vm<0>();  // the look-ahead DMAs land before the LDS is reused
+  wait_vm<0>();  // the look-ahead DMAs land before the LDS is reused (and this wave's stores)
   raw_barrier();
+  // Peer stores (multi-rank handles, NLS_PEER=1): the pass's last output -- the next
+  // stencil vector -- of local planes 0, 1 straight into the neighbour below's upper
+  // ghost planes (ps->pdn), of planes nzl-2, nzl-1 into the neighbour above's lower
+  // ones (ps->pup): no exchange step and no boundary/interior split.  Read back from
+  // this wave's own stores (complete after the wait above), after the march loop, so
+  // the loop and its hand-counted vmcnt are untouched; the pass's all-reduce, which
+  // every rank joins after its pass, orders the stores before the neighbour's next pass.
+  // (a separate instantiation: the epilogue's live values cost the plain pass's march
+  // loop ~20 instructions per step at J = 12)
+  if (PEER && (k0 < 2 || k1 > nzl - 2)) {  // uniform: a tile holding a boundary plane
+    constexpr int OUT = J + (HZ ? 2 : 1);
+    cplx *const tdn = static_cast<cplx *>(ps->pdn[OUT]), *const tup = static_cast<cplx *>(ps->pup[OUT]);
+    const cplx *__restrict__ ov = HZ ? Zo : Xo;
+    const int64_t ro = (int64_t)y * nx + x0 + src_lane;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kk = e < 2 ? e : nzl - 4 + e;
+      cplx *dst = e < 2 ? tdn : tup;
+      if (dst && kk >= k0 && kk < k1) {
+        // a global (not flat) store: the table's pointers are generic
+        typedef double __attribute__((ext_vector_type(2))) d2v;
+        const cplx v = ld_nt(ov + (int64_t)kk * P + ro);
+        __attribute__((address_space(1))) d2v *gp =
+            (__attribute__((address_space(1))) d2v *)(dst + (int64_t)(e & 1) * P + ro);
+        __builtin_nontemporal_store(d2v{v.re, v.im}, gp);
+      }
+    }
+  }
   cplx *red = reinterpret_cast<cplx *>(smem);  // [4][NC]
 #pragma unroll
   for (int c = 0; c < NC; ++c) {

@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "nls_step_sewi", "nls_debug_oplog", "nls_debug_knob",
 )
 # nls_debug_oplog entry kinds (include/nls.h enum nls_op_kind)
-OP_ALLREDUCE, OP_SEND, OP_RECV, OP_WAIT_HALO, OP_WAIT_COMPUTE = 1, 2, 3, 4, 5
+OP_ALLREDUCE, OP_SEND, OP_RECV, OP_WAIT_HALO, OP_WAIT_COMPUTE, OP_ALLGATHER, OP_DROPPED = 1, 2, 3, 4, 5, 6, 7
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)

@@ -3,7 +3,8 @@ include/nls.h): the issue order the RCCL communicator sees.
 
 Entries are (kind, stream, count, peer) with kind 1 all-reduce, 2 send, 3 recv,
 4 the compute stream waits for the halo stream, 5 the halo stream waits for the
-compute stream; stream 0 = compute, 1 = halo.
+compute stream, 6 all-gather (the peer-store handshake), 7 the log was truncated
+before this entry (NLS_OPLOG_MAX); stream 0 = compute, 1 = halo.
 
 Two properties make one communicator safe without relying on RCCL to order its
 operations across HIP streams:
@@ -17,8 +18,8 @@ operations across HIP streams:
 """
 from __future__ import annotations
 
-ALLREDUCE, SEND, RECV, WAIT_HALO, WAIT_COMPUTE = 1, 2, 3, 4, 5
-COMM_OPS = (ALLREDUCE, SEND, RECV)
+ALLREDUCE, SEND, RECV, WAIT_HALO, WAIT_COMPUTE, ALLGATHER, DROPPED = 1, 2, 3, 4, 5, 6, 7
+COMM_OPS = (ALLREDUCE, SEND, RECV, ALLGATHER)
 
 
 def stream_order_violations(log):
@@ -27,7 +28,9 @@ def stream_order_violations(log):
     pending = [False, False]  # pending[s]: the other stream has unordered ops for s
     bad = []
     for i, (kind, stream, _count, _peer) in enumerate(log):
-        if kind == WAIT_HALO:
+        if kind == DROPPED:  # nothing is known about what came before
+            pending = [False, False]
+        elif kind == WAIT_HALO:
             pending[0] = False
         elif kind == WAIT_COMPUTE:
             pending[1] = False
@@ -38,10 +41,18 @@ def stream_order_violations(log):
     return bad
 
 
+def truncated(log):
+    """Entries dropped before the log's first one (its leading DROPPED entry), else 0."""
+    return log[0][2] if log and log[0][0] == DROPPED else 0
+
+
 def rank_sequence_mismatches(logs):
-    """logs[r] = op log of rank r.  Returns a list of human-readable mismatches."""
-    out = []
-    ar = [[(k, c) for k, _s, c, _p in lg if k == ALLREDUCE] for lg in logs]
+    """logs[r] = op log of rank r.  Returns a list of human-readable mismatches (a
+    truncated log cannot be matched and is reported as such)."""
+    out = [f"rank {r}: log truncated ({truncated(lg)} entries dropped)" for r, lg in enumerate(logs) if truncated(lg)]
+    if out:
+        return out
+    ar = [[(k, c) for k, _s, c, _p in lg if k in (ALLREDUCE, ALLGATHER)] for lg in logs]
     for r in range(1, len(logs)):
         if ar[r] != ar[0]:
             out.append(f"rank {r} all-reduce sequence differs from rank 0 ({len(ar[r])} vs {len(ar[0])})")

@@ -80,9 +80,13 @@ def test_graph_replay_bitwise_g2(monkeypatch, dim, n):
     assert g0 == 0 and g1 >= 5
 
 
-@pytest.mark.parametrize("eq,dim,n", [(nls_amd.KG_GAUTSCHI, 3, 14), (nls_amd.KG_GAUTSCHI, 2, 40),
-                                      (nls_amd.SG_GAUTSCHI, 2, 48)])
+@pytest.mark.parametrize("eq,dim,n", [(nls_amd.KG_GAUTSCHI, 3, 14), (nls_amd.KG_GAUTSCHI, 3, 16),
+                                      (nls_amd.KG_GAUTSCHI, 2, 40), (nls_amd.SG_GAUTSCHI, 2, 48)])
 def test_graph_replay_bitwise_real(monkeypatch, eq, dim, n):
+    """KG 3D n = 14 (ny % 4 != 0): the one-vector passes; n = 16: the s-step cell-pair
+    passes (run_lanczos2 on both bases, the TAIL_COMBINE_W0 -> TAIL_KG_END1 tails), whose
+    first step after set_* is eager.  KG 2D keeps the one-vector passes; SG 2D runs the
+    s-step passes (eager again after its second set_sg_state)."""
     def body():
         cells = n ** dim
         nz = n if dim == 3 else 1
@@ -112,6 +116,9 @@ def test_graph_replay_bitwise_real(monkeypatch, eq, dim, n):
     a0, v0, g0 = _run(monkeypatch, False, body)
     a1, v1, g1 = _run(monkeypatch, True, body)
     assert np.array_equal(a0, a1) and np.array_equal(v0, v1)
-    # SG 2D runs the two-vector passes: the first step after each set_sg_state is
-    # eager (cold bases); KG (anisotropic operator) keeps the one-vector passes
-    assert g0 == 0 and g1 == (5 if eq == nls_amd.KG_GAUTSCHI else 8)
+    # s-step passes: the first step after each set_sg_state is eager (cold bases) --
+    # SG 2D (two set_sg_state calls: 10 - 2) and KG 3D with ny % 4 == 0 and nx even
+    # (5 - 1); the one-vector passes replay every step
+    s_step_kg = eq == nls_amd.KG_GAUTSCHI and dim == 3 and n % 4 == 0
+    want = 8 if eq == nls_amd.SG_GAUTSCHI else (4 if s_step_kg else 5)
+    assert g0 == 0 and g1 == want

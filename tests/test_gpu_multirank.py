@@ -143,7 +143,7 @@ def _ran_pass2(s, m):
     return cnt[0] > 0 and cnt[1] == 0  # s-step passes start at J = 0, 2, (5,) ... never at 1
 
 
-@pytest.mark.parametrize("split", ["1", "0"], ids=["split", "unsplit"])
+@pytest.mark.parametrize("split", ["1", "0", "peer"], ids=["split", "unsplit", "peer"])
 @pytest.mark.parametrize("nranks,m", [(4, 16), (3, 15), (2, 10)])
 def test_pass2_slabs_match_oracle(monkeypatch, nranks, m, split):
     """The two-vector passes (k_p2d, the default for the 3D NLSE) on z slabs: two
@@ -152,8 +152,13 @@ def test_pass2_slabs_match_oracle(monkeypatch, nranks, m, split):
     sums; uneven slabs (40 planes over 3 ranks) and an odd m (X-only last pass).
     Spacing of the 512^3 bench (dx = 20/511): the stiff regime.  split: the slabs'
     boundary planes as their own k_p2d launch ahead of the interior (the default,
-    slabs of >= 8 planes) or one launch per pass (NLS_P2_SPLIT=0)."""
-    monkeypatch.setenv("NLS_P2_SPLIT", split)
+    slabs of >= 8 planes) or one launch per pass (NLS_P2_SPLIT=0); peer: NLS_PEER=1,
+    each pass stores its next stencil vector's boundary planes straight into the
+    neighbours' ghost planes (k_p2d<..., PEER>: no exchange step, no split)."""
+    if split == "peer":
+        monkeypatch.setenv("NLS_PEER", "1")
+    else:
+        monkeypatch.setenv("NLS_P2_SPLIT", split)
     nx, ny, nz = 64, 24, 40
     dx = 20.0 / 511
     P = nx * ny
@@ -197,3 +202,51 @@ def test_pass2_rccl_collective_path_single_rank(monkeypatch):
         assert _ran_pass2(s, m)
         assert s.comm_size() == (1, "rccl")  # ncclCommCount of the forced communicator
     assert rel_l2(got, ref) <= 1e-10
+
+
+@pytest.mark.parametrize("nranks,nz", [(2, 24), (4, 40)])
+def test_peer_slabs_bitwise_equal_exchange(monkeypatch, nranks, nz):
+    """The peer-store path moves the same bytes as the exchange: the unsplit two-vector
+    passes (one k_p2d launch per pass, the send/recv after it) and NLS_PEER=1 (the same
+    launch shape; k_p2d<..., PEER> stores the boundary planes into the neighbours' ghost
+    planes itself) give bit-identical fields."""
+    nx, ny, m = 64, 16, 12
+    dx = 20.0 / 511
+    P = nx * ny
+    u0 = field(nx * ny * nz, seed=11)
+
+    def run(env):
+        for k in ("NLS_PEER", "NLS_P2_SPLIT"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+
+        def mk(r, grp):
+            return nls_amd.Solver(3, nx, ny, nz, dx, dx, m=m, device=0, nranks=nranks, rank=r, group=grp)
+
+        def body(s):
+            s.set_field(u0[s.z0 * P:(s.z0 + s.nzl) * P])
+            s.step(1e-3, 4)
+            return s.z0, s.get_field()
+        res = sorted(run_ranks(nranks, mk, body), key=lambda t: t[0])
+        return np.concatenate([r[1] for r in res])
+    a = run({"NLS_P2_SPLIT": "0"})
+    b = run({"NLS_PEER": "1"})
+    assert np.array_equal(a, b)
+
+
+def test_peer_loopback_single_rank_unchanged(monkeypatch):
+    """NLS_PEER=1 on a 1-rank handle (the slab probe's cost measurement): the peer
+    stores land in the slab's own out-of-grid ghost planes, which nothing reads --
+    bit-identical to the plain handle."""
+    n, m = 24, 16
+    dx = 20.0 / 511
+    u0 = field(n ** 3, 12)
+    out = []
+    for peer in ("0", "1"):
+        monkeypatch.setenv("NLS_PEER", peer)
+        with nls_amd.Solver(3, n, n, n, dx, dx, m=m, device=0) as s:
+            s.set_field(u0)
+            s.step(1e-3, 3)
+            out.append(s.get_field())
+    assert np.array_equal(out[0], out[1])

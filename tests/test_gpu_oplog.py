@@ -15,11 +15,15 @@ pytestmark = pytest.mark.gpu
 nls_amd = pytest.importorskip("nls_amd")
 
 
-@pytest.mark.parametrize("pass2", ["1", "0"], ids=["two_vector", "one_vector"])
+@pytest.mark.parametrize("pass2", ["1", "0", "peer"], ids=["two_vector", "one_vector", "peer"])
 @pytest.mark.parametrize("nranks", [2, 3, 4])
 def test_slab_oplog_is_stream_ordered_and_rank_matched(monkeypatch, nranks, pass2):
+    """peer: NLS_PEER=1, the passes' boundary planes go by peer stores; the only
+    exchanges left are the start vectors' (one per step), all on the compute stream."""
     monkeypatch.setenv("NLS_OPLOG", "1")
-    monkeypatch.setenv("NLS_PASS2", pass2)
+    monkeypatch.setenv("NLS_PASS2", "1" if pass2 == "peer" else pass2)
+    if pass2 == "peer":
+        monkeypatch.setenv("NLS_PEER", "1")
     nx, ny, nz, m = 64, 16, 40, 12
     dx = 20.0 / 511
     P = nx * ny
@@ -40,7 +44,11 @@ def test_slab_oplog_is_stream_ordered_and_rank_matched(monkeypatch, nranks, pass
         kinds = [e[0] for e in lg]
         assert kinds.count(ALLREDUCE) >= 3 * (m // 2), f"rank {r}: too few all-reduces"
         assert SEND in kinds and RECV in kinds
-        assert WAIT_HALO in kinds
+        if pass2 == "peer":  # no halo stream: every transport op on the compute stream
+            assert WAIT_HALO not in kinds and all(e[1] == 0 for e in lg)
+            assert kinds.count(SEND) <= 2 * (3 + 1)  # set_field + one start vector per step
+        else:
+            assert WAIT_HALO in kinds
         bad = stream_order_violations(lg)
         assert not bad, f"rank {r}: unordered cross-stream ops at {bad[:5]}: {[lg[i] for i in bad[:5]]}"
     mism = rank_sequence_mismatches(logs)
@@ -100,3 +108,33 @@ def test_oplog_partial_drain(monkeypatch):
         first = [tuple(buf[4 * i:4 * i + 4]) for i in range(2)]
         rest = s.oplog()
         assert first + rest == full
+
+
+def test_oplog_truncation_is_marked(monkeypatch):
+    """A log that outgrows NLS_OPLOG_MAX keeps the newest entries behind one leading
+    NLS_OP_DROPPED entry that counts the dropped ones (a truncated log must
+    not read as an ordering violation, nor as a complete log)."""
+    import ctypes as C
+    from oplog_check import DROPPED, truncated
+    monkeypatch.setenv("NLS_OPLOG", "1")
+    monkeypatch.setenv("NLS_FORCE_RCCL", "1")
+    n = 8
+    dx = 20.0 / (n - 1)
+    L = nls_amd.lib()
+    cnt = C.c_uint64()
+    with nls_amd.Solver(3, n, n, n, dx, dx, m=4, device=0) as s:
+        s.set_field(field(n ** 3, 6))
+        total = 0
+        for _ in range(200):
+            s.step(1e-3, 500)
+            s.sync()
+            assert L.nls_debug_oplog(s._h, None, 0, C.byref(cnt)) == 0
+            if cnt.value >= 65536:
+                break
+        s.step(1e-3, 50)
+        s.sync()
+        lg = s.oplog()
+    assert len(lg) == 65536
+    assert lg[0][0] == DROPPED and truncated(lg) > 0
+    assert all(e[0] != DROPPED for e in lg[1:])
+    assert not stream_order_violations(lg)

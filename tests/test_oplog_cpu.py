@@ -2,7 +2,7 @@
 the two-vector pass of a split slab (boundary launch + exchange on the halo
 stream, interior + all-reduce on the compute stream) with and without the wait
 that orders the all-reduce after the exchange (the ADVICE r02 finding)."""
-from oplog_check import (ALLREDUCE, RECV, SEND, WAIT_COMPUTE, WAIT_HALO, rank_sequence_mismatches,
+from oplog_check import (ALLREDUCE, DROPPED, RECV, SEND, WAIT_COMPUTE, WAIT_HALO, rank_sequence_mismatches,
                          stream_order_violations)
 
 
@@ -46,3 +46,14 @@ def test_next_pass_without_wait_compute_is_flagged():
     the next exchange."""
     lg = _pass(0, 2) + [e for e in _pass(0, 2) if e[0] != WAIT_COMPUTE]
     assert stream_order_violations(lg)
+
+
+def test_truncated_log_is_reported_not_compared():
+    """A log whose first entry is DROPPED (NLS_OPLOG_MAX exceeded) is reported as
+    truncated instead of being compared entry by entry with the other ranks'."""
+    full = [(ALLREDUCE, 0, 4, -1)] * 3
+    cut = [(DROPPED, 0, 7, -1), (ALLREDUCE, 0, 4, -1)]
+    assert rank_sequence_mismatches([full, full]) == []
+    mism = rank_sequence_mismatches([full, cut])
+    assert len(mism) == 1 and "truncated" in mism[0] and "7" in mism[0]
+    assert stream_order_violations(cut) == []

@@ -34,7 +34,7 @@ with nls_amd.Solver(3, n, n, nz, dx, dx, m=16) as s:
     s.set_timing(False)
 cls = {k: round(v / 3, 3) for k, v in tm["class_ms"].items() if v}
 upd = {j: round(tm["update_ms"][j] / 3, 3) for j in range(16) if tm["update_count"][j]}
-print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} kz={os.environ.get('NLS_P2_KZ', 'auto')} {el * 1e3:8.3f} ms/step "
+print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} peer={os.environ.get('NLS_PEER', '0')} kz={os.environ.get('NLS_P2_KZ', 'auto')} {el * 1e3:8.3f} ms/step "
       f"{n * n * nz / el / 1e6:8.0f} Mcells*steps/s  per step {cls}  per step and J {upd}", flush=True)
 """
 
@@ -43,9 +43,13 @@ print(f"nz={nz:3d} rccl={os.environ.get('NLS_FORCE_RCCL', '0')} kz={os.environ.g
 # computes it; NLS_P2_SPLIT=0 drops the boundary/interior split (the exchange would
 # then follow each pass).  Two interleaved rounds: separate processes differ by a few
 # per cent from the placement of their allocations.
+# NLS_PEER=1: the peer-store passes (one launch per pass, the boundary planes stored by
+# k_p2d<..., PEER> itself; on one rank into its own out-of-grid ghost planes, so the row
+# carries the stores' cost but not the xGMI latency).
 BASE = [
     (64, {}), (64, {"NLS_FORCE_RCCL": "1"}), (64, {"NLS_FORCE_RCCL": "1", "NLS_P2_SPLIT": "0"}),
-    (128, {}), (128, {"NLS_FORCE_RCCL": "1"}),
+    (64, {"NLS_FORCE_RCCL": "1", "NLS_PEER": "1"}),
+    (128, {}), (128, {"NLS_FORCE_RCCL": "1"}), (128, {"NLS_FORCE_RCCL": "1", "NLS_PEER": "1"}),
 ]
 VARIANTS = BASE + BASE
 if len(sys.argv) > 1:  # a subset: python tools/slab_probe.py 0 2 3
