@@ -105,8 +105,24 @@ def moved_bytes_per_cell_step(w, m, sched, pass2, u_frac, tm, steps):
         per basis (g, then u) alpha_0 (W_0 + c; blind start: first step only), the passes
         (S_0..S_J + c in, ns out), the tail's alpha (S_{m-2} + c); the g basis's tail
         (m-1 reads + c, its W_0 written), the Gautschi tail (m-1 reads + c + that W_0 +
-        u_past; u, u_past, v written)."""
+        u_past; u, u_past, v written);
+      G2 sEWI (steps > 1, nls_step_sewi: three Krylov actions on one basis, each cold --
+        alpha_0 (W_0 + c), the passes (LDS-DMA or register form, as the G2 NLSE), the
+        tail's alpha (S_{m-2} + c)): B(u) (u, m in, W_0 out); the sinc action's tail into
+        W_0 (m-1 reads + c, W_0 written); the exp action's tail into e (the same, e
+        written); the W_0 <- u_prev copy (read + write); the exp(2 tau) action's tail
+        (m-1 reads + c + e + u in; u and u_prev written).  (The driver's Neumann BC after
+        each step touches the boundary shell only, ~6/n of a vector: not counted.)"""
     eq = w["eq"]
+    if pass2 and w.get("sewi"):
+        reg = tm["update_count"][0] > 4.5 * max(1, tm["steps"])  # two J = 0 launches per action
+        if reg:
+            passes = sum((j + 1 + ns) * 16 + (16 + 8 + 16) + (16 + 8) for j, ns in sched)
+        else:
+            passes = sum((j + 1 + ns) * 16 + 8 for j, ns in sched)
+        action = (16 + 8) + passes + (16 + 8)
+        tails = 2 * ((m - 1) * 16 + 8 + 16) + ((m - 1) * 16 + 8 + 16 + 16 + 16 + 16)
+        return (16 + 8 + 16) + 3 * action + tails + 32
     if pass2 and eq == 4 and not w.get("sewi"):
         a0 = tm["class_count"].get("alpha", 0) - tm["class_count"].get("final", 0)  # alpha_0 launches
         a0 = max(0, a0) / max(1, tm["steps"])  # per step, both bases

@@ -266,8 +266,7 @@ void oplog(nls_handle *h, int kind, int stream, int64_t count, int peer) {
       dropped = h->oplog.front()[2];
       h->oplog.pop_front();
     }
-    h->oplog.pop_front();
-    ++dropped;
+    for (; h->oplog.size() + 2 > (size_t)NLS_OPLOG_MAX; ++dropped) h->oplog.pop_front();  // room: marker + new
     h->oplog.push_front({NLS_OP_DROPPED, 0, (int32_t)std::min<int64_t>(dropped, INT32_MAX), -1});
   }
   h->oplog.push_back({(int32_t)kind, (int32_t)stream, (int32_t)count, (int32_t)peer});
@@ -1247,10 +1246,10 @@ void alloc_all(nls_handle *h) {
     // 8-plane queue tiles in 3D (512^3 m = 16, one handle, three interleaved rounds:
     // 5.77 ms against 5.86 with 16 planes and 5.95 with 4, profiles/r04/knob_ab_512.txt)
     if (h->tail_dyn && dim == 3) h->kz_fused = 8;
-    // the dynamic tile queue of the tail (nls_stencil.hpp tq_next): two counters, zero
-    // between launches (the last workgroup of each launch resets them)
-    hip_check(h, hipMalloc(&h->tailq, 2 * sizeof(int32_t)), "hipMalloc(tailq)");
-    hip_check(h, hipMemsetAsync(h->tailq, 0, 2 * sizeof(int32_t), h->stream), "hipMemset");
+    // the dynamic tile queue of the tail (nls_common.hpp tq_next_xcd: eight band heads and
+    // a done counter), zero between launches (the last workgroup of each launch resets them)
+    hip_check(h, hipMalloc(&h->tailq, tq_words() * sizeof(int32_t)), "hipMalloc(tailq)");
+    hip_check(h, hipMemsetAsync(h->tailq, 0, tq_words() * sizeof(int32_t), h->stream), "hipMemset");
     h->tail_one_tile = one_tile;
     tail_grids(h, one_tile);
   }
@@ -1276,7 +1275,9 @@ void alloc_all(nls_handle *h) {
   }
 
   // (u in an extra slot after the basis vectors measured no systematic effect against
-  // its own allocation, tools/exp_uslot.sh in round 1; removed in round 4)
+  // its own allocation, tools/exp_uslot.sh in round 1; removed in round 4.  Physically
+  // contiguous allocations (hipDeviceMallocContiguous) were slower: 512^3 update 24.8-24.9
+  // vs 24.3 ms per step, profiles/r05/envab_contig.txt; round 5, not kept)
   for (int b = 0; b < h->nbasis; ++b) {
     const size_t bytes = (size_t)h->nvec[b] * h->vs * h->esize;
     hip_check(h, hipMalloc(&h->B[b].W, bytes), "hipMalloc(basis)");
@@ -1615,7 +1616,7 @@ void p2_cold(nls_handle *h) {
   // the tail's tile-queue counters return to 0 at the end of every launch; a launch
   // that did not complete would leave them set, and every later tail on this handle
   // would skip tiles -- every new state starts from zeroed counters
-  if (h->tailq) hip_check(h, hipMemsetAsync(h->tailq, 0, 2 * sizeof(int32_t), h->stream), "hipMemset");
+  if (h->tailq) hip_check(h, hipMemsetAsync(h->tailq, 0, tq_words() * sizeof(int32_t), h->stream), "hipMemset");
 }
 
 int nls_set_field(nls_handle *h, const double *u, uint64_t n) {

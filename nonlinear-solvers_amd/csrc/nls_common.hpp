@@ -85,8 +85,55 @@ __device__ __forceinline__ int tq_next(int32_t *tq) {
   __syncthreads();
   return s_tile;
 }
+// XCD-banded tile queue (NLS_TQ_XCD): eight heads, one per band of tiles; workgroup b
+// takes the tiles of band b % 8 (blocks b, b + 8 share an XCD -- which XCD does not
+// matter) and, once its band is empty, helps the next bands.  A band is a range of tile
+// rows jt (all x tiles, all z chunks; 2D or ny < 8 tiles: a range of chunks kt), dealt
+// x-fastest, then jt, then kt: the y-neighbour tiles whose edge rows a tile's stencil
+// re-reads run at the same time on the same XCD (its L2), and every band moves through
+// the z chunks at the same pace (one compact streamed window, as the single queue).
+// Heads at tq[TQ_STRIDE * h] (own 128-B lines), the done counter at tq[TQ_STRIDE * 8].
+// Off: the 512^3 tail took 6.04-6.06 ms against 5.75 with the single queue (same box,
+// profiles/r05/ab_r5d.txt) -- the band's shared L2 does not pay for losing the chip-wide
+// dispatch order of the single head
+#ifndef NLS_TQ_XCD
+#define NLS_TQ_XCD 0
+#endif
+constexpr int TQ_STRIDE = 32;
+constexpr int TQ_WORDS = TQ_STRIDE * 9;
+__device__ __forceinline__ int tq_next_xcd(int32_t *tq, int ntx, int nty, int ntz) {
+  __shared__ int s_tile;
+  __syncthreads();  // every thread has read the previous index
+  if (threadIdx.x == 0) {
+    const bool yb = nty >= 8;  // band over tile rows, else over z chunks
+    const int nb = yb ? nty : ntz, h0 = (int)(blockIdx.x & 7);
+    int tile = ntx * nty * ntz;  // none left
+    for (int d = 0; d < 8; ++d) {
+      const int h = (h0 + d) & 7, lo = h * nb / 8, hi = (h + 1) * nb / 8;
+      const int cnt = ntx * (hi - lo) * (yb ? ntz : nty);
+      if (cnt == 0) continue;
+      const int t = atomicAdd(tq + TQ_STRIDE * h, 1);
+      if (t >= cnt) continue;
+      const int it = t % ntx, r = t / ntx;
+      const int jt = yb ? lo + r % (hi - lo) : r % nty;
+      const int kt = yb ? r / (hi - lo) : lo + r / nty;
+      tile = (kt * nty + jt) * ntx + it;
+      break;
+    }
+    s_tile = tile;
+  }
+  __syncthreads();
+  return s_tile;
+}
 // the last workgroup to finish (every other one has taken its last index) resets the queue
 __device__ __forceinline__ void tq_done(int32_t *tq) {
+  if (NLS_TQ_XCD) {
+    if (threadIdx.x == 0 && atomicAdd(tq + TQ_STRIDE * 8, 1) == (int)gridDim.x - 1) {
+      for (int h = 0; h < 8; ++h) atomicExch(tq + TQ_STRIDE * h, 0);
+      atomicExch(tq + TQ_STRIDE * 8, 0);
+    }
+    return;
+  }
   if (threadIdx.x == 0 && atomicAdd(tq + 1, 1) == (int)gridDim.x - 1) {
     atomicExch(tq, 0);
     atomicExch(tq + 1, 0);

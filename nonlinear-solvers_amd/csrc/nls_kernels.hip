@@ -55,6 +55,7 @@ int update_rows_per_thread(int J, bool ani, bool qa) {
 int alpha_rows_per_thread() { return RB_ALPHA; }
 int fused_rows_per_thread() { return FUSED_RB; }
 int alpha_l2_rows_per_thread() { return RB_L2; }
+int tq_words() { return NLS_TQ_XCD ? TQ_WORDS : 2; }
 
 // ---------------------------------------------------------------------------
 // single-workgroup reductions + coefficient math + m x m eigensolve

@@ -20,6 +20,7 @@ int update_rows_per_thread(int J, bool ani, bool qa = false);
 int alpha_rows_per_thread();
 int fused_rows_per_thread();
 int alpha_l2_rows_per_thread();
+int tq_words();  // int32 words of the tail's tile queue (Geo::tq): heads + done counter
 
 // per-variant tables (nls_stencil.hip, one object per operator x dimension)
 enum { NLS_KIND_UPDATE = 0, NLS_KIND_ALPHA = 1, NLS_KIND_LAP = 2, NLS_KIND_ALPHA_L2 = 3,

@@ -122,6 +122,15 @@ __host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
   return NLS_P2D_JREG && (A == 0 ? J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ
                                  : A == 1 && J >= NLS_P2A_JREG_MINJ && J <= NLS_P2A_JREG_MAXJ);
 }
+// JPF: a register-row pass loads plane k+1's J rows at the top of step k (one step of
+// look-ahead, J more registers: J = 8 fits two workgroups per CU, J = 10 would not);
+// the prologue loads plane k0's, the last step reloads its own plane (every step issues
+// the same loads, which the vmcnt replay counts).  Off (NLS_P2D_JPF_MAXJ 0): no gain
+// measured (round 5, with RF: passes +0.35 ms per step, profiles/r05/ab_r5d.txt)
+#ifndef NLS_P2D_JPF_MAXJ
+#define NLS_P2D_JPF_MAXJ 0
+#endif
+__host__ __device__ constexpr bool p2d_jpf(int J, int A = 0) { return p2d_jreg(J, A) && A == 0 && J <= NLS_P2D_JPF_MAXJ; }
 // Workgroups per CU: two where the registers (<= 256 per lane) and the rings
 // (<= 80 KiB) allow, so the second workgroup's waves cover the first's barriers
 // and LDS latencies; one for the long passes.
@@ -130,6 +139,9 @@ __host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
 #endif
 #ifndef NLS_P2D_DS3_MAXJ
 #define NLS_P2D_DS3_MAXJ 4  // one workgroup per CU: three planes of S look-ahead up to this J, then one (J = 6: 3.78 vs 3.90 ms, NP 4 vs 3)
+#endif
+#ifndef NLS_P2D_DS2O_MAXJ
+#define NLS_P2D_DS2O_MAXJ 4  // one WG per CU: two planes of S look-ahead up to this J (above DS3_MAXJ; 12: J = 12 no gain, r05)
 #endif
 #ifndef NLS_P2D_OCC0
 #define NLS_P2D_OCC0 3  // workgroups per CU of the J = 0 pass (S look-ahead 1; 512^3: 1.40 vs 1.61 ms at 2)
@@ -146,7 +158,12 @@ __host__ __device__ constexpr int p2d_ds(int J, int A = 0) {
            : (p2d_occ(J) >= 3 ? 1
                                 : (p2d_occ(J) == 2
                                        ? (J == 0 ? 3 : (J <= NLS_P2D_DS2_MAXJ ? 2 : 1))
-                                       : (J == 0 ? 6 : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J <= 12 || !NLS_P2D_EARLY ? 1 : 0)))));
+                                       : (J == 0 ? 6
+                                                 : (J <= NLS_P2D_DS3_MAXJ
+                                                        ? 3
+                                                        : (J <= NLS_P2D_DS2O_MAXJ
+                                                               ? 2
+                                                               : (J <= 12 || !NLS_P2D_EARLY ? 1 : 0))))));
 }
 // early issue only at one workgroup per CU (two: the other workgroup covers the wait,
 // and the LDS is short); not where the anisotropic rings leave no slot for it
@@ -174,6 +191,18 @@ __host__ __device__ constexpr int p2d_np(int J, int A = 0) {
                                                                           : NLS_P2D_NP_MAX);
 }
 __host__ __device__ constexpr bool p2d_late(int J, int A = 0) { return J > 0 && p2d_np(J, A) == 1; }
+// RF ("refill"): a J ring of NP >= 2 planes whose slot is refilled with plane k + NP as soon
+// as the wave has read plane k's rows into registers (every step reads all J rows into
+// sv[] anyway), instead of issuing plane k + NP - 1 into the slot plane k - 1 freed: NP
+// planes of look-ahead instead of NP - 1 from the same LDS (J = 12: two instead of one).
+// Off: no pass got faster (J = 2, 4 unchanged, J = 12 5.93-6.00 vs 5.82-5.88 ms, same box,
+// profiles/r05/p2ab_rf_ds2.txt) -- the ring passes are not waiting on the J look-ahead
+#ifndef NLS_P2D_RF
+#define NLS_P2D_RF 0
+#endif
+__host__ __device__ constexpr bool p2d_rf(int J, int A = 0) {
+  return NLS_P2D_RF && A == 0 && J > 0 && !p2d_jreg(J, A) && p2d_np(J, A) >= 2;
+}
 __host__ __device__ constexpr int p2d_off_c(int J, int A = 0) {
   return p2d_off_j(J, A) + p2d_np(J, A) * J * P2D_TR * 1024;
 }
@@ -211,7 +240,7 @@ __host__ __device__ constexpr int p2d_dspre(int J, int A = 0) {
 }
 __host__ __device__ constexpr int p2d_after(int J, int STW, int i, int A = 0) {
   const int DS = p2d_ds(J, A), NP = p2d_np(J, A), NSD = p2d_nsd(A);
-  const bool early = p2d_early(J, A), late = p2d_late(J, A), jreg = p2d_jreg(J, A);
+  const bool early = p2d_early(J, A), late = p2d_late(J, A), jreg = p2d_jreg(J, A), rf = p2d_rf(J, A);
   // the issue order ahead of the loop: [S groups d < DSPRE][J groups][S groups d >= DSPRE]
   // (DSPRE = 0: every S group first, as the round-3 kernel issued them)
   const int dspre = p2d_dspre(J, A) > 0 ? p2d_dspre(J, A) : DS;
@@ -221,7 +250,7 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, int A = 0) {
     if (d == i) lastS = n;
   }
   if (J > 0 && !jreg) {
-    const int pj = late ? 1 : NP - 1;
+    const int pj = late ? 1 : (rf ? NP : NP - 1);
     for (int d = 0; d < pj; ++d) {
       n += J;
       if (d == i) lastJ = n;
@@ -231,12 +260,13 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, int A = 0) {
     n += NSD;
     if (d == i) lastS = n;
   }
+  if (p2d_jpf(J, A)) n += J;  // plane k0's J rows, the last prologue loads
   for (int s = 0;; ++s) {
     if (jreg) n += J;  // the step's J row loads at its top (the compiler awaits them)
     if (early) {
       n += NSD;
       if (s + DS == i) lastS = n;
-      if (J > 0 && !late && !jreg) {
+      if (J > 0 && !late && !jreg && !rf) {
         n += J;
         if (s + NP - 1 == i) lastJ = n;
       }
@@ -245,14 +275,14 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, int A = 0) {
     if (!early) {
       n += NSD;
       if (s + DS == i) lastS = n;
-      if (J > 0 && !late && !jreg) {
+      if (J > 0 && !late && !jreg && !rf) {
         n += J;
         if (s + NP - 1 == i) lastJ = n;
       }
     }
-    if (late) {
+    if (late || rf) {  // the slot just read takes plane s + 1 (late) / s + NP (rf)
       n += J;
-      if (s + 1 == i) lastJ = n;
+      if (s + (late ? 1 : NP) == i) lastJ = n;
     }
     n += STW;
   }
@@ -360,7 +390,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   static_assert(p2d_rings_ok(J, AK), "rings exceed LDS");
   static_assert(!(A && D2), "the anisotropic pass is 3D");
   constexpr int DS = p2d_ds(J, AK), NSL = p2d_nsl(J, AK), NP = p2d_np(J, AK);
-  constexpr bool LATE = p2d_late(J, AK), JREG = p2d_jreg(J, AK);
+  constexpr bool LATE = p2d_late(J, AK), JREG = p2d_jreg(J, AK), RF = p2d_rf(J, AK), JPF = p2d_jpf(J, AK);
   // WC: the own row's face weights div(c grad) needs at plane k were computed with its
   // L S_J one step earlier (same c, same conditions, so the same bits): kept in
   // registers (nwc -> cwc) instead of recomputed from the c ring by L^2 S_J
@@ -668,7 +698,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // one memory latency, not two
   // (the J groups the prologue issues: none for J = 0 and the register-row passes, which
   // have no J ring -- as p2d_after's replay skips them)
-  constexpr int DSPRE = p2d_dspre(J, AK), PJ = (J == 0 || JREG) ? 0 : (LATE ? 1 : NP - 1);
+  constexpr int DSPRE = p2d_dspre(J, AK), PJ = (J == 0 || JREG) ? 0 : (LATE ? 1 : (RF ? NP : NP - 1));
 #pragma unroll
   for (int d = 0; d < DSPRE; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
   if constexpr (DSPRE > 0) {
@@ -676,7 +706,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
       P2D_ISSUE_J(k0, 0);
     } else if constexpr (J > 0) {
 #pragma unroll
-      for (int d = 0; d + 1 < NP; ++d) P2D_ISSUE_J(k0 + d, d);
+      for (int d = 0; d < PJ; ++d) P2D_ISSUE_J(k0 + d, d);
     }
   }
   wait_vm<DSPRE * p2d_nsd(AK) + (DSPRE > 0 ? PJ * J : 0)>();
@@ -703,7 +733,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
       P2D_ISSUE_J(k0, 0);
     } else if constexpr (J > 0) {
 #pragma unroll
-      for (int d = 0; d + 1 < NP; ++d) P2D_ISSUE_J(k0 + d, d);
+      for (int d = 0; d < PJ; ++d) P2D_ISSUE_J(k0 + d, d);
     }
   }
   // ring slots as running counters (no divisions in the loop)
@@ -716,10 +746,22 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // JREG: this lane's cell of plane k in the stored vectors (a ragged tile's extra lanes
   // read the row's last cell)
   const cplx *__restrict__ jrow = W + ((int64_t)y * nx + x0 + src_lane);
+  cplx svn[JPF ? J : 1];  // JPF: plane k+1's J rows, loaded one step ahead
+  if constexpr (JPF) {
+    const cplx *__restrict__ src = jrow + (int64_t)k0 * P;
+#pragma unroll
+    for (int l = 0; l < J; ++l) svn[l] = ld_nt(src + (int64_t)l * vs);
+  }
   for (int k = k0; k < k1; ++k) {
     const int i = k - k0;
     cplx sv[J + 1];
-    if constexpr (JREG) {
+    if constexpr (JPF) {
+#pragma unroll
+      for (int l = 0; l < J; ++l) sv[l] = svn[l];
+      const cplx *__restrict__ src = jrow + (int64_t)min(k + 1, k1 - 1) * P;
+#pragma unroll
+      for (int l = 0; l < J; ++l) svn[l] = ld_nt(src + (int64_t)l * vs);
+    } else if constexpr (JREG) {
       const cplx *__restrict__ src = jrow + (int64_t)k * P;
 #pragma unroll
       for (int l = 0; l < J; ++l) sv[l] = ld_nt(src + (int64_t)l * vs);
@@ -728,13 +770,13 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     // barrier, the wave's own J plane k-1 since its last step), then wait
     if constexpr (p2d_early(J, AK)) {
       P2D_ISSUE_S(k + DS + 2, sis);
-      if constexpr (J > 0 && !LATE && !JREG) P2D_ISSUE_J(k + NP - 1, jis);
+      if constexpr (J > 0 && !LATE && !JREG && !RF) P2D_ISSUE_J(k + NP - 1, jis);
     }
     wait_step<J, STW, AK>(i);
     raw_barrier();
     if constexpr (!p2d_early(J, AK)) {
       P2D_ISSUE_S(k + DS + 2, sis);
-      if constexpr (J > 0 && !LATE && !JREG) P2D_ISSUE_J(k + NP - 1, jis);
+      if constexpr (J > 0 && !LATE && !JREG && !RF) P2D_ISSUE_J(k + NP - 1, jis);
     }
     const int s1 = sk + 1 == NSL ? 0 : sk + 1, s2 = s1 + 1 == NSL ? 0 : s1 + 1;
     // L S_J of plane k+1: own row (register) + halo values, shared rows into L slot lsl^1
@@ -830,6 +872,11 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
 #pragma unroll
       for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, cZ[l], sv[l]);
       Z = Za + Zb;
+    }
+    if constexpr (RF) {
+      // plane k's J rows are consumed (X, Z): the slot takes plane k + NP
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      P2D_ISSUE_J(k + NP, jr);
     }
     // stores from every lane (a ragged last tile repeats its last valid lane's store)
     const int flat = k * P + y * nx + x0 + src_lane;

@@ -72,7 +72,8 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
   const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, qa = g.qa, qb = g.qb, kz = g.kz;
   const int z0 = (int)g.z0, npl = (int)g.npl;
   int32_t *const tq = g.tq;
-  for (int t0 = tq ? tq_next(tq) : (int)blockIdx.x; t0 < tiles; t0 = tq ? tq_next(tq) : t0 + (int)gridDim.x) {
+#define NLS_TQ_NEXT() (NLS_TQ_XCD ? tq_next_xcd(tq, ntx, nty, (int)ntz64) : tq_next(tq))
+  for (int t0 = tq ? NLS_TQ_NEXT() : (int)blockIdx.x; t0 < tiles; t0 = tq ? NLS_TQ_NEXT() : t0 + (int)gridDim.x) {
     // optional XCD-banded order (workgroups b, b+8 share an XCD): speed only
     const int t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
     const int it = t % ntx;
@@ -270,6 +271,7 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
     }
   }
   if (tq) tq_done(tq);
+#undef NLS_TQ_NEXT
 }
 
 #include "nls_march_q.hpp"

@@ -158,8 +158,11 @@ class P2dSchedule:
         self.OCC0, self.OCC2 = define("NLS_P2D_OCC0"), define("NLS_P2D_OCC2_MAXJ")
         self.OCC2A, self.EARLYA, self.DS1A = define("NLS_P2A_OCC2_MAXJ"), define("NLS_P2A_EARLY"), define("NLS_P2A_DS1")
         self.DS2, self.DS3 = define("NLS_P2D_DS2_MAXJ"), define("NLS_P2D_DS3_MAXJ")
+        self.DS2O = define("NLS_P2D_DS2O_MAXJ")
         self.EARLY, self.NPMAX = define("NLS_P2D_EARLY"), define("NLS_P2D_NP_MAX")
         self.PRE_LA = define("NLS_P2D_PRE_LA")
+        self.RF = define("NLS_P2D_RF")
+        self.JPF = define("NLS_P2D_JPF_MAXJ")
         self.JREG = define("NLS_P2D_JREG")
         self.JREG_MINJ, self.JREG_MAXJ = define("NLS_P2D_JREG_MINJ"), define("NLS_P2D_JREG_MAXJ")
         self.JREGA_MINJ, self.JREGA_MAXJ = define("NLS_P2A_JREG_MINJ"), define("NLS_P2A_JREG_MAXJ")
@@ -190,7 +193,13 @@ class P2dSchedule:
             return 1
         if o == 2:
             return 3 if J == 0 else (2 if J <= self.DS2 else 1)
-        return 6 if J == 0 else (3 if J <= self.DS3 else (1 if (J <= 12 or not self.EARLY) else 0))
+        if J == 0:
+            return 6
+        if J <= self.DS3:
+            return 3
+        if J <= self.DS2O:
+            return 2
+        return 1 if (J <= 12 or not self.EARLY) else 0
 
     def early(self, J, A=0):
         if A:
@@ -209,6 +218,14 @@ class P2dSchedule:
     def late(self, J, A=0):
         return J > 0 and self.np(J, A) == 1
 
+    def jpf(self, J, A=0):
+        """Register-row pass with plane k+1's rows loaded one step ahead (p2d_jpf)."""
+        return self.jreg(J, A) and A == 0 and J <= self.JPF
+
+    def rf(self, J, A=0):
+        """J slot refilled with plane k + NP right after its rows are read (p2d_rf)."""
+        return bool(self.RF) and A == 0 and J > 0 and not self.jreg(J, A) and self.np(J, A) >= 2
+
     def nsl(self, J, A=0):
         return self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
 
@@ -219,7 +236,7 @@ class P2dSchedule:
 
     def after(self, J, stw, i, A=0):
         DS, NP, NSD = self.ds(J, A), self.np(J, A), {0: 4, 1: 6, 2: 8}[A]
-        early, late, jreg = self.early(J, A), self.late(J, A), self.jreg(J, A)
+        early, late, jreg, rf = self.early(J, A), self.late(J, A), self.jreg(J, A), self.rf(J, A)
         n = lastS = lastJ = 0
         pre = self.dspre(J, A)
         for d in range(pre):
@@ -227,7 +244,7 @@ class P2dSchedule:
             if d == i:
                 lastS = n
         if J > 0 and not jreg:
-            for d in range(1 if late else NP - 1):
+            for d in range(1 if late else (NP if rf else NP - 1)):
                 n += J
                 if d == i:
                     lastJ = n
@@ -235,6 +252,8 @@ class P2dSchedule:
             n += NSD
             if d == i:
                 lastS = n
+        if self.jpf(J, A):
+            n += J  # plane k0's J rows, the last prologue loads
         s = 0
         while True:
             if jreg:
@@ -243,7 +262,7 @@ class P2dSchedule:
                 n += NSD
                 if s + DS == i:
                     lastS = n
-                if J > 0 and not late and not jreg:
+                if J > 0 and not late and not jreg and not rf:
                     n += J
                     if s + NP - 1 == i:
                         lastJ = n
@@ -253,13 +272,13 @@ class P2dSchedule:
                 n += NSD
                 if s + DS == i:
                     lastS = n
-                if J > 0 and not late and not jreg:
+                if J > 0 and not late and not jreg and not rf:
                     n += J
                     if s + NP - 1 == i:
                         lastJ = n
-            if late:
+            if late or rf:  # the slot just read takes plane s + 1 / s + NP
                 n += J
-                if s + 1 == i:
+                if s + (1 if late else NP) == i:
                     lastJ = n
             n += stw
             s += 1

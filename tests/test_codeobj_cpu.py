@@ -45,11 +45,12 @@ def test_checker_flags_an_extra_vmem_op():
     """The loop check is not vacuous: one more load in a synthetic loop body fails it."""
     sched = C.P2dSchedule(HDR)
     name = "_ZN3nls5k_p2dILi2ELb1ELb0ELb0ELb0EEEv"
-    body = [(0x100, "s_waitcnt", "vmcnt(4)")] + \
+    waits = [(0x0f0 + 4 * i, "s_waitcnt", f"vmcnt({w})") for i, w in enumerate(sched.waits(2, 2))]
+    body = waits + \
         [(0x104 + 4 * i, "global_load_lds_dwordx4", "v[2:3], off") for i in range(4)] + \
         [(0x120, "global_load_lds_dword", ""), (0x124, "global_load_lds_dword", ""),
          (0x128, "global_store_dwordx4", ""), (0x12c, "global_store_dwordx4", ""),
-         (0x130, "s_cbranch_scc1", f"<{name}+0x100>")]
+         (0x130, "s_cbranch_scc1", f"<{name}+0x0f0>")]
     ins = [(0x0, "s_load_dwordx2", "")] + body
     md = {name: {"private_segment_fixed_size": "0", "vgpr_spill_count": "0"}}
     assert C.check_p2d({name: ins}, md, sched)[0][1] == []

@@ -26,7 +26,8 @@ run() {  # run LIMIT OUTFILE CMD...: stop the chain on any failure
   local rc=$?
   if [ $rc -ne 0 ]; then
     echo "[gpu.sh] '$*' exited $rc; stopping" >&2
-    tail -20 "$out" "$out.err" >&2
+    tail -n 20 "$out" >&2
+    tail -n 20 "$out.err" >&2
     exit $rc
   fi
 }
@@ -82,6 +83,15 @@ for st in "$@"; do
         SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/sq_$wl/p1" -o run -- \
         python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/sq_$wl/p1.log" 2>&1 || exit $?
       python3 tools/pmc_table.py "$OUT/sq_$wl" > "$OUT/sq_$wl.txt" && cat "$OUT/sq_$wl.txt" ;;
+    sq2)
+      # LDS and instruction-wait detail (8 SQ counters, one pass)
+      wl=${arg:-nlse3d_512}
+      mkdir -p "$OUT/sq2_$wl"
+      echo "[gpu.sh] $(date +%T) sq2 $wl"
+      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/sq2_$wl/p1" -o run -- \
+        python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/sq2_$wl/p1.log" 2>&1 || exit $?
+      python3 tools/pmc_table.py "$OUT/sq2_$wl" > "$OUT/sq2_$wl.txt" && cat "$OUT/sq2_$wl.txt" ;;
     ab)
       # same-box A/B: every variant build nonlinear-solvers_amd/lib_v*/ against lib, two
       # rounds interleaved, one bench process each -> ab_WL.txt (ms/step, dominant kernel ms)

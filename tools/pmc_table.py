@@ -40,10 +40,12 @@ def main():
             parts.append(f"L2hit {c['TCC_HIT_sum'] / max(c['TCC_HIT_sum'] + c.get('TCC_MISS_sum', 0), 1):.2f}")
         wc = c.get("SQ_WAVE_CYCLES")
         if wc:
-            for n in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
-                      "SQ_ACTIVE_INST_SALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM"):
+            for n in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS",
+                      "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM"):
                 if n in c:
                     parts.append(f"{n[3:].lower()} {c[n] / wc:.2f}")
+        if "SQ_LDS_IDX_ACTIVE" in c:
+            parts.append(f"lds_bank_conflict/idx_active {c.get('SQ_LDS_BANK_CONFLICT', 0) / max(c['SQ_LDS_IDX_ACTIVE'], 1):.3f}")
         wv = c.get("SQ_WAVES")
         if wv:
             for n in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_INSTS_SMEM"):
