@@ -118,9 +118,19 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 #ifndef NLS_P2A_JREG_MAXJ
 #define NLS_P2A_JREG_MAXJ 8  // J = 10 with Z: 255 VGPRs and scratch
 #endif
+// The real cell-pair passes of the G2 operator (Klein-Gordon, A = 2) at two workgroups per
+// CU up to J = NLS_P2A2_OCC2_MAXJ: their S and c rings (4 slots each) and the L ring fill
+// exactly 80 KiB once the tile's x-halo L values stay in registers (no EXT1) and the
+// coefficients of X and Z in registers (p2d_rcoef); the J rows then come straight into
+// registers (no J ring: p2d_jreg).  At one workgroup per CU these passes were latency-
+// bound (KG 256^3: J = 0 at 1.7 TB/s, 742 instructions per step at one wave per SIMD)
+#ifndef NLS_P2A2_OCC2_MAXJ
+#define NLS_P2A2_OCC2_MAXJ 6  // KG 256^3: 5190 -> 5712 Mcells*steps/s (profiles/r05/ab_kg_occ2.txt)
+#endif
 __host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
-  return NLS_P2D_JREG && (A == 0 ? J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ
-                                 : A == 1 && J >= NLS_P2A_JREG_MINJ && J <= NLS_P2A_JREG_MAXJ);
+  return NLS_P2D_JREG && (A == 0   ? J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ
+                          : A == 1 ? J >= NLS_P2A_JREG_MINJ && J <= NLS_P2A_JREG_MAXJ
+                                   : J > 0 && J <= NLS_P2A2_OCC2_MAXJ);
 }
 // JPF: a register-row pass loads plane k+1's J rows at the top of step k (one step of
 // look-ahead, J more registers: J = 8 fits two workgroups per CU, J = 10 would not);
@@ -147,14 +157,19 @@ __host__ __device__ constexpr bool p2d_jpf(int J, int A = 0) { return p2d_jreg(J
 #define NLS_P2D_OCC0 3  // workgroups per CU of the J = 0 pass (S look-ahead 1; 512^3: 1.40 vs 1.61 ms at 2)
 #endif
 __host__ __device__ constexpr int p2d_occ(int J, int A = 0) {
-  return A ? (A == 1 && (J <= NLS_P2A_OCC2_MAXJ || p2d_jreg(J, A)) ? 2 : 1)  // pairs: the c ring as large as S's
-           : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ || p2d_jreg(J) ? 2 : 1));
+  return A == 1   ? (J <= NLS_P2A_OCC2_MAXJ || p2d_jreg(J, A) ? 2 : 1)
+         : A == 2 ? (J <= NLS_P2A2_OCC2_MAXJ ? 2 : 1)  // pairs: the c ring as large as S's
+                  : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ || p2d_jreg(J) ? 2 : 1));
 }
+// the x-halo L values of the tile computed by one wave into LDS (EXT1), and the X / Z
+// coefficients in LDS -- except on the cell-pair passes at two workgroups per CU (above)
+__host__ __device__ constexpr bool p2d_ext1(int J, int A = 0) { return NLS_P2D_EXT1 && !(A == 2 && p2d_occ(J, A) == 2); }
+__host__ __device__ constexpr bool p2d_rcoef(int J, int A = 0) { return A == 2 && p2d_occ(J, A) == 2; }
 // S ring: the planes k .. k+2 being read, DS planes of look-ahead and the slot of
 // plane k-2 (free since the previous step's barrier), into which a step issues
 // before its own wait and barrier
 __host__ __device__ constexpr int p2d_ds(int J, int A = 0) {
-  return A ? (p2d_occ(J, A) == 2 ? (J == 0 ? 2 : 1) : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J >= 22 ? 1 : NLS_P2A_DS1)))
+  return A ? (p2d_occ(J, A) == 2 ? (J == 0 && A == 1 ? 2 : 1) : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J >= 22 ? 1 : NLS_P2A_DS1)))
            : (p2d_occ(J) >= 3 ? 1
                                 : (p2d_occ(J) == 2
                                        ? (J == 0 ? 3 : (J <= NLS_P2D_DS2_MAXJ ? 2 : 1))
@@ -177,9 +192,12 @@ __host__ __device__ constexpr int p2d_off_l(int J, int A = 0) {
 }
 // the L ring: [2][P2D_LR] rows of 64, then [2][P2D_TR][2] x-halo values (x0-1, x0+64)
 constexpr int P2D_LXB = 2 * P2D_TR * 2 * 16;
-__host__ __device__ constexpr int p2d_off_j(int J, int A = 0) { return p2d_off_l(J, A) + 2 * P2D_LR * 1024 + P2D_LXB; }
+__host__ __device__ constexpr int p2d_off_j(int J, int A = 0) {
+  return p2d_off_l(J, A) + 2 * P2D_LR * 1024 + (p2d_ext1(J, A) ? P2D_LXB : 0);
+}
+__host__ __device__ constexpr int p2d_coef_bytes(int J, int A = 0) { return p2d_rcoef(J, A) ? 0 : 2 * (J + 1) * 16; }
 __host__ __device__ constexpr int p2d_avail(int J, int A = 0) {
-  return P2D_LDS / p2d_occ(J, A) - p2d_off_j(J, A) - 2 * (J + 1) * 16;
+  return P2D_LDS / p2d_occ(J, A) - p2d_off_j(J, A) - p2d_coef_bytes(J, A);
 }
 // J ring: NP whole planes of the J stored vectors of the wave's row (1 KiB each),
 // the plane being read + NP-1 planes of look-ahead.  NP = 1 ("late" J ring, the long
@@ -206,7 +224,7 @@ __host__ __device__ constexpr bool p2d_rf(int J, int A = 0) {
 __host__ __device__ constexpr int p2d_off_c(int J, int A = 0) {
   return p2d_off_j(J, A) + p2d_np(J, A) * J * P2D_TR * 1024;
 }
-__host__ __device__ constexpr int p2d_lds_bytes(int J, int A = 0) { return p2d_off_c(J, A) + 2 * (J + 1) * 16; }
+__host__ __device__ constexpr int p2d_lds_bytes(int J, int A = 0) { return p2d_off_c(J, A) + p2d_coef_bytes(J, A); }
 __host__ __device__ constexpr bool p2d_rings_ok(int J, int A = 0) {
   return J == 0 ? p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS
                 : (J <= (A == 2 ? P2D_JMAX_A2 : (A ? P2D_JMAX_A : P2D_JMAX)) && (p2d_np(J, A) >= 1 || p2d_jreg(J, A)) &&
@@ -391,6 +409,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   static_assert(!(A && D2), "the anisotropic pass is 3D");
   constexpr int DS = p2d_ds(J, AK), NSL = p2d_nsl(J, AK), NP = p2d_np(J, AK);
   constexpr bool LATE = p2d_late(J, AK), JREG = p2d_jreg(J, AK), RF = p2d_rf(J, AK), JPF = p2d_jpf(J, AK);
+  constexpr bool EXT1 = p2d_ext1(J, AK), RCOEF = p2d_rcoef(J, AK);
   // WC: the own row's face weights div(c grad) needs at plane k were computed with its
   // L S_J one step earlier (same c, same conditions, so the same bits): kept in
   // registers (nwc -> cwc) instead of recomputed from the c ring by L^2 S_J
@@ -408,8 +427,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   const double *Cr = reinterpret_cast<const double *>(smem + p2d_off_c_ring(J, AK));  // A: [NSL][p2d_csb/8]
   cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J, AK));       // [2][P2D_LR][64]
   cplx *Lx = Lr + 2 * P2D_LR * 64;                                     // [2][P2D_TR][2]
-  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J, AK));       // [J+1]
+  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J, AK));       // [J+1] (not with RCOEF)
   cplx *cZ = cX + (J + 1);                                           // [J+1]
+  cplx rcX[RCOEF ? J + 1 : 1], rcZ[RCOEF ? J + 1 : 1];               // RCOEF: in registers
   // w through readfirstlane: wave-uniform for the compiler too, so row and plane
   // logic stays scalar
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -451,9 +471,17 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   const bool full = x0 + P2D_XO <= nx;                    // uniform
   const int src_lane = xin ? lane : nx - 1 - x0;          // last valid lane of a ragged tile
   const int y = y0 + w;  // this wave's row (ny % 4 == 0: always a real row)
-  for (int l = t; l <= J; l += NTHREADS) {
-    cX[l] = ps->aX[l];
-    cZ[l] = ps->aZ[l];
+  if constexpr (RCOEF) {
+#pragma unroll
+    for (int l = 0; l <= J; ++l) {
+      rcX[l] = ps->aX[l];
+      rcZ[l] = ps->aZ[l];
+    }
+  } else {
+    for (int l = t; l <= J; l += NTHREADS) {
+      cX[l] = ps->aX[l];
+      cZ[l] = ps->aZ[l];
+    }
   }
   cplx bX1 = ps->bX1, bZ1 = ps->bZ1, bZ2 = ps->bZ2;
   double s = g.s, sdi = g.sd_in, sdb = g.sd_bd;
@@ -670,15 +698,15 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
 #define P2D_LROWS(p, sm, sc, sp, slot, own, ext)                                        \
   do {                                                                                  \
     P2D_LAP(own, p, w + 2, sm, sc, sp, x, lane, mi, pi, 1);                             \
-    if constexpr (!NLS_P2D_EXT1) P2D_LAP(ext, p, w + 2, sm, sc, sp, xe, eci, emi, epi, 0); \
+    if constexpr (!EXT1) P2D_LAP(ext, p, w + 2, sm, sc, sp, xe, eci, emi, epi, 0);     \
     Lr[((slot) * P2D_LR + w + 1) * 64 + lane] = own;                                    \
-    if (NLS_P2D_EXT1 && w == 0) {                                                       \
+    if (EXT1 && w == 0) {                                                               \
       cplx e_;                                                                          \
       P2D_LAP(e_, p, xr, sm, sc, sp, xe, eci, emi, epi, 0);                             \
       if (lane < 2 * P2D_TR) Lx[(slot) * 2 * P2D_TR + lane] = e_;                       \
     }                                                                                   \
-    if (NLS_P2D_EXT1 ? (w == 1 || w == 2) : (w == 0 || w == P2D_TR - 1)) {              \
-      const int er_ = (NLS_P2D_EXT1 ? w == 1 : w == 0) ? 0 : P2D_LR - 1;                \
+    if (EXT1 ? (w == 1 || w == 2) : (w == 0 || w == P2D_TR - 1)) {                      \
+      const int er_ = (EXT1 ? w == 1 : w == 0) ? 0 : P2D_LR - 1;                        \
       cplx e_;                                                                          \
       P2D_LAP(e_, p, er_ + 1, sm, sc, sp, x, lane, mi, pi, 0);                          \
       Lr[((slot) * P2D_LR + er_) * 64 + lane] = e_;                                     \
@@ -798,14 +826,14 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     // X (and Z) as two partial sums: shorter dependent FMA chains
     cplx Xa = cmul(bX1, l1), Xb = {0.0, 0.0};
 #pragma unroll
-    for (int l = 0; l <= J; ++l) cmac((l & 1) ? Xb : Xa, cX[l], sv[l]);
+    for (int l = 0; l <= J; ++l) cmac((l & 1) ? Xb : Xa, RCOEF ? rcX[l] : cX[l], sv[l]);
     const cplx X = Xa + Xb;
     cplx Z = {0.0, 0.0};
     if constexpr (HZ) {
       // x neighbours: lanes i-1 / i+1 by DPP, the tile-edge ones from the halo values
       // (EXT1: Lx of the wave's row; else x0-1 on lane 0 of le1, x0+64 on its lane 1)
       cplx xm = lane_prev(l1), xp = lane_next(l1);
-      if constexpr (NLS_P2D_EXT1) {
+      if constexpr (EXT1) {
         const cplx hm = Lx[lsl * 2 * P2D_TR + 2 * w], hp = Lx[lsl * 2 * P2D_TR + 2 * w + 1];
         if (lane == 0) xm = hm;
         if (lane == 63) xp = hp;
@@ -870,7 +898,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
         l2 = P2D_DIAG(x, y, z0 + k) * l1 + s * ((zz + (xm + xp)) + (ym + yp));
       cplx Za = cmul(bZ2, l2) + cmul(bZ1, l1), Zb = {0.0, 0.0};
 #pragma unroll
-      for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, cZ[l], sv[l]);
+      for (int l = 0; l <= J; ++l) cmac((l & 1) ? Zb : Za, RCOEF ? rcZ[l] : cZ[l], sv[l]);
       Z = Za + Zb;
     }
     if constexpr (RF) {

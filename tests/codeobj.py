@@ -166,6 +166,8 @@ class P2dSchedule:
         self.JREG = define("NLS_P2D_JREG")
         self.JREG_MINJ, self.JREG_MAXJ = define("NLS_P2D_JREG_MINJ"), define("NLS_P2D_JREG_MAXJ")
         self.JREGA_MINJ, self.JREGA_MAXJ = define("NLS_P2A_JREG_MINJ"), define("NLS_P2A_JREG_MAXJ")
+        self.OCC2A2 = define("NLS_P2A2_OCC2_MAXJ")
+        self.EXT1 = define("NLS_P2D_EXT1")
         self.SR, self.SRB, self.LR = const("P2D_SR"), const("P2D_SRB"), const("P2D_LR")
         self.CSB = const("P2D_CSB")
         self.LDS = 160 * 1024
@@ -178,17 +180,21 @@ class P2dSchedule:
             return False
         if A == 0:
             return self.JREG_MINJ <= J <= self.JREG_MAXJ
-        return A == 1 and self.JREGA_MINJ <= J <= self.JREGA_MAXJ
+        if A == 1:
+            return self.JREGA_MINJ <= J <= self.JREGA_MAXJ
+        return 0 < J <= self.OCC2A2
 
     def occ(self, J, A=0):
-        if A:
-            return 2 if A == 1 and (J <= self.OCC2A or self.jreg(J, A)) else 1
+        if A == 1:
+            return 2 if (J <= self.OCC2A or self.jreg(J, A)) else 1
+        if A == 2:
+            return 2 if J <= self.OCC2A2 else 1
         return self.OCC0 if J == 0 else (2 if J <= self.OCC2 or self.jreg(J) else 1)
 
     def ds(self, J, A=0):
         o = self.occ(J, A)
         if A:
-            return (2 if J == 0 else 1) if o == 2 else (3 if J <= self.DS3 else (1 if J >= 22 else self.DS1A))
+            return (2 if J == 0 and A == 1 else 1) if o == 2 else (3 if J <= self.DS3 else (1 if J >= 22 else self.DS1A))
         if o >= 3:
             return 1
         if o == 2:
@@ -211,8 +217,10 @@ class P2dSchedule:
             return 0
         nsl = self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
         csb = self.SR * self.SRB if A == 2 else (self.CSB if A else 0)
-        off_j = nsl * self.SR * self.SRB + nsl * csb + 2 * self.LR * 1024 + 2 * self.TR * 2 * 16  # + P2D_LXB
-        avail = self.LDS // self.occ(J, A) - off_j - 2 * (J + 1) * 16
+        ocp2 = A == 2 and self.occ(J, A) == 2  # no EXT1 x-halo area, coefficients in registers
+        lxb = 0 if (ocp2 or not self.EXT1) else 2 * self.TR * 2 * 16  # P2D_LXB
+        off_j = nsl * self.SR * self.SRB + nsl * csb + 2 * self.LR * 1024 + lxb
+        avail = self.LDS // self.occ(J, A) - off_j - (0 if ocp2 else 2 * (J + 1) * 16)
         return min(avail // (self.TR * 1024 * J), self.NPMAX)
 
     def late(self, J, A=0):

@@ -43,6 +43,13 @@ for st in "$@"; do
         run 900 "$OUT/suite.txt" python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
       fi
       tail -3 "$OUT/suite.txt" ;;
+    suitev)
+      # suitev:VARIANT:EXPR -- the GPU tests matching EXPR against nonlinear-solvers_amd/VARIANT
+      v=${arg%%:*}
+      ex=${arg#*:}
+      NLS_AMD_LIB=$PWD/nonlinear-solvers_amd/$v/libnls_amd.so run 900 "$OUT/suite_$v.txt" \
+        python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$ex"
+      tail -n 3 "$OUT/suite_$v.txt" ;;
     smoke)
       run 180 "$OUT/smoke.txt" python -c "import __graft_entry__ as g; g.smoke()"
       cat "$OUT/smoke.txt" ;;
