@@ -66,6 +66,9 @@ struct UpdPlan {
 };
 
 constexpr int NSUM = 2 * MMAX + 8;  // cplx words of KState::sums
+#ifndef NLS_KG_CONCURRENT
+#define NLS_KG_CONCURRENT 1  // the two Klein-Gordon bases on two streams (one rank, s-step passes)
+#endif
 constexpr int EVRING = 8;            // events per handle for the local transport
 
 }  // namespace
@@ -136,6 +139,12 @@ struct nls_handle {
   int p2mkz = 16;              // tile depth of k_lap / k_p2m (G2 256^3 m=25: 13.36 ms/step vs 13.76 at 32)
   bool p2_blind = true;        // J = 0 pass without an alpha pass once warm
   bool large = false;          // large-slab launch shapes (setup_geometry)
+  // Klein-Gordon s-step passes on one rank: the sinc^2 basis of g runs on stream2,
+  // concurrently with the cos basis of u on stream (their own partial buffers), joined
+  // before the Gautschi tail (kg_concurrent)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  cplx *partP2b = nullptr, *partAb = nullptr;
   int p2order = 0;             // k_p2d tile order (Geo::remap bits: 2 x-fastest, 4 no XCD bands; debug knob 3)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
   // a new state was set (nls_set_*): the next step starts its bases cold, so it is
@@ -293,6 +302,7 @@ hipEvent_t get_event(nls_handle *h) {
 void harvest_timing(nls_handle *h) {
   if (h->recs.empty()) return;
   hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  if (h->stream2) hip_check(h, hipStreamSynchronize(h->stream2), "hipStreamSynchronize");  // (KG's second basis)
   for (auto &r : h->recs) {
     float ms = 0.f;
     hip_check(h, hipEventElapsedTime(&ms, r.a, r.b), "hipEventElapsedTime");
@@ -1357,6 +1367,13 @@ void alloc_all(nls_handle *h) {
   const size_t na = std::max<size_t>(2 * (size_t)h->grid_alpha, h->fused_tail ? 3 * (size_t)h->grid_alpha2 : 0);
   hip_check(h, hipMalloc(&h->partA, na * sizeof(cplx)), "hipMalloc(partA)");
   hip_check(h, hipMalloc(&h->partU, (size_t)cap * sizeof(cplx)), "hipMalloc(partU)");
+  if (NLS_KG_CONCURRENT && h->kg && h->pass2 && !h->collective) {  // the second basis' own partials and stream
+    hip_check(h, hipMalloc(&h->partAb, na * sizeof(cplx)), "hipMalloc(partA)");
+    hip_check(h, hipMalloc(&h->partP2b, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)), "hipMalloc(partP2)");
+    hip_check(h, hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(h, hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming), "hipEventCreate");
+    hip_check(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming), "hipEventCreate");
+  }
   h->grid_pw = (int)std::max<int64_t>(1, std::min<int64_t>((g.nloc + NTHREADS - 1) / NTHREADS, 8192));
 }
 
@@ -1369,8 +1386,9 @@ void free_all(nls_handle *h) {
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
                   (void *)h->vel, h->xedge, (void *)h->partX, h->p2, (void *)h->partP2,
                   (void *)h->zbuf, (void *)h->p2gbuf, (void *)h->partA, (void *)h->partU,
-                  (void *)h->tailq})
+                  (void *)h->tailq, (void *)h->partAb, (void *)h->partP2b})
     if (p) (void)hipFree(p);
+  h->partAb = h->partP2b = nullptr;
   h->p2 = nullptr;
   h->tailq = nullptr;
   h->partP2 = h->zbuf = h->p2gbuf = nullptr;
@@ -1553,12 +1571,14 @@ int nls_destroy(nls_handle *h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->cstream) (void)hipStreamSynchronize(h->cstream);
   if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   peer_close(h);  // the neighbours' IPC mappings before our own allocations go
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
-  for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_bdone, h->ev_snap, h->ev_snap_done})
+  for (hipEvent_t e : {h->ev_bnd, h->ev_halo, h->ev_bdone, h->ev_snap, h->ev_snap_done, h->ev_fork, h->ev_join})
     if (e) (void)hipEventDestroy(e);
   if (h->cstream) (void)hipStreamDestroy(h->cstream);
   if (h->xstream) (void)hipStreamDestroy(h->xstream);
+  if (h->stream2) (void)hipStreamDestroy(h->stream2);
   for (auto &r : h->recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -1889,10 +1909,34 @@ void issue_step(nls_handle *h, double dt) {
     if (h->pass2) {
       // s-step passes (k_p2d on cell pairs): the sinc^2 action into the g basis's own
       // W_0 (TAIL_COMBINE_W0), then the cos basis ends in the Gautschi update that reads
-      // that one vector (TAIL_KG_END1)
-      run_lanczos2(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
-      tail_launch(h, TAIL_COMBINE_W0, tail_args(h, 1));
-      run_lanczos2(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0);
+      // that one vector (TAIL_KG_END1).  On one rank the two bases run concurrently
+      // (each basis' chain of small reduction kernels then overlaps the other's passes)
+      if (h->stream2) {
+        hip_check(h, hipEventRecord(h->ev_fork, h->stream), "hipEventRecord");
+        hip_check(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0), "hipStreamWaitEvent");
+        struct Swap {  // basis 1 on stream2 with its own partial buffers
+          nls_handle *h;
+          Swap(nls_handle *hh) : h(hh) { flip(); }
+          ~Swap() { flip(); }
+          void flip() {
+            std::swap(h->stream, h->stream2);
+            std::swap(h->partP2, h->partP2b);
+            std::swap(h->partA, h->partAb);
+          }
+        };
+        {
+          Swap sw(h);
+          run_lanczos2(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
+          tail_launch(h, TAIL_COMBINE_W0, tail_args(h, 1));
+          hip_check(h, hipEventRecord(h->ev_join, h->stream), "hipEventRecord");
+        }
+        run_lanczos2(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0);
+        hip_check(h, hipStreamWaitEvent(h->stream, h->ev_join, 0), "hipStreamWaitEvent");
+      } else {
+        run_lanczos2(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
+        tail_launch(h, TAIL_COMBINE_W0, tail_args(h, 1));
+        run_lanczos2(h, 0, 1, NLS_F_COS_SQRT, 0, dt, 0.0);
+      }
       TailArgs ta = tail_args(h, 0);
       ta.W2 = vec_ptr(h, 1, 0);
       ta.up = h->up;
