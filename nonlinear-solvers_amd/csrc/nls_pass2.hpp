@@ -63,10 +63,14 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
   __shared__ cplx sC[P2M][P2M], sD[P2M][P2M], sH[P2M][P2M];
   const int t = threadIdx.x;
   int Jn;  // J of the next pass
-  for (int e = t; e < P2M * P2M; e += NTHREADS) {
-    (&sC[0][0])[e] = (&ps->C[0][0])[e];
-    (&sD[0][0])[e] = (&ps->D[0][0])[e];
-    (&sH[0][0])[e] = (&ps->H[0][0])[e];
+  // mode 1 touches rows / columns < J + ns + 2 only (the start modes zero and write back
+  // the whole matrices, so everything beyond stays zero): stage that block
+  const int nb = (mode == 1) ? min(J + ns + 2, P2M) : P2M;
+  for (int e = t; e < nb * nb; e += NTHREADS) {
+    const int r = e / nb, c = e % nb;
+    sC[r][c] = ps->C[r][c];
+    sD[r][c] = ps->D[r][c];
+    sH[r][c] = ps->H[r][c];
   }
   if (t == 0) s_prev = ps->H[0][0].re;  // mode 2's shift: the previous step's alpha_0
   __syncthreads();
@@ -179,8 +183,8 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
       // the stored S_1..S_ns are beta times the normalised scheme's: their C rows scale
       // by 1/beta, their D columns by beta (C = D^-1 stays consistent)
       const double b = s_beta, ib = b > 0.0 ? 1.0 / b : 0.0;
-      for (int e = t; e < ns * P2M; e += NTHREADS) {
-        const int l = 1 + e / P2M, k = e % P2M;
+      for (int e = t; e < ns * nb; e += NTHREADS) {
+        const int l = 1 + e / nb, k = e % nb;
         sC[l][k] = ib * sC[l][k];
         sD[k][l] = b * sD[k][l];
       }
@@ -248,10 +252,11 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
     st->s[t] = 1.0;
   }
   __syncthreads();
-  for (int e = t; e < P2M * P2M; e += NTHREADS) {
-    (&ps->C[0][0])[e] = (&sC[0][0])[e];
-    (&ps->D[0][0])[e] = (&sD[0][0])[e];
-    (&ps->H[0][0])[e] = (&sH[0][0])[e];
+  for (int e = t; e < nb * nb; e += NTHREADS) {
+    const int r = e / nb, c = e % nb;
+    ps->C[r][c] = sC[r][c];
+    ps->D[r][c] = sD[r][c];
+    ps->H[r][c] = sH[r][c];
   }
 }
 
