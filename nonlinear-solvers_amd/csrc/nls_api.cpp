@@ -67,7 +67,7 @@ struct UpdPlan {
 
 constexpr int NSUM = 2 * MMAX + 8;  // cplx words of KState::sums
 #ifndef NLS_KG_CONCURRENT
-#define NLS_KG_CONCURRENT 1  // the two Klein-Gordon bases on two streams (one rank, s-step passes)
+#define NLS_KG_CONCURRENT 1  // the two Klein-Gordon bases / sEWI's third action on two streams (one rank, s-step passes)
 #endif
 constexpr int EVRING = 8;            // events per handle for the local transport
 
@@ -145,6 +145,7 @@ struct nls_handle {
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   cplx *partP2b = nullptr, *partAb = nullptr;
+  bool sewi_serial = false;  // the second sEWI basis could not be allocated
   int p2order = 0;             // k_p2d tile order (Geo::remap bits: 2 x-fastest, 4 no XCD bands; debug knob 3)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
   // a new state was set (nls_set_*): the next step starts its bases cold, so it is
@@ -1804,6 +1805,66 @@ void ss2_step(nls_handle *h, double dt) {
   h->w0_dt = dt;
 }
 
+// Work issued inside the scope goes to the handle's second stream with the second set
+// of partial buffers (KG's sinc^2 basis, sEWI's exp(2 tau L) action): everything in
+// the issue path takes h->stream / h->partP2 / h->partA.
+struct OnStream2 {
+  nls_handle *h;
+  explicit OnStream2(nls_handle *hh) : h(hh) { flip(); }
+  ~OnStream2() { flip(); }
+  void flip() {
+    std::swap(h->stream, h->stream2);
+    std::swap(h->partP2, h->partP2b);
+    std::swap(h->partA, h->partAb);
+  }
+};
+
+// sEWI on one rank with the s-step passes: the third Krylov action (exp(2 tau L) u_prev)
+// does not depend on the first two, so it runs on a second basis and stream while they
+// run (its Lanczos and theirs overlap each other's chains of small reduction kernels).
+// The second basis is allocated on the first sEWI step; if the memory is not there the
+// step stays serial.
+bool sewi_concurrent(nls_handle *h) {
+  // (not the register form: its y = L S_J buffer is one per handle)
+  if (!NLS_KG_CONCURRENT || h->collective || !h->pass2 || h->p2reg || !use_tail(h, TAIL_SEWI_END)) return false;
+  if (h->B[1].W) return true;
+  if (h->sewi_serial) return false;
+  if (const char *e = std::getenv("NLS_SEWI_CONCURRENT"))  // 0: the serial order (A/B)
+    if (std::atoi(e) == 0) return false;
+  const size_t bytes = (size_t)h->nvec[0] * h->vs * h->esize;
+  const size_t psb = p2state_bytes();
+  const size_t na = std::max<size_t>(2 * (size_t)h->grid_alpha, 3 * (size_t)h->grid_alpha2);
+  void *W = nullptr, *st = nullptr, *p2 = nullptr, *pa = nullptr, *pp = nullptr;
+  bool ok = hipMalloc(&W, bytes) == hipSuccess && hipMalloc(&st, sizeof(KState)) == hipSuccess &&
+            hipMalloc(&p2, 2 * psb) == hipSuccess && hipMalloc(&pa, na * sizeof(cplx)) == hipSuccess &&
+            hipMalloc(&pp, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)) == hipSuccess;
+  if (ok && !h->stream2) {
+    ok = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
+  }
+  if (!ok) {
+    (void)hipGetLastError();
+    for (void *q : {W, st, p2, pa, pp})
+      if (q) (void)hipFree(q);
+    h->sewi_serial = true;
+    return false;
+  }
+  hip_check(h, hipMemsetAsync(W, 0, bytes, h->stream), "hipMemset");
+  hip_check(h, hipMemsetAsync(st, 0, sizeof(KState), h->stream), "hipMemset");
+  hip_check(h, hipMemsetAsync(static_cast<char *>(p2) + psb, 0, psb, h->stream), "hipMemset");
+  hip_check(h, hipMemcpyAsync(p2, h->p2, psb, hipMemcpyDeviceToDevice, h->stream), "hipMemcpy(P2State)");
+  hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  (void)hipFree(h->p2);
+  h->p2 = p2;
+  h->B[1].W = W;
+  h->B[1].st = static_cast<KState *>(st);
+  h->nvec[1] = h->nvec[0];
+  h->partAb = static_cast<cplx *>(pa);
+  h->partP2b = static_cast<cplx *>(pp);
+  return true;
+}
+
 // One of the three Krylov actions of an sEWI step on basis 0: the two-vector passes
 // where the handle has them (always ending in the fused tail; each action starts cold,
 // with its own alpha_0 as the first shift -- the three start vectors differ), else the
@@ -1839,6 +1900,18 @@ int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number) {
       ensure_scratch(h);
       void *W = vec_ptr(h, 0, 0);
       KState *st = h->B[0].st;
+      // exp(2 tau L) u_prev on the second basis and stream, concurrently with the rest
+      const bool conc = sewi_concurrent(h);
+      if (conc) {
+        hip_check(h, hipEventRecord(h->ev_fork, h->stream), "hipEventRecord");
+        hip_check(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0), "hipStreamWaitEvent");
+        OnStream2 sw(h);
+        hip_check(h, hipMemcpyAsync(vec_ptr(h, 1, 0), h->uprev, bytes, hipMemcpyDeviceToDevice, h->stream), "D2D");
+        halo(h, 1, 0);
+        h->p2_warm[1] = false;
+        run_lanczos2(h, 1, 1, NLS_F_EXP, 0, 0.0, 2.0 * dt);
+        hip_check(h, hipEventRecord(h->ev_join, h->stream), "hipEventRecord");
+      }
       // B(u) -> sinc(dt L) B -> exp(tau L) (.) -> e (scratch)
       {
         void *args[] = {&h->u, &h->mf, &W, &n};
@@ -1866,12 +1939,18 @@ int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number) {
         pw_launch(h, 3, kernel_combine(true, m), args);
       }
       // exp(2 tau L) u_prev, then u = that - 2 tau e, u_prev <- old u
-      hip_check(h, hipMemcpyAsync(W, h->uprev, bytes, hipMemcpyDeviceToDevice, h->stream), "D2D");
-      halo(h, 0, 0);
-      tail = use_tail(h, TAIL_SEWI_END);
-      sewi_lanczos(h, NLS_F_EXP, 0.0, 2.0 * dt, tail);
+      const int b3 = conc ? 1 : 0;
+      if (conc) {
+        hip_check(h, hipStreamWaitEvent(h->stream, h->ev_join, 0), "hipStreamWaitEvent");
+        tail = true;
+      } else {
+        hip_check(h, hipMemcpyAsync(W, h->uprev, bytes, hipMemcpyDeviceToDevice, h->stream), "D2D");
+        halo(h, 0, 0);
+        tail = use_tail(h, TAIL_SEWI_END);
+        sewi_lanczos(h, NLS_F_EXP, 0.0, 2.0 * dt, tail);
+      }
       if (tail) {
-        TailArgs ta = tail_args(h, 0);
+        TailArgs ta = tail_args(h, b3);
         ta.u = h->u;
         ta.up = h->uprev;
         ta.e = h->scratch;
@@ -1914,18 +1993,8 @@ void issue_step(nls_handle *h, double dt) {
       if (h->stream2) {
         hip_check(h, hipEventRecord(h->ev_fork, h->stream), "hipEventRecord");
         hip_check(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0), "hipStreamWaitEvent");
-        struct Swap {  // basis 1 on stream2 with its own partial buffers
-          nls_handle *h;
-          Swap(nls_handle *hh) : h(hh) { flip(); }
-          ~Swap() { flip(); }
-          void flip() {
-            std::swap(h->stream, h->stream2);
-            std::swap(h->partP2, h->partP2b);
-            std::swap(h->partA, h->partAb);
-          }
-        };
         {
-          Swap sw(h);
+          OnStream2 sw(h);
           run_lanczos2(h, 1, 1, NLS_F_SINC2_SQRT, 0, dt, 0.0);
           tail_launch(h, TAIL_COMBINE_W0, tail_args(h, 1));
           hip_check(h, hipEventRecord(h->ev_join, h->stream), "hipEventRecord");
