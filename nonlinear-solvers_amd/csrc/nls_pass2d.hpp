@@ -309,12 +309,21 @@ __host__ __device__ constexpr int p2d_after(int J, int STW, int i, int A = 0) {
 }
 // from this step on every wait is the same (a safe bound of the replay's warm-up)
 __host__ __device__ constexpr int p2d_i0(int J, int A = 0) { return p2d_ds(J, A) + p2d_np(J, A) + 1; }
+// the first step from which the replay's wait equals the steady one (every warm-up
+// step of the current schedules but step 0 already waits the steady count)
+__host__ __device__ constexpr int p2d_isteady(int J, int STW, int A = 0) {
+  int s = p2d_i0(J, A);
+  while (s > 0 && p2d_after(J, STW, s - 1, A) == p2d_after(J, STW, p2d_i0(J, A), A)) --s;
+  return s;
+}
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 0 ? 0 : (N > 63 ? 63 : N)) : "memory");
 }
+// one compare per distinct warm-up step (a chain over every step < p2d_i0 cost ~20
+// SALU per march step at J = 12)
 template <int J, int STW, int A, int I = 0> __device__ __forceinline__ void wait_step(int i) {
-  if constexpr (I >= p2d_i0(J, A)) {
-    wait_vm<p2d_after(J, STW, I, A)>();
+  if constexpr (I >= p2d_isteady(J, STW, A)) {
+    wait_vm<p2d_after(J, STW, p2d_i0(J, A), A)>();
   } else {
     if (i == I) {
       wait_vm<p2d_after(J, STW, I, A)>();
@@ -511,7 +520,6 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // lane -> cells x0 + 2 (lane & 31) + {0, 1} (clamped into the row), halo lane
   // (0..15) -> dword lane & 1 of cell x0-2, x0-1, x0+64, x0+65
   const char *__restrict__ Cg = reinterpret_cast<const char *>(g.cf);
-  const int64_t P8 = (int64_t)P * 8;
   const int64_t coff = (int64_t)min(x0 + 2 * (lane & 31), nx - 2) * 8;
   const int hcc = (lane >> 1) & 3;
   const int64_t choff = (int64_t)clampx(hcc < 2 ? x0 - 2 + hcc : x0 + 62 + hcc) * 8 + (lane & 1) * 4;
@@ -549,10 +557,13 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // DMA this wave's two S_J rows of plane p into ring slot sl: the 64 aligned
   // cells and the 4 halo cells (the zero row outside the grid and past the
   // tile's last needed plane)
-#define P2D_ISSUE_S(p, sl)                                                              \
+// (P2D_ISSUE_SO: with the plane's byte offset pb = p * P16 kept by the caller -- the
+// march steps it by an add instead of a 64-bit multiply per step)
+#define P2D_ISSUE_S(p, sl) P2D_ISSUE_SO(p, (int64_t)(p) * P16, sl)
+#define P2D_ISSUE_SO(p, pb, sl)                                                         \
   do {                                                                                  \
     const int p_ = (p);                                                                 \
-    const int64_t pb_ = (int64_t)p_ * P16;                                              \
+    const int64_t pb_ = (pb);                                                           \
     char *dst_ = smem + ((sl) * P2D_SR + 2 * w) * P2D_SRB;                              \
     _Pragma("unroll") for (int r_ = 0; r_ < 2; ++r_) {                                  \
       /* the row inside the grid and the allocation and needed (s_lo / s_hi) */       \
@@ -578,13 +589,13 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
       const int yc_ = y0 - 2 + 2 * w + (lane >> 5), kc_ = P2D_PLANE(p_, yc_), lc_ = kc_ - z0; \
       const bool okc_ = kc_ >= 0 && kc_ < nz && lc_ >= -P2D_GHOST && lc_ < nzl + P2D_GHOST && \
                         p_ <= k1 + 1;                                                   \
-      const char *cb_ = okc_ ? Cg + (p_ * P8 + (int64_t)yc_ * nx * 8)                   \
+      const char *cb_ = okc_ ? Cg + ((pb_ >> 1) + (int64_t)yc_ * nx * 8)                \
                              : reinterpret_cast<const char *>(zbuf);                    \
       glds16(cb_ + coff, cd_ + 2 * w * P2D_CRB);                                        \
       const int yh_ = y0 - 2 + 2 * w + ((lane >> 3) & 1), kh_ = P2D_PLANE(p_, yh_), lh_ = kh_ - z0; \
       const bool okh_ = kh_ >= 0 && kh_ < nz && lh_ >= -P2D_GHOST && lh_ < nzl + P2D_GHOST && \
                         p_ <= k1 + 1;                                                   \
-      const char *hb_ = okh_ ? Cg + (p_ * P8 + (int64_t)yh_ * nx * 8)                   \
+      const char *hb_ = okh_ ? Cg + ((pb_ >> 1) + (int64_t)yh_ * nx * 8)                \
                              : reinterpret_cast<const char *>(zbuf);                    \
       if (lane < 16) glds4(hb_ + choff, cd_ + P2D_SR * P2D_CRB + 2 * w * 32);           \
     }                                                                                   \
@@ -596,9 +607,10 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // keeps every step's issue count the same.
   const char *const jb0 = reinterpret_cast<const char *>(W) + (int64_t)y * nx * 16;
   const int64_t vsb = vs * 16;
-#define P2D_ISSUE_J(p, sl)                                                              \
+#define P2D_ISSUE_J(p, sl) P2D_ISSUE_JO((int64_t)min((p), k1 - 1) * P16, sl)
+#define P2D_ISSUE_JO(jo, sl)                                                            \
   do {                                                                                  \
-    const char *b_ = jb0 + (int64_t)min((p), k1 - 1) * P16;                             \
+    const char *b_ = jb0 + (jo);                                                        \
     char *dst_ = smem + p2d_off_j(J, AK) + (((sl) * J) * P2D_TR + w) * 1024;             \
     _Pragma("unroll") for (int l_ = 0; l_ < J; ++l_) {                                  \
       asm volatile("" : "+s"(b_));  /* keep the walk: no J loop-invariant pointers */   \
@@ -775,6 +787,9 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // read the row's last cell)
   const cplx *__restrict__ jrow = W + ((int64_t)y * nx + x0 + src_lane);
   cplx svn[JPF ? J : 1];  // JPF: plane k+1's J rows, loaded one step ahead
+  // byte offsets of the planes the step issues: S plane k+DS+2, J plane min(k+NP-1, k1-1)
+  int64_t sob = (int64_t)(k0 + DS + 2) * P16;
+  int64_t job = (int64_t)min(k0 + NP - 1, k1 - 1) * P16;
   if constexpr (JPF) {
     const cplx *__restrict__ src = jrow + (int64_t)k0 * P;
 #pragma unroll
@@ -797,14 +812,14 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     // NLS_P2D_EARLY: issue first (the slots are free: S plane k-2 since the last
     // barrier, the wave's own J plane k-1 since its last step), then wait
     if constexpr (p2d_early(J, AK)) {
-      P2D_ISSUE_S(k + DS + 2, sis);
-      if constexpr (J > 0 && !LATE && !JREG && !RF) P2D_ISSUE_J(k + NP - 1, jis);
+      P2D_ISSUE_SO(k + DS + 2, sob, sis);
+      if constexpr (J > 0 && !LATE && !JREG && !RF) P2D_ISSUE_JO(job, jis);
     }
     wait_step<J, STW, AK>(i);
     raw_barrier();
     if constexpr (!p2d_early(J, AK)) {
-      P2D_ISSUE_S(k + DS + 2, sis);
-      if constexpr (J > 0 && !LATE && !JREG && !RF) P2D_ISSUE_J(k + NP - 1, jis);
+      P2D_ISSUE_SO(k + DS + 2, sob, sis);
+      if constexpr (J > 0 && !LATE && !JREG && !RF) P2D_ISSUE_JO(job, jis);
     }
     const int s1 = sk + 1 == NSL ? 0 : sk + 1, s2 = s1 + 1 == NSL ? 0 : s1 + 1;
     // L S_J of plane k+1: own row (register) + halo values, shared rows into L slot lsl^1
@@ -938,6 +953,8 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     le1 = lne;
     sk = s1;
     sis = sis + 1 == NSL ? 0 : sis + 1;
+    sob += P16;
+    if (k + NP < k1) job += P16;
     if constexpr (J > 0) {
       jr = jr + 1 == NPD ? 0 : jr + 1;
       jis = jis + 1 == NPD ? 0 : jis + 1;
@@ -952,6 +969,8 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
 #undef P2D_BYZ
 #undef P2D_ISSUE_S
 #undef P2D_ISSUE_J
+#undef P2D_ISSUE_SO
+#undef P2D_ISSUE_JO
 #undef P2D_LAP
 #undef P2D_CV
 #undef P2D_CV2
