@@ -386,6 +386,29 @@ def test_sewi_trajectory_matches_oracle(monkeypatch, form, dim, nx, ny, nz, m):
     assert rel_l2(out, ref) <= TOL_TRAJ
 
 
+@pytest.mark.parametrize("dim,nx,ny,nz,m", [(3, 12, 12, 12, 15), (3, 130, 8, 20, 15)])
+def test_sewi_concurrent_action_bitwise_equal_serial(monkeypatch, dim, nx, ny, nz, m):
+    """The third Krylov action of an sEWI step (exp(2 tau L) u_prev) on a second basis and
+    stream, concurrently with the first two (nls_api.cpp sewi_concurrent): the same kernels
+    on the same inputs, so the trajectory is bit-for-bit the serial order's."""
+    monkeypatch.setenv("NLS_PASS2", "1")
+    monkeypatch.setenv("NLS_P2_REG", "0")
+    L, dt, steps = 4.0, 1e-3, 5
+    dx = 2 * L / (nx - 1)
+    u, mf, c = fields(dim, nx, ny, nz, seed=11)
+    out = {}
+    for conc in ("1", "0"):
+        monkeypatch.setenv("NLS_SEWI_CONCURRENT", conc)
+        with solver(dim, nx, ny, nz, dx, m) as s:
+            s.set_coefficients(mf, c)
+            s.set_field(u)
+            for i in range(1, steps + 1):
+                s.step_sewi(dt, i)
+                s.apply_bc()
+            out[conc] = s.get_field()
+    assert np.array_equal(out["1"].view(np.uint64), out["0"].view(np.uint64))
+
+
 def test_sewi_golden_and_errors():
     d = np.load(os.path.join(GOLD, "sewi_3d.npz"))
     n, m, dt = int(d["n"]), int(d["m"]), float(d["dt"])
