@@ -145,6 +145,7 @@ struct nls_handle {
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   cplx *partP2b = nullptr, *partAb = nullptr;
+  void *prepad = nullptr;  // NLS_DEBUG_PREPAD_KB: a dummy allocation ahead of the bases (placement probe)
   bool sewi_serial = false;  // the second sEWI basis could not be allocated
   int p2order = 0;             // k_p2d tile order (Geo::remap bits: 2 x-fastest, 4 no XCD bands; debug knob 3)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
@@ -1289,6 +1290,11 @@ void alloc_all(nls_handle *h) {
   // its own allocation, tools/exp_uslot.sh in round 1; removed in round 4.  Physically
   // contiguous allocations (hipDeviceMallocContiguous) were slower: 512^3 update 24.8-24.9
   // vs 24.3 ms per step, profiles/r05/envab_contig.txt; round 5, not kept)
+  // (placement probe: shifts every later allocation by the given size; the same code then
+  // runs on other physical pages -- tools/gpu.sh envab with NLS_DEBUG_PREPAD_KB=...)
+  if (const char *e = std::getenv("NLS_DEBUG_PREPAD_KB"))
+    if (const size_t kb = std::strtoull(e, nullptr, 10))
+      hip_check(h, hipMalloc(&h->prepad, kb * 1024), "hipMalloc(prepad)");
   for (int b = 0; b < h->nbasis; ++b) {
     const size_t bytes = (size_t)h->nvec[b] * h->vs * h->esize;
     hip_check(h, hipMalloc(&h->B[b].W, bytes), "hipMalloc(basis)");
@@ -1387,9 +1393,10 @@ void free_all(nls_handle *h) {
   for (void *p : {h->u, (void *)h->up, (void *)h->mf, (void *)h->cfb, h->scratch, h->snap, h->uprev,
                   (void *)h->vel, h->xedge, (void *)h->partX, h->p2, (void *)h->partP2,
                   (void *)h->zbuf, (void *)h->p2gbuf, (void *)h->partA, (void *)h->partU,
-                  (void *)h->tailq, (void *)h->partAb, (void *)h->partP2b})
+                  (void *)h->tailq, (void *)h->partAb, (void *)h->partP2b, h->prepad})
     if (p) (void)hipFree(p);
   h->partAb = h->partP2b = nullptr;
+  h->prepad = nullptr;
   h->p2 = nullptr;
   h->tailq = nullptr;
   h->partP2 = h->zbuf = h->p2gbuf = nullptr;
