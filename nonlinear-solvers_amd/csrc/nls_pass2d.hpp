@@ -108,7 +108,9 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 // ring the rings take ~47 KiB, so two workgroups fit per CU and the second covers the
 // first's barriers and waits, and short tiles (no J-ring prologue) stream from a
 // compact address window (512^3, same box: J = 10 5.17 ms at kz 32 vs 5.36 at 256 and
-// 5.22 through the ring).  J = 12 with Z does not fit: all rows live across the step
+// 5.22 through the ring).  From J = 2 (round 5, same box): 3D 512^3 J = 2 2.00 -> 1.93 ms,
+// J = 4 2.78 -> 2.71, the step -0.1 ms; SG 8192^2 +0.2 ms (2.7 %), 2D 4096^2 and G2 (A = 1)
+// unchanged -- not kept (profiles/r05/p2ab_jreg24.txt, ab_jreg24.txt).  J = 12 with Z does not fit: all rows live across the step
 // took 256 VGPRs and scratch; half of them loaded after the S issue (SGPR-walked
 // addresses) fit but ran slower than the ring (6.16 vs 6.06 ms; round 4,
 // profiles/r04/p2ab_512.txt).

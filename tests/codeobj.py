@@ -300,7 +300,7 @@ class P2dSchedule:
 
 def check_p2d(funcs, meta, sched: P2dSchedule):
     """Per k_p2d instantiation: (name, problems list, record dict).  Checks: no
-    scratch / buffer / flat access and no private segment or VGPR spill; the march
+    scratch / buffer / flat access (nor an accessed private segment) and no VGPR spill; the march
     loop issues exactly the source's loads per step (2 + J DMA rows + 2 halo
     pieces) and its STW stores (once, or once per full / ragged-tile branch), no
     other VMEM operation; and its s_waitcnt vmcnt values are exactly the
@@ -319,7 +319,10 @@ def check_p2d(funcs, meta, sched: P2dSchedule):
         if bad:
             probs.append(f"scratch/buffer/flat ops in the kernel: {bad}")
         md = meta.get(name, {})
-        if md.get("private_segment_fixed_size", "0") != "0":
+        # a private segment the code never touches (the register scavenger's reserved
+        # emergency slot next to many SGPR spills) issues no VMEM op: only one that is
+        # accessed -- by the scratch / buffer / flat ops flagged above -- breaks the count
+        if md.get("private_segment_fixed_size", "0") != "0" and bad:
             probs.append(f"private segment {md.get('private_segment_fixed_size')} B")
         if md.get("vgpr_spill_count", "0") != "0":
             probs.append(f"vgpr spills {md.get('vgpr_spill_count')}")

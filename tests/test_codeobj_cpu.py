@@ -1,7 +1,7 @@
 """CPU: the hand-counted vmcnt schedule of k_p2d holds in the compiled gfx950 code
 object (tests/codeobj.py; nls_pass2d.hpp:30-38, p2d_after / wait_step).  For every
-k_p2d<J, HZ, D2, PR, A> instantiation: no scratch / buffer / flat access, no private
-segment, no VGPR spill; the march loop issues exactly the source's DMA loads and
+k_p2d<J, HZ, D2, PR, A> instantiation: no scratch / buffer / flat access (so no accessed
+private segment), no VGPR spill; the march loop issues exactly the source's DMA loads and
 stores; and its s_waitcnt vmcnt values are exactly the source's p2d_after values."""
 import os
 
@@ -42,18 +42,21 @@ def test_p2d_vmcnt_contract_holds(p2d_results):
 
 
 def test_checker_flags_an_extra_vmem_op():
-    """The loop check is not vacuous: one more load in a synthetic loop body fails it."""
+    """The loop check is not vacuous: one more load in a synthetic loop body fails it
+    (a J-ring pass: J = 12, 2 S rows + 12 J rows per step, 2 halo pieces, 2 stores)."""
     sched = C.P2dSchedule(HDR)
-    name = "_ZN3nls5k_p2dILi2ELb1ELb0ELb0ELb0EEEv"
-    waits = [(0x0f0 + 4 * i, "s_waitcnt", f"vmcnt({w})") for i, w in enumerate(sched.waits(2, 2))]
+    J = 12
+    assert not sched.jreg(J)
+    name = f"_ZN3nls5k_p2dILi{J}ELb1ELb0ELb0ELb0EEEv"
+    waits = [(0x0f0 + 4 * i, "s_waitcnt", f"vmcnt({w})") for i, w in enumerate(sched.waits(J, 2))]
     body = waits + \
-        [(0x104 + 4 * i, "global_load_lds_dwordx4", "v[2:3], off") for i in range(4)] + \
-        [(0x120, "global_load_lds_dword", ""), (0x124, "global_load_lds_dword", ""),
-         (0x128, "global_store_dwordx4", ""), (0x12c, "global_store_dwordx4", ""),
-         (0x130, "s_cbranch_scc1", f"<{name}+0x0f0>")]
+        [(0x104 + 4 * i, "global_load_lds_dwordx4", "v[2:3], off") for i in range(2 + J)] + \
+        [(0x180, "global_load_lds_dword", ""), (0x184, "global_load_lds_dword", ""),
+         (0x188, "global_store_dwordx4", ""), (0x18c, "global_store_dwordx4", ""),
+         (0x190, "s_cbranch_scc1", f"<{name}+0x0f0>")]
     ins = [(0x0, "s_load_dwordx2", "")] + body
     md = {name: {"private_segment_fixed_size": "0", "vgpr_spill_count": "0"}}
     assert C.check_p2d({name: ins}, md, sched)[0][1] == []
-    extra = ins[:-1] + [(0x12e, "scratch_load_dword", "v1, off"), ins[-1]]
+    extra = ins[:-1] + [(0x18e, "scratch_load_dword", "v1, off"), ins[-1]]
     probs = C.check_p2d({name: extra}, md, sched)[0][1]
     assert probs and any("scratch" in p for p in probs)
