@@ -133,10 +133,10 @@ print(f\"$v rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} domina
       cat "$OUT/p2ab.txt" ;;
     envab)
       # same-box A/B of environment settings on one workload: ARG = WL:SET,SET,... ("-" =
-      # none), two interleaved rounds -> envab_WL.txt
+      # none), two interleaved rounds (ENVAB_REPS) -> envab_WL.txt
       wl=${arg%%:*}
       sets=${arg#*:}
-      for rep in 1 2; do
+      for rep in $(seq 1 "${ENVAB_REPS:-2}"); do
         for ev in $(echo "$sets" | tr ',' ' '); do
           [ "$ev" != "-" ] && export "${ev?}"
           run 300 "$OUT/envab_cur.json" python bench.py --workload "$wl" --steps 10 --warmup 2 --no-cpu-baseline
