@@ -1862,6 +1862,11 @@ bool sewi_concurrent(nls_handle *h) {
   hip_check(h, hipMemsetAsync(static_cast<char *>(p2) + psb, 0, psb, h->stream), "hipMemset");
   hip_check(h, hipMemcpyAsync(p2, h->p2, psb, hipMemcpyDeviceToDevice, h->stream), "hipMemcpy(P2State)");
   hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  // a step graph captured by nls_step holds the old P2State address: re-capture
+  if (h->gexec) {
+    hip_check(h, hipGraphExecDestroy(h->gexec), "hipGraphExecDestroy");
+    h->gexec = nullptr;
+  }
   (void)hipFree(h->p2);
   h->p2 = p2;
   h->B[1].W = W;

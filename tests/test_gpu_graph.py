@@ -53,8 +53,11 @@ def test_graph_replay_bitwise_nlse(monkeypatch, dim, n, eq):
     assert g1 == 15 - 4   # eager: the first step, both dt changes, the step after set_field
 
 
-@pytest.mark.parametrize("dim,n", [(3, 14), (2, 40)])
+@pytest.mark.parametrize("dim,n", [(3, 14), (3, 16), (2, 40)])
 def test_graph_replay_bitwise_g2(monkeypatch, dim, n):
+    """n = 16 (3D): the anisotropic s-step passes; the sEWI steps then move the P2State
+    to make room for their second basis (sewi_concurrent), which drops the step graph
+    captured before them -- the steps after re-capture it."""
     def body():
         cells = n ** dim
         nz = n if dim == 3 else 1
