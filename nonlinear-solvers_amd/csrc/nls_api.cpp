@@ -1893,7 +1893,7 @@ void sewi_lanczos(nls_handle *h, int f, double tr, double ti, bool &tail) {
 
 int nls_step_sewi(nls_handle *h, double dt, uint32_t step_number) {
   return guarded(h, [&] {
-    if (!h->ani) fail(h, NLS_ERR_STATE, "nls_step_sewi needs a G2 (NLS_NLSE_G2) handle");
+    if (!h->ani || h->kg) fail(h, NLS_ERR_STATE, "nls_step_sewi needs a G2 (NLS_NLSE_G2) handle");
     if (!h->field_set) fail(h, NLS_ERR_STATE, "no field set");
     if (!h->coef_set) fail(h, NLS_ERR_STATE, "G2: nls_set_coefficients not called");
     if (!std::isfinite(dt)) fail(h, NLS_ERR_ARG, "dt not finite");

@@ -427,6 +427,13 @@ def test_sewi_golden_and_errors():
         with pytest.raises(nls_amd.NlsError) as e:
             s.step_sewi(1e-3, 1)
         assert e.value.code == -6
+    # the Klein-Gordon handle has the same operator but a real field: no sEWI
+    with nls_amd.Solver(3, 8, 8, 8, 0.5, equation=nls_amd.KG_GAUTSCHI, m=4) as s:
+        s.set_coefficients(np.ones(512), np.ones(512))
+        s.set_sg_state(np.ones(512), np.ones(512))
+        with pytest.raises(nls_amd.NlsError) as e:
+            s.step_sewi(1e-3, 1)
+        assert e.value.code == -6
 
 
 @pytest.mark.parametrize("dim", [3, 2])
