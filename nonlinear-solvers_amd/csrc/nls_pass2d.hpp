@@ -61,8 +61,13 @@ constexpr int P2D_CSB = P2D_SR * P2D_CRB + P2D_SR * 32;
 // (Klein-Gordon): c is then one f64 per cell, so a row of 64 pairs is 128 c values =
 // the same 1 KiB + 4 halo pairs as an S_J row, and its c ring is staged exactly like
 // the S ring (P2D_SRB per row; c of cell 2P + h at double index 2P + h of the row,
-// halo pairs P = 64..67 as in S)
-__host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_SRB : (A ? P2D_CSB : 0); }
+// halo pairs P = 64..67 as in S); 3 the isotropic 2D passes (planes of 4 rows, D2), which
+// are kind 0 except where their register rows start (p2d_jreg).  p2d_kind maps 3 to 0 for
+// every other rule.
+__host__ __device__ constexpr int p2d_kind(int A) { return A == 3 ? 0 : A; }
+__host__ __device__ constexpr int p2d_csb(int A) {
+  return p2d_kind(A) == 2 ? P2D_SR * P2D_SRB : (p2d_kind(A) ? P2D_CSB : 0);
+}
 #ifndef NLS_P2D_OCC2_MAXJ
 #define NLS_P2D_OCC2_MAXJ 6   // two workgroups per CU up to this J (J = 6: late J ring, 512^3 4.08 -> 3.64 ms; J = 8 no gain)
 #endif
@@ -97,20 +102,24 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 #define NLS_P2D_JREG 1        // isotropic passes from J = NLS_P2D_JREG_MINJ: J rows in registers (p2d_jreg)
 #endif
 #ifndef NLS_P2D_JREG_MINJ
-#define NLS_P2D_JREG_MINJ 8
+#define NLS_P2D_JREG_MINJ 2    // 3D
+#endif
+#ifndef NLS_P2D_JREG2D_MINJ
+#define NLS_P2D_JREG2D_MINJ 8  // 2D (kind 3)
 #endif
 #ifndef NLS_P2D_JREG_MAXJ
 #define NLS_P2D_JREG_MAXJ 10
 #endif
-// The isotropic passes at J = 8, 10 read their J stored rows straight into registers
+// The isotropic passes at J = 2 .. 10 in 3D, J = 8, 10 in 2D read their J stored rows straight into registers
 // (one non-temporal load per row at the top of each step, awaited by the compiler's own
 // counted vmcnt before the first use) instead of through an LDS ring: without the J
 // ring the rings take ~47 KiB, so two workgroups fit per CU and the second covers the
 // first's barriers and waits, and short tiles (no J-ring prologue) stream from a
 // compact address window (512^3, same box: J = 10 5.17 ms at kz 32 vs 5.36 at 256 and
 // 5.22 through the ring).  From J = 2 (round 5, same box): 3D 512^3 J = 2 2.00 -> 1.93 ms,
-// J = 4 2.78 -> 2.71, the step -0.1 ms; SG 8192^2 +0.2 ms (2.7 %), 2D 4096^2 and G2 (A = 1)
-// unchanged -- not kept (profiles/r05/p2ab_jreg24.txt, ab_jreg24.txt).  J = 12 with Z does not fit: all rows live across the step
+// J = 4 2.78 -> 2.71, the step -0.1 ms; but SG 8192^2 +0.2 ms (2.7 %) and 2D 4096^2 and G2
+// (A = 1) unchanged, so 2D keeps the ring below J = 8 (profiles/r05/p2ab_jreg24.txt,
+// ab_jreg24.txt).  J = 12 with Z does not fit: all rows live across the step
 // took 256 VGPRs and scratch; half of them loaded after the S issue (SGPR-walked
 // addresses) fit but ran slower than the ring (6.16 vs 6.06 ms; round 4,
 // profiles/r04/p2ab_512.txt).
@@ -131,6 +140,7 @@ __host__ __device__ constexpr int p2d_csb(int A) { return A == 2 ? P2D_SR * P2D_
 #endif
 __host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
   return NLS_P2D_JREG && (A == 0   ? J >= NLS_P2D_JREG_MINJ && J <= NLS_P2D_JREG_MAXJ
+                          : A == 3 ? J >= NLS_P2D_JREG2D_MINJ && J <= NLS_P2D_JREG_MAXJ
                           : A == 1 ? J >= NLS_P2A_JREG_MINJ && J <= NLS_P2A_JREG_MAXJ
                                    : J > 0 && J <= NLS_P2A2_OCC2_MAXJ);
 }
@@ -142,7 +152,9 @@ __host__ __device__ constexpr bool p2d_jreg(int J, int A = 0) {
 #ifndef NLS_P2D_JPF_MAXJ
 #define NLS_P2D_JPF_MAXJ 0
 #endif
-__host__ __device__ constexpr bool p2d_jpf(int J, int A = 0) { return p2d_jreg(J, A) && A == 0 && J <= NLS_P2D_JPF_MAXJ; }
+__host__ __device__ constexpr bool p2d_jpf(int J, int A = 0) {
+  return p2d_jreg(J, A) && p2d_kind(A) == 0 && J <= NLS_P2D_JPF_MAXJ;
+}
 // Workgroups per CU: two where the registers (<= 256 per lane) and the rings
 // (<= 80 KiB) allow, so the second workgroup's waves cover the first's barriers
 // and LDS latencies; one for the long passes.
@@ -161,19 +173,20 @@ __host__ __device__ constexpr bool p2d_jpf(int J, int A = 0) { return p2d_jreg(J
 __host__ __device__ constexpr int p2d_occ(int J, int A = 0) {
   return A == 1   ? (J <= NLS_P2A_OCC2_MAXJ || p2d_jreg(J, A) ? 2 : 1)
          : A == 2 ? (J <= NLS_P2A2_OCC2_MAXJ ? 2 : 1)  // pairs: the c ring as large as S's
-                  : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ || p2d_jreg(J) ? 2 : 1));
+                  : (J == 0 ? NLS_P2D_OCC0 : (J <= NLS_P2D_OCC2_MAXJ || p2d_jreg(J, A) ? 2 : 1));
 }
 // the x-halo L values of the tile computed by one wave into LDS (EXT1), and the X / Z
 // coefficients in LDS -- except on the cell-pair passes at two workgroups per CU (above)
 __host__ __device__ constexpr bool p2d_ext1(int J, int A = 0) { return NLS_P2D_EXT1 && !(A == 2 && p2d_occ(J, A) == 2); }
 __host__ __device__ constexpr bool p2d_rcoef(int J, int A = 0) { return A == 2 && p2d_occ(J, A) == 2; }
+// (these two test A == 2 only, which kind 3 never is)
 // S ring: the planes k .. k+2 being read, DS planes of look-ahead and the slot of
 // plane k-2 (free since the previous step's barrier), into which a step issues
 // before its own wait and barrier
 __host__ __device__ constexpr int p2d_ds(int J, int A = 0) {
-  return A ? (p2d_occ(J, A) == 2 ? (J == 0 && A == 1 ? 2 : 1) : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J >= 22 ? 1 : NLS_P2A_DS1)))
-           : (p2d_occ(J) >= 3 ? 1
-                                : (p2d_occ(J) == 2
+  return p2d_kind(A) ? (p2d_occ(J, A) == 2 ? (J == 0 && A == 1 ? 2 : 1) : (J <= NLS_P2D_DS3_MAXJ ? 3 : (J >= 22 ? 1 : NLS_P2A_DS1)))
+           : (p2d_occ(J, A) >= 3 ? 1
+                                : (p2d_occ(J, A) == 2
                                        ? (J == 0 ? 3 : (J <= NLS_P2D_DS2_MAXJ ? 2 : 1))
                                        : (J == 0 ? 6
                                                  : (J <= NLS_P2D_DS3_MAXJ
@@ -185,7 +198,7 @@ __host__ __device__ constexpr int p2d_ds(int J, int A = 0) {
 // early issue only at one workgroup per CU (two: the other workgroup covers the wait,
 // and the LDS is short); not where the anisotropic rings leave no slot for it
 __host__ __device__ constexpr bool p2d_early(int J, int A = 0) {
-  return A ? NLS_P2A_EARLY && p2d_occ(J, A) == 1 && J < 22 : NLS_P2D_EARLY && p2d_occ(J) == 1;
+  return p2d_kind(A) ? NLS_P2A_EARLY && p2d_occ(J, A) == 1 && J < 22 : NLS_P2D_EARLY && p2d_occ(J, A) == 1;
 }
 __host__ __device__ constexpr int p2d_nsl(int J, int A = 0) { return p2d_ds(J, A) + 3 + (p2d_early(J, A) ? 1 : 0); }
 __host__ __device__ constexpr int p2d_off_c_ring(int J, int A = 0) { return p2d_nsl(J, A) * P2D_SR * P2D_SRB; }
@@ -221,7 +234,7 @@ __host__ __device__ constexpr bool p2d_late(int J, int A = 0) { return J > 0 && 
 #define NLS_P2D_RF 0
 #endif
 __host__ __device__ constexpr bool p2d_rf(int J, int A = 0) {
-  return NLS_P2D_RF && A == 0 && J > 0 && !p2d_jreg(J, A) && p2d_np(J, A) >= 2;
+  return NLS_P2D_RF && p2d_kind(A) == 0 && J > 0 && !p2d_jreg(J, A) && p2d_np(J, A) >= 2;
 }
 __host__ __device__ constexpr int p2d_off_c(int J, int A = 0) {
   return p2d_off_j(J, A) + p2d_np(J, A) * J * P2D_TR * 1024;
@@ -229,7 +242,8 @@ __host__ __device__ constexpr int p2d_off_c(int J, int A = 0) {
 __host__ __device__ constexpr int p2d_lds_bytes(int J, int A = 0) { return p2d_off_c(J, A) + p2d_coef_bytes(J, A); }
 __host__ __device__ constexpr bool p2d_rings_ok(int J, int A = 0) {
   return J == 0 ? p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS
-                : (J <= (A == 2 ? P2D_JMAX_A2 : (A ? P2D_JMAX_A : P2D_JMAX)) && (p2d_np(J, A) >= 1 || p2d_jreg(J, A)) &&
+                : (J <= (A == 2 ? P2D_JMAX_A2 : (p2d_kind(A) ? P2D_JMAX_A : P2D_JMAX)) &&
+                   (p2d_np(J, A) >= 1 || p2d_jreg(J, A)) &&
                    p2d_lds_bytes(J, A) * p2d_occ(J, A) <= P2D_LDS);
 }
 static_assert(p2d_rings_ok(2) && p2d_rings_ok(4) && p2d_rings_ok(6) && p2d_rings_ok(8) && p2d_rings_ok(10) &&
@@ -250,7 +264,7 @@ static_assert(p2d_rings_ok(0, 2) && p2d_rings_ok(2, 2) && p2d_rings_ok(4, 2) && 
 // plane k0); then per step: [S group k+DS+2 and J group k+NP-1] before the wait
 // (early) or after it, the late J group k+1 after the J rows are read, then the STW
 // stores.  Step i needs S(k+2) and J plane k.
-__host__ __device__ constexpr int p2d_nsd(int A) { return A == 2 ? 8 : (A ? 6 : 4); }
+__host__ __device__ constexpr int p2d_nsd(int A) { return A == 2 ? 8 : (p2d_kind(A) ? 6 : 4); }
 // look-ahead S groups issued, with the J groups, before the prologue's wait (their slots
 // (4 + d) % NSL are clear of the prologue's slots 0..3: the one-workgroup-per-CU passes
 // with early issue); 0: every look-ahead group after the wait, S before J (the round-3
@@ -410,21 +424,22 @@ __device__ __forceinline__ cplx pr_lap(cplx c, cplx xm, cplx xp, cplx yz, double
 // PEER: the multi-rank peer-store variant (3D isotropic; NLS_PEER=1): after the march the
 // pass's last output's boundary planes also go to the neighbours' ghost planes
 template <int J, bool HZ, bool D2 = false, bool PR = false, bool A = false, bool PEER = false>
-__global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
+__global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : (D2 ? 3 : 0))) void k_p2d(cplx *__restrict__ W, int64_t vs, Geo g,
                                                               const P2State *__restrict__ ps,
                                                               cplx *__restrict__ part, int nb,
                                                               const cplx *__restrict__ zbuf, int poff) {
   // the anisotropic kind of the ring functions (p2d_csb): 1 complex, 2 real cell pairs
   constexpr int AK = A ? (PR ? 2 : 1) : 0;
-  static_assert(p2d_rings_ok(J, AK), "rings exceed LDS");
+  constexpr int KA = !A && D2 ? 3 : AK;  // the kind the ring and wait rules take (3: isotropic 2D)
+  static_assert(p2d_rings_ok(J, KA), "rings exceed LDS");
   static_assert(!(A && D2), "the anisotropic pass is 3D");
-  constexpr int DS = p2d_ds(J, AK), NSL = p2d_nsl(J, AK), NP = p2d_np(J, AK);
-  constexpr bool LATE = p2d_late(J, AK), JREG = p2d_jreg(J, AK), RF = p2d_rf(J, AK), JPF = p2d_jpf(J, AK);
-  constexpr bool EXT1 = p2d_ext1(J, AK), RCOEF = p2d_rcoef(J, AK);
+  constexpr int DS = p2d_ds(J, KA), NSL = p2d_nsl(J, KA), NP = p2d_np(J, KA);
+  constexpr bool LATE = p2d_late(J, KA), JREG = p2d_jreg(J, KA), RF = p2d_rf(J, KA), JPF = p2d_jpf(J, KA);
+  constexpr bool EXT1 = p2d_ext1(J, KA), RCOEF = p2d_rcoef(J, KA);
   // WC: the own row's face weights div(c grad) needs at plane k were computed with its
   // L S_J one step earlier (same c, same conditions, so the same bits): kept in
   // registers (nwc -> cwc) instead of recomputed from the c ring by L^2 S_J
-  constexpr bool WC = NLS_P2D_WCACHE && A && HZ && (p2d_occ(J, AK) == 1 || J <= 6);  // (J = 8 at two per CU: scratch)
+  constexpr bool WC = NLS_P2D_WCACHE && A && HZ && (p2d_occ(J, KA) == 1 || J <= 6);  // (J = 8 at two per CU: scratch)
   constexpr int NWC = AK == 2 ? 13 : 7;
   double nwc[NWC], cwc[NWC];
   constexpr int STW = HZ ? 2 : 1;            // stores per step
@@ -433,12 +448,12 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   constexpr int NC = (HZ ? 2 * (J + 1) + 3 : J + 2) + (J == 0 ? 1 : 0);
   constexpr int NPD = NP > 0 ? NP : 1;
   constexpr int RW = P2D_SRB / 16;           // cplx per staged S row (68)
-  __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J, AK)];
+  __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J, KA)];
   const cplx *Sr = reinterpret_cast<const cplx *>(smem);             // [NSL][P2D_SR][RW]
-  const double *Cr = reinterpret_cast<const double *>(smem + p2d_off_c_ring(J, AK));  // A: [NSL][p2d_csb/8]
-  cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J, AK));       // [2][P2D_LR][64]
+  const double *Cr = reinterpret_cast<const double *>(smem + p2d_off_c_ring(J, KA));  // A: [NSL][p2d_csb/8]
+  cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J, KA));       // [2][P2D_LR][64]
   cplx *Lx = Lr + 2 * P2D_LR * 64;                                     // [2][P2D_TR][2]
-  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J, AK));       // [J+1] (not with RCOEF)
+  cplx *cX = reinterpret_cast<cplx *>(smem + p2d_off_c(J, KA));       // [J+1] (not with RCOEF)
   cplx *cZ = cX + (J + 1);                                           // [J+1]
   cplx rcX[RCOEF ? J + 1 : 1], rcZ[RCOEF ? J + 1 : 1];               // RCOEF: in registers
   // w through readfirstlane: wave-uniform for the compiler too, so row and plane
@@ -577,7 +592,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
       if (lane < 16) dma4(b_, hoff, dst_ + r_ * P2D_SRB + 1024);                        \
       if constexpr (AK == 2) {                                                          \
         /* cell pairs: the c row of the same S row, staged as S rows are */           \
-        char *cd_ = smem + p2d_off_c_ring(J, AK) + ((sl) * P2D_SR + 2 * w + r_) * P2D_SRB; \
+        char *cd_ = smem + p2d_off_c_ring(J, KA) + ((sl) * P2D_SR + 2 * w + r_) * P2D_SRB; \
         const char *c_ = ok_ ? Cg + o_ : reinterpret_cast<const char *>(zbuf);          \
         asm volatile("" : "+s"(c_));                                                    \
         dma16(c_, xoff, cd_, 0);                                                        \
@@ -587,7 +602,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     if constexpr (AK == 1) {                                                           \
       /* the c rows of the same two S rows: lanes 0..31 / 32..63 two cells each of   \
          row 2w / 2w+1, then their halo cells on lanes 0..15 (8 lanes x 4 B a row) */ \
-      char *cd_ = smem + p2d_off_c_ring(J, AK) + (sl) * P2D_CSB;                        \
+      char *cd_ = smem + p2d_off_c_ring(J, KA) + (sl) * P2D_CSB;                        \
       const int yc_ = y0 - 2 + 2 * w + (lane >> 5), kc_ = P2D_PLANE(p_, yc_), lc_ = kc_ - z0; \
       const bool okc_ = kc_ >= 0 && kc_ < nz && lc_ >= -P2D_GHOST && lc_ < nzl + P2D_GHOST && \
                         p_ <= k1 + 1;                                                   \
@@ -613,7 +628,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
 #define P2D_ISSUE_JO(jo, sl)                                                            \
   do {                                                                                  \
     const char *b_ = jb0 + (jo);                                                        \
-    char *dst_ = smem + p2d_off_j(J, AK) + (((sl) * J) * P2D_TR + w) * 1024;             \
+    char *dst_ = smem + p2d_off_j(J, KA) + (((sl) * J) * P2D_TR + w) * 1024;             \
     _Pragma("unroll") for (int l_ = 0; l_ < J; ++l_) {                                  \
       asm volatile("" : "+s"(b_));  /* keep the walk: no J loop-invariant pointers */   \
       dma16(b_, xoff, dst_ + l_ * P2D_TR * 1024, 1);                                    \
@@ -740,7 +755,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
   // one memory latency, not two
   // (the J groups the prologue issues: none for J = 0 and the register-row passes, which
   // have no J ring -- as p2d_after's replay skips them)
-  constexpr int DSPRE = p2d_dspre(J, AK), PJ = (J == 0 || JREG) ? 0 : (LATE ? 1 : (RF ? NP : NP - 1));
+  constexpr int DSPRE = p2d_dspre(J, KA), PJ = (J == 0 || JREG) ? 0 : (LATE ? 1 : (RF ? NP : NP - 1));
 #pragma unroll
   for (int d = 0; d < DSPRE; ++d) P2D_ISSUE_S(k0 + 2 + d, (4 + d) % NSL);
   if constexpr (DSPRE > 0) {
@@ -751,7 +766,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
       for (int d = 0; d < PJ; ++d) P2D_ISSUE_J(k0 + d, d);
     }
   }
-  wait_vm<DSPRE * p2d_nsd(AK) + (DSPRE > 0 ? PJ * J : 0)>();
+  wait_vm<DSPRE * p2d_nsd(KA) + (DSPRE > 0 ? PJ * J : 0)>();
   raw_barrier();
   cplx lq0, lq1, le1 = {0.0, 0.0};  // L S_J of planes k-1 and k (own row), (!EXT1) halo values of plane k
   P2D_LAP(lq0, k0 - 1, w + 2, 0, 1, 2, x, lane, mi, pi, 0);
@@ -813,13 +828,13 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     }
     // NLS_P2D_EARLY: issue first (the slots are free: S plane k-2 since the last
     // barrier, the wave's own J plane k-1 since its last step), then wait
-    if constexpr (p2d_early(J, AK)) {
+    if constexpr (p2d_early(J, KA)) {
       P2D_ISSUE_SO(k + DS + 2, sob, sis);
       if constexpr (J > 0 && !LATE && !JREG && !RF) P2D_ISSUE_JO(job, jis);
     }
-    wait_step<J, STW, AK>(i);
+    wait_step<J, STW, KA>(i);
     raw_barrier();
-    if constexpr (!p2d_early(J, AK)) {
+    if constexpr (!p2d_early(J, KA)) {
       P2D_ISSUE_SO(k + DS + 2, sob, sis);
       if constexpr (J > 0 && !LATE && !JREG && !RF) P2D_ISSUE_JO(job, jis);
     }
@@ -829,7 +844,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : 0)) void k_
     P2D_LROWS(k + 1, sk, s1, s2, lsl ^ 1, ln, lne);
     // the J stored vectors of this cell and S_J itself
     if constexpr (J > 0 && !JREG) {
-      const cplx *jv = reinterpret_cast<const cplx *>(smem + p2d_off_j(J, AK) + ((jr * J) * P2D_TR + w) * 1024);
+      const cplx *jv = reinterpret_cast<const cplx *>(smem + p2d_off_j(J, KA) + ((jr * J) * P2D_TR + w) * 1024);
 #pragma unroll
       for (int l = 0; l < J; ++l) sv[l] = jv[l * P2D_TR * 64 + lane];
       if constexpr (LATE) {

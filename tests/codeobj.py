@@ -165,6 +165,7 @@ class P2dSchedule:
         self.JPF = define("NLS_P2D_JPF_MAXJ")
         self.JREG = define("NLS_P2D_JREG")
         self.JREG_MINJ, self.JREG_MAXJ = define("NLS_P2D_JREG_MINJ"), define("NLS_P2D_JREG_MAXJ")
+        self.JREG2D_MINJ = define("NLS_P2D_JREG2D_MINJ")
         self.JREGA_MINJ, self.JREGA_MAXJ = define("NLS_P2A_JREG_MINJ"), define("NLS_P2A_JREG_MAXJ")
         self.OCC2A2 = define("NLS_P2A2_OCC2_MAXJ")
         self.EXT1 = define("NLS_P2D_EXT1")
@@ -174,12 +175,19 @@ class P2dSchedule:
 
     TR = 4
 
+    @staticmethod
+    def kind(A):
+        """p2d_kind: kind 3 (the isotropic 2D passes) is kind 0 except for p2d_jreg."""
+        return 0 if A == 3 else A
+
     def jreg(self, J, A=0):
         """J rows loaded into registers (no J ring)."""
         if not self.JREG:
             return False
         if A == 0:
             return self.JREG_MINJ <= J <= self.JREG_MAXJ
+        if A == 3:
+            return self.JREG2D_MINJ <= J <= self.JREG_MAXJ
         if A == 1:
             return self.JREGA_MINJ <= J <= self.JREGA_MAXJ
         return 0 < J <= self.OCC2A2
@@ -189,11 +197,11 @@ class P2dSchedule:
             return 2 if (J <= self.OCC2A or self.jreg(J, A)) else 1
         if A == 2:
             return 2 if J <= self.OCC2A2 else 1
-        return self.OCC0 if J == 0 else (2 if J <= self.OCC2 or self.jreg(J) else 1)
+        return self.OCC0 if J == 0 else (2 if J <= self.OCC2 or self.jreg(J, A) else 1)
 
     def ds(self, J, A=0):
         o = self.occ(J, A)
-        if A:
+        if self.kind(A):
             return (2 if J == 0 and A == 1 else 1) if o == 2 else (3 if J <= self.DS3 else (1 if J >= 22 else self.DS1A))
         if o >= 3:
             return 1
@@ -208,7 +216,7 @@ class P2dSchedule:
         return 1 if (J <= 12 or not self.EARLY) else 0
 
     def early(self, J, A=0):
-        if A:
+        if self.kind(A):
             return bool(self.EARLYA) and self.occ(J, A) == 1 and J < 22
         return bool(self.EARLY) and self.occ(J, A) == 1
 
@@ -216,7 +224,7 @@ class P2dSchedule:
         if J == 0 or self.jreg(J, A):
             return 0
         nsl = self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
-        csb = self.SR * self.SRB if A == 2 else (self.CSB if A else 0)
+        csb = self.SR * self.SRB if A == 2 else (self.CSB if self.kind(A) else 0)
         ocp2 = A == 2 and self.occ(J, A) == 2  # no EXT1 x-halo area, coefficients in registers
         lxb = 0 if (ocp2 or not self.EXT1) else 2 * self.TR * 2 * 16  # P2D_LXB
         off_j = nsl * self.SR * self.SRB + nsl * csb + 2 * self.LR * 1024 + lxb
@@ -228,11 +236,11 @@ class P2dSchedule:
 
     def jpf(self, J, A=0):
         """Register-row pass with plane k+1's rows loaded one step ahead (p2d_jpf)."""
-        return self.jreg(J, A) and A == 0 and J <= self.JPF
+        return self.jreg(J, A) and self.kind(A) == 0 and J <= self.JPF
 
     def rf(self, J, A=0):
         """J slot refilled with plane k + NP right after its rows are read (p2d_rf)."""
-        return bool(self.RF) and A == 0 and J > 0 and not self.jreg(J, A) and self.np(J, A) >= 2
+        return bool(self.RF) and self.kind(A) == 0 and J > 0 and not self.jreg(J, A) and self.np(J, A) >= 2
 
     def nsl(self, J, A=0):
         return self.ds(J, A) + 3 + (1 if self.early(J, A) else 0)
@@ -243,7 +251,7 @@ class P2dSchedule:
         return pre if pre > 0 else self.ds(J, A)
 
     def after(self, J, stw, i, A=0):
-        DS, NP, NSD = self.ds(J, A), self.np(J, A), {0: 4, 1: 6, 2: 8}[A]
+        DS, NP, NSD = self.ds(J, A), self.np(J, A), {0: 4, 1: 6, 2: 8}[self.kind(A)]
         early, late, jreg, rf = self.early(J, A), self.late(J, A), self.jreg(J, A), self.rf(J, A)
         n = lastS = lastJ = 0
         pre = self.dspre(J, A)
@@ -313,6 +321,7 @@ def check_p2d(funcs, meta, sched: P2dSchedule):
             continue
         J, hz, d2, pr, A = prm
         A = (2 if pr else 1) if A else 0  # the ring functions' anisotropic kind
+        K = 3 if (A == 0 and d2) else A   # ... and the kind the ring / wait rules take (KA)
         probs = []
         allv = vmem_counts(ins)
         bad = {k: v for k, v in allv.items() if k.startswith(("scratch_", "buffer_", "flat_"))}
@@ -330,7 +339,7 @@ def check_p2d(funcs, meta, sched: P2dSchedule):
         got = vmem_counts(loop)
         stw = 1 + hz
         loads = {k: v for k, v in got.items() if k != "global_store_dwordx4"}
-        jreg = sched.jreg(J, A)
+        jreg = sched.jreg(J, K)
         if loads != p2d_loop_loads(J, A, jreg):
             probs.append(f"march loop loads {loads} != the source's {p2d_loop_loads(J, A, jreg)}")
         if got.get("global_store_dwordx4", 0) not in (stw, 2 * stw):
@@ -338,8 +347,8 @@ def check_p2d(funcs, meta, sched: P2dSchedule):
         waits = sorted({int(re.search(r"vmcnt\((\d+)\)", o).group(1)) for _a, mn, o in loop
                         if mn == "s_waitcnt" and "vmcnt" in o})
         # jreg: the compiler adds its own counted waits for the J register loads
-        if (not set(sched.waits(J, stw, A)) <= set(waits)) if jreg else waits != sched.waits(J, stw, A):
-            probs.append(f"march loop vmcnt waits {waits} != p2d_after {sched.waits(J, stw, A)}")
+        if (not set(sched.waits(J, stw, K)) <= set(waits)) if jreg else waits != sched.waits(J, stw, K):
+            probs.append(f"march loop vmcnt waits {waits} != p2d_after {sched.waits(J, stw, K)}")
         rec = {"J": J, "HZ": hz, "D2": d2, "PR": pr, "A": A, "vgpr": md.get("vgpr_count"), "agpr": md.get("agpr_count"),
                "sgpr": md.get("sgpr_count"), "sgpr_spill": md.get("sgpr_spill_count"),
                "vgpr_spill": md.get("vgpr_spill_count"), "lds": md.get("group_segment_fixed_size"),
