@@ -1374,7 +1374,10 @@ void alloc_all(nls_handle *h) {
   const size_t na = std::max<size_t>(2 * (size_t)h->grid_alpha, h->fused_tail ? 3 * (size_t)h->grid_alpha2 : 0);
   hip_check(h, hipMalloc(&h->partA, na * sizeof(cplx)), "hipMalloc(partA)");
   hip_check(h, hipMalloc(&h->partU, (size_t)cap * sizeof(cplx)), "hipMalloc(partU)");
-  if (NLS_KG_CONCURRENT && h->kg && h->pass2 && !h->collective) {  // the second basis' own partials and stream
+  // (NLS_KG_CONCURRENT=0 in the environment: the serial order, for the bitwise check)
+  const char *kgc = std::getenv("NLS_KG_CONCURRENT");
+  if (NLS_KG_CONCURRENT && !(kgc && std::atoi(kgc) == 0) && h->kg && h->pass2 && !h->collective) {
+    // the second basis' own partials and stream
     hip_check(h, hipMalloc(&h->partAb, na * sizeof(cplx)), "hipMalloc(partA)");
     hip_check(h, hipMalloc(&h->partP2b, (size_t)h->p2grid * (3 * MMAX + 8) * sizeof(cplx)), "hipMalloc(partP2)");
     hip_check(h, hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking), "hipStreamCreate");

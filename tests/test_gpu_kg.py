@@ -205,6 +205,29 @@ def test_kg_pair_passes_match_oracle(monkeypatch, nx, ny, nz, m, kz):
     assert rel_l2(res["1"][0], res["0"][0]) <= TOL_TRAJ
 
 
+@pytest.mark.parametrize("nx,ny,nz,m", [(12, 12, 12, 10), (140, 8, 9, 10), (64, 16, 10, 16)])
+def test_kg_two_streams_bitwise_equal_serial(monkeypatch, nx, ny, nz, m):
+    """The two Krylov actions of the s-step KG step on two streams (nls_api.cpp: the sinc^2
+    basis on stream2 with its own partial buffers) against the serial order
+    (NLS_KG_CONCURRENT=0): the same kernels on the same inputs, bit for bit."""
+    L, dt, steps = 3.0, 5e-3, 6
+    dx = 2 * L / (nx - 1)
+    u0, v0, mf, c = kg_fields(3, nx, ny, nz, L, seed=6)
+    up0 = u0 - dt * v0
+    res = {}
+    for conc in ("1", "0"):
+        monkeypatch.setenv("NLS_KG_CONCURRENT", conc)
+        with kg_solver(3, nx, ny, nz, dx, m=m) as s:
+            s.set_coefficients(mf, c)
+            s.set_sg_state(u0, up0)
+            for _ in range(steps):
+                s.step(dt, 1)
+                s.apply_bc()
+            res[conc] = (s.get_field(), s.get_sg_velocity(dt))
+    for a, b in zip(res["1"], res["0"]):
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
 @pytest.mark.parametrize("n,nranks", [(16, 2), (16, 3)])
 def test_kg_pair_passes_slabs_match_single_rank(n, nranks):
     """The cell-pair passes on z-slabs (two ghost planes; in-process local transport)."""
