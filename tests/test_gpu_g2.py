@@ -386,7 +386,8 @@ def test_sewi_trajectory_matches_oracle(monkeypatch, form, dim, nx, ny, nz, m):
     assert rel_l2(out, ref) <= TOL_TRAJ
 
 
-@pytest.mark.parametrize("dim,nx,ny,nz,m", [(3, 12, 12, 12, 15), (3, 130, 8, 20, 15)])
+@pytest.mark.parametrize("dim,nx,ny,nz,m", [(3, 12, 12, 12, 15), (3, 130, 8, 20, 15), (3, 12, 8, 6, 3),
+                                            (3, 16, 12, 10, 4)])
 def test_sewi_concurrent_action_bitwise_equal_serial(monkeypatch, dim, nx, ny, nz, m):
     """The third Krylov action of an sEWI step (exp(2 tau L) u_prev) on a second basis and
     stream, concurrently with the first two (nls_api.cpp sewi_concurrent): the same kernels
@@ -407,6 +408,10 @@ def test_sewi_concurrent_action_bitwise_equal_serial(monkeypatch, dim, nx, ny, n
                 s.apply_bc()
             out[conc] = s.get_field()
     assert np.array_equal(out["1"].view(np.uint64), out["0"].view(np.uint64))
+    if m <= 4:  # the shortest bases (one / two s-step passes per action) against the oracle too
+        g = O.grid(dim, nx, ny, nz, dx, dx)
+        ref, _ = O.nlse_sewi_steps(g, c, mf, u, None, dt, 1, steps, m, bc=True)
+        assert rel_l2(out["1"], ref) <= TOL_TRAJ
 
 
 def test_sewi_golden_and_errors():
