@@ -60,3 +60,20 @@ def test_checker_flags_an_extra_vmem_op():
     extra = ins[:-1] + [(0x18e, "scratch_load_dword", "v1, off"), ins[-1]]
     probs = C.check_p2d({name: extra}, md, sched)[0][1]
     assert probs and any("scratch" in p for p in probs)
+
+
+def test_register_row_kinds():
+    """Kind 3 (the isotropic 2D passes) follows kind 0's ring rules except where its
+    register rows start: 3D from J = 2, 2D from J = 8 (nls_pass2d.hpp p2d_kind / p2d_jreg);
+    the code-object check above reads the instantiations through the same rules."""
+    s = C.P2dSchedule(HDR)
+    assert [J for J in range(0, 15, 2) if s.jreg(J, 0)] == [J for J in range(s.JREG_MINJ, s.JREG_MAXJ + 1, 2)]
+    assert [J for J in range(0, 15, 2) if s.jreg(J, 3)] == [J for J in range(s.JREG2D_MINJ, s.JREG_MAXJ + 1, 2)]
+    assert s.JREG2D_MINJ > s.JREG_MINJ
+    for J in range(0, 15, 2):
+        if s.jreg(J, 0) == s.jreg(J, 3):  # same storage form: identical schedule
+            assert (s.occ(J, 0), s.ds(J, 0), s.np(J, 0), s.early(J, 0)) == (s.occ(J, 3), s.ds(J, 3), s.np(J, 3),
+                                                                         s.early(J, 3))
+            assert s.waits(J, 2, 0) == s.waits(J, 2, 3)
+        else:  # 3D register rows, 2D J ring
+            assert s.np(J, 0) == 0 and s.np(J, 3) >= 1
