@@ -498,6 +498,7 @@ def main():
     s = nls_amd.Solver(dim, n, n, n if dim == 3 else 1, dx, dx, equation=w["eq"], m=m,
                        device=local_rank, nranks=world, rank=rank, rccl_id=rid)
     comm_ranks, comm_transport = s.comm_size()  # what the library's transport reports
+    placement = s.placement()  # basis placement probed at creation (nls_placement)
     u = synthetic_ic(w, s.z0, s.nzl)
     if w["eq"] == 2:
         s.set_sg_state(u, u.copy(), -np.ones(u.size))
@@ -663,6 +664,9 @@ def main():
             if pass2 else "one-vector passes + fused tail",
             "bases_per_step": 2 if w["eq"] in (2, 4) else (3 if w.get("sewi") else 1),
         },
+        # the basis allocation kept among the candidates probed at nls_create (DESIGN.md
+        # section 4 "Placement"; candidates 0: no probe on this handle)
+        "placement": placement,
     }
     s.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define NLS_ABI_VERSION 5
+#define NLS_ABI_VERSION 6
 #define NLS_MAX_KRYLOV 32
 
 enum nls_status {
@@ -284,6 +284,18 @@ enum nls_knob {
   NLS_KNOB_P2_ORDER = 3   /* k_p2d tile order bits */
 };
 int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value);
+
+/* Basis placement chosen at nls_create.  The streams of one pass run 2-4 % faster or
+ * slower depending on which HBM pages back the Krylov basis (DESIGN.md section 4,
+ * "Placement"), which no allocation call controls: large single-rank handles allocate
+ * up to NLS_PLACE candidate bases (default 6, where free memory allows), time the
+ * same probe step sequence on each, keep the fastest and free the rest; the chosen
+ * basis is then zeroed, so results do not depend on the choice.  *n = candidates
+ * probed (0: no probe on this handle), *chosen = index kept, ms[0..min(n,cap)) =
+ * each candidate's probe time (ms).  No reference counterpart (the reference has one
+ * cudaMalloc per buffer, device/nlse_solver_dev.hpp:58-93). */
+#define NLS_PLACE_MAX 8
+int nls_placement(const nls_handle *h, int32_t *n, int32_t *chosen, float *ms, uint32_t cap);
 
 #ifdef __cplusplus
 }

@@ -146,6 +146,10 @@ struct nls_handle {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   cplx *partP2b = nullptr, *partAb = nullptr;
   void *prepad = nullptr;  // NLS_DEBUG_PREPAD_KB: a dummy allocation ahead of the bases (placement probe)
+  // basis placement (place_basis, DESIGN.md section 4 "Placement"): candidate allocations
+  // probed at nls_create, the fastest kept; place_ms[i] = probe time of candidate i
+  int place_n = 0, place_pick = -1;
+  float place_ms[NLS_PLACE_MAX] = {};
   bool sewi_serial = false;  // the second sEWI basis could not be allocated
   int p2order = 0;             // k_p2d tile order (Geo::remap bits: 2 x-fastest, 4 no XCD bands; debug knob 3)
   bool p2_warm[2] = {false, false};  // the basis' P2State holds a previous alpha_0
@@ -1088,6 +1092,7 @@ void setup_geometry(nls_handle *h) {
   // -> 24.15-24.27 ms per step on two boxes (2048: +0.1; 4160: +0.3; 16384: +0.0), 4096^2
   // and G2 256^3 within 1 % (profiles/r04/ab_vpad.txt)
   h->vpad = NLS_VPAD;
+  if (const char *e = std::getenv("NLS_DEBUG_VPAD")) h->vpad = std::max<int64_t>(0, std::atoll(e));  // (A/B sweeps)
   // (the vector stride h->vs follows in alloc_all, once the ghost depth is known)
 }
 
@@ -1295,9 +1300,14 @@ void alloc_all(nls_handle *h) {
   if (const char *e = std::getenv("NLS_DEBUG_PREPAD_KB"))
     if (const size_t kb = std::strtoull(e, nullptr, 10))
       hip_check(h, hipMalloc(&h->prepad, kb * 1024), "hipMalloc(prepad)");
+  // (NLS_DEBUG_CONTIG=1: physically contiguous bases, for the placement A/B)
+  const bool contig = std::getenv("NLS_DEBUG_CONTIG") && std::atoi(std::getenv("NLS_DEBUG_CONTIG"));
   for (int b = 0; b < h->nbasis; ++b) {
     const size_t bytes = (size_t)h->nvec[b] * h->vs * h->esize;
-    hip_check(h, hipMalloc(&h->B[b].W, bytes), "hipMalloc(basis)");
+    if (contig)
+      hip_check(h, hipExtMallocWithFlags(&h->B[b].W, bytes, hipDeviceMallocContiguous), "hipExtMallocWithFlags(basis)");
+    else
+      hip_check(h, hipMalloc(&h->B[b].W, bytes), "hipMalloc(basis)");
     hip_check(h, hipMemsetAsync(h->B[b].W, 0, bytes, h->stream), "hipMemset");
     hip_check(h, hipMalloc(&h->B[b].st, sizeof(KState)), "hipMalloc(state)");
     hip_check(h, hipMemsetAsync(h->B[b].st, 0, sizeof(KState), h->stream), "hipMemset");
@@ -1461,6 +1471,8 @@ void nls_config_default(nls_config *c) {
   c->rccl_id = nullptr;
 }
 
+void place_basis(nls_handle *h);
+
 int nls_create(const nls_config *cfg, nls_handle **out) {
   if (!out) return NLS_ERR_ARG;
   *out = nullptr;
@@ -1558,6 +1570,7 @@ int nls_create(const nls_config *cfg, nls_handle **out) {
     }
     alloc_all(h);  // the update launch plan depends on h->collective
     hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    place_basis(h);
   });
   if (rc != NLS_OK) {
     g_create_error = h->err;
@@ -1813,6 +1826,104 @@ void ss2_step(nls_handle *h, double dt) {
   halo(h, 0, 0);
   h->w0_ready = true;
   h->w0_dt = dt;
+}
+
+// Basis placement (nls_placement; DESIGN.md section 4 "Placement").  The same kernels on
+// the same handle run 2-4 % faster or slower in different processes according to which
+// HBM pages back the basis (profiles/r05/envab_prepad.txt: a 4 GB dummy allocation ahead
+// of the basis selected the fast passes in every process); no allocation call chooses
+// pages.  So the handle chooses among allocations: up to NLS_PLACE candidate bases
+// (default 6; those that fit in free memory beside an 8 GB reserve) are allocated while
+// the earlier ones are held, each runs the same probe -- one cold SS2 step, then
+// PLACE_STEPS timed steps of the real launch sequence on a constant field -- and the
+// fastest is kept.  512^3 m = 16 (profiles/r06/envab_place.txt): 30.40-31.52 ms per step
+// with one allocation, 29.98-30.44 with the probe.
+// Everything the probe wrote is reset to the state alloc_all left (bases, Lanczos state,
+// tile-queue counters zero; no live start vector), so no result depends on the choice.
+// Large single-rank complex handles with the s-step passes (the 512^3 class); others
+// keep their one allocation.
+constexpr int PLACE_STEPS = 3;  // timed probe steps per candidate
+void place_basis(nls_handle *h) {
+  int K = 6;
+  if (const char *e = std::getenv("NLS_PLACE")) K = std::atoi(e);
+  K = std::min(K, NLS_PLACE_MAX);
+  const bool contig = std::getenv("NLS_DEBUG_CONTIG") && std::atoi(std::getenv("NLS_DEBUG_CONTIG"));
+  if (K <= 1 || contig || h->collective || !h->cplx_ || !h->pass2 || h->p2reg || h->ani || !h->large ||
+      h->nbasis != 1 || h->cfg.dim != 3 || h->prepad)
+    return;
+  const size_t bytes = (size_t)h->nvec[0] * h->vs * h->esize;
+  size_t fr = 0, tot = 0;
+  hip_check(h, hipMemGetInfo(&fr, &tot), "hipMemGetInfo");
+  const size_t reserve = size_t(8) << 30;
+  const int fit = fr > reserve ? (int)((fr - reserve) / bytes) : 0;
+  K = std::min(K, 1 + fit);
+  if (K <= 1) return;
+  std::vector<void *> cand{h->B[0].W};
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  auto reset = [&] {
+    // the state alloc_all leaves: zero basis (out-of-grid ghost planes included), zero
+    // Lanczos state, zero tile-queue counters, no live start vector
+    hip_check(h, hipMemsetAsync(h->B[0].W, 0, bytes, h->stream), "hipMemset");
+    hip_check(h, hipMemsetAsync(h->B[0].st, 0, sizeof(KState), h->stream), "hipMemset");
+    hip_check(h, hipMemsetAsync(h->p2, 0, p2state_bytes() * h->nbasis, h->stream), "hipMemset");
+    p2_cold(h);
+    h->w0_ready = false;
+  };
+  try {
+    hip_check(h, hipEventCreate(&e0), "hipEventCreate");
+    hip_check(h, hipEventCreate(&e1), "hipEventCreate");
+    const size_t nb = (size_t)h->geo.nloc * h->esize;
+    const double dt = 1e-3;
+    for (int c = 0; c < K; ++c) {
+      if (c > 0) {
+        void *w = nullptr;
+        if (hipMalloc(&w, bytes) != hipSuccess) {
+          (void)hipGetLastError();
+          break;
+        }
+        cand.push_back(w);
+      }
+      h->B[0].W = cand[c];
+      reset();
+      // a constant field (0x3FF00000 words: each value ~ 1 + 2^-20 in both parts); its
+      // Krylov space grows from the boundary layer, no breakdown within m vectors
+      hip_check(h, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->u), 0x3FF00000, nb / 4, h->stream),
+                "hipMemsetD32");
+      ss2_step(h, dt);  // cold: the alpha_0 pass; later steps start blind, as a run does
+      hip_check(h, hipEventRecord(e0, h->stream), "hipEventRecord");
+      for (int s = 0; s < PLACE_STEPS; ++s) ss2_step(h, dt);
+      hip_check(h, hipEventRecord(e1, h->stream), "hipEventRecord");
+      hip_check(h, hipEventSynchronize(e1), "hipEventSynchronize");
+      float ms = 0.f;
+      hip_check(h, hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+      h->place_ms[c] = ms;
+    }
+  } catch (...) {
+    h->B[0].W = cand[0];
+    for (size_t c = 1; c < cand.size(); ++c) (void)hipFree(cand[c]);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    throw;
+  }
+  h->place_n = (int)cand.size();
+  int best = 0;
+  for (int c = 1; c < h->place_n; ++c)
+    if (h->place_ms[c] < h->place_ms[best]) best = c;
+  h->place_pick = best;
+  hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  for (int c = 0; c < h->place_n; ++c)
+    if (c != best) (void)hipFree(cand[c]);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  h->B[0].W = cand[best];
+  reset();
+  hip_check(h, hipMemsetAsync(h->u, 0, (size_t)h->geo.nloc * h->esize, h->stream), "hipMemset");
+  hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  if (std::getenv("NLS_PLACE_LOG")) {
+    std::fprintf(stderr, "[nls] placement: %d candidates, kept %d; probe ms", h->place_n, best);
+    for (int c = 0; c < h->place_n; ++c) std::fprintf(stderr, " %.3f", h->place_ms[c]);
+    std::fprintf(stderr, "\n");
+  }
 }
 
 // Work issued inside the scope goes to the handle's second stream with the second set
@@ -2381,6 +2492,15 @@ int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value) {
       default: fail(h, NLS_ERR_ARG, "nls_debug_knob: unknown knob");
     }
   });
+}
+
+int nls_placement(const nls_handle *h, int32_t *n, int32_t *chosen, float *ms, uint32_t cap) {
+  if (!h || !n) return NLS_ERR_ARG;
+  *n = h->place_n;
+  if (chosen) *chosen = h->place_pick;
+  if (ms)
+    for (int c = 0; c < h->place_n && (uint32_t)c < cap; ++c) ms[c] = h->place_ms[c];
+  return NLS_OK;
 }
 
 int nls_reset_timing(nls_handle *h) {

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert sorted(nls_amd.EXPORTED_SYMBOLS) == syms
-    assert L.nls_abi_version() == 5
+    assert L.nls_abi_version() == 6
     out = subprocess.run(["nm", "-D", "--defined-only", nls_amd.lib_path()], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (nls_\w+)", out))
     assert set(syms) <= exported

@@ -138,11 +138,12 @@ print(f\"$v rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} domina
       sets=${arg#*:}
       for rep in $(seq 1 "${ENVAB_REPS:-2}"); do
         for ev in $(echo "$sets" | tr ',' ' '); do
-          [ "$ev" != "-" ] && export "${ev?}"
+          # a setting is one VAR=VALUE or several joined by '+'
+          [ "$ev" != "-" ] && for kv in $(echo "$ev" | tr '+' ' '); do export "${kv?}"; done
           run 300 "$OUT/envab_cur.json" python bench.py --workload "$wl" --steps 10 --warmup 2 --no-cpu-baseline
-          [ "$ev" != "-" ] && unset "${ev%%=*}"
+          [ "$ev" != "-" ] && for kv in $(echo "$ev" | tr '+' ' '); do unset "${kv%%=*}"; done
           python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['step_roofline']['gpu_kernel_ms_per_step']; \
-print(f\"$ev rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} \" + ' '.join(f'{a}:{b:.3f}' for a, b in k.items()))" \
+print(f\"$ev rep$rep ms/step {d['ms_per_step']:.3f} value {d['value']:.1f} \" + ' '.join(f'{a}:{b:.3f}' for a, b in k.items()) + ' place:' + str(d.get('placement')))" \
             "$OUT/envab_cur.json" | tee -a "$OUT/envab_$wl.txt"
         done
       done ;;
