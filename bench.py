@@ -447,6 +447,197 @@ def launch_ranks(n: int, argv):
     return p.returncode, line
 
 
+# ---- N > 1: the run validates its own multi-GPU path before timing ----
+#
+# Rank 0 starts, before any rank touches a GPU, a child job on the same N GPUs (the same
+# launcher line, its own rendezvous port) that
+#   * checks the N-rank field against a 1-rank run on rank 0's GPU (64^3 cubic NLSE, m = 16,
+#     SELFCHECK_STEPS SS2 steps; rel-L2 <= SELFCHECK_TOL) and that the library's
+#     communicator counts N ranks (ncclCommCount, nls_comm_size), once over the default
+#     exchange (RCCL send/recv + all-reduce) and once with NLS_PEER=1 (IPC handshake,
+#     peer stores, their ordering by the pass all-reduces and the W_0 halo);
+#   * times both exchange paths on the bench workload (SELFCHECK_AB_STEPS steps each,
+#     after a warm-up, max over ranks).
+# The parent ranks then run the timed region on the exchange the child validated and
+# measured faster (the default unless the peer path passed its check AND was faster); the
+# child's report goes into the JSON line.  A child that faults, hangs (SELFCHECK_TIMEOUT)
+# or fails a check leaves the default exchange in place and says so in the line.
+SELFCHECK_N, SELFCHECK_M, SELFCHECK_STEPS, SELFCHECK_TOL = 64, 16, 5, 1e-12
+SELFCHECK_AB_STEPS, SELFCHECK_TIMEOUT = 5, 420
+_LAUNCHER_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                 "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def selfcheck_env(env):
+    """The child job's environment: the parent's, without the launcher's per-rank
+    variables (the child's own torch.distributed.run sets them) and without NLS_PEER."""
+    out = {k: v for k, v in env.items()
+           if k not in _LAUNCHER_ENV and not k.startswith("TORCHELASTIC_") and k != "NLS_PEER"}
+    out.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return out
+
+
+def selfcheck_cmd(n, args, json_path, port):
+    argv = ["--gpus", str(n), "--workload", args.workload, "--selfcheck-json", json_path]
+    if args.n:
+        argv += ["--n", str(args.n)]
+    if args.m:
+        argv += ["--m", str(args.m)]
+    return rank_launch_cmd(n, argv, port)
+
+
+def run_selfcheck(n, args):
+    """Rank 0 of the parent job: run the child job, return its report (or the failure)."""
+    import subprocess
+    import tempfile
+    t0 = time.perf_counter()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "selfcheck.json")
+        try:
+            p = subprocess.run(selfcheck_cmd(n, args, path, free_port()), env=selfcheck_env(os.environ),
+                               stdout=sys.stderr, stderr=sys.stderr, timeout=SELFCHECK_TIMEOUT)
+            rc = p.returncode
+        except subprocess.TimeoutExpired:
+            rc = "timeout"
+        rep = None
+        if os.path.exists(path):
+            with open(path) as f:
+                rep = json.load(f)
+    if rep is None:
+        rep = {"default": {"ok": False}, "peer": {"ok": False}, "error": f"self-check job ended with {rc}"}
+    rep["child_rc"] = rc
+    rep["seconds"] = time.perf_counter() - t0
+    return rep
+
+
+def choose_exchange(rep):
+    """The exchange the timed run uses: the peer stores only when they passed the field
+    check, actually ran (not the library's fallback) and were faster in the A/B leg."""
+    ab = rep.get("ab") or {}
+    peer_ok = bool(rep.get("peer", {}).get("ok")) and rep.get("peer", {}).get("state") == "active"
+    if peer_ok and ab.get("peer_ms") and ab.get("default_ms") and ab["peer_ms"] < ab["default_ms"]:
+        return "peer"
+    return "default"
+
+
+def gather_slabs(local, dist, world, rank):
+    """Rank 0: the ranks' slabs concatenated in rank order (None elsewhere)."""
+    parts = [None] * world
+    dist.all_gather_object(parts, np.ascontiguousarray(local))
+    return np.concatenate(parts) if rank == 0 else None
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def _bcast(obj, dist, rank):
+    o = [obj if rank == 0 else None]
+    dist.broadcast_object_list(o, src=0)
+    return o[0]
+
+
+def _selfcheck_field(nls_amd, dist, world, rank, local_rank, peer):
+    """One leg of the field check (see above); the report (rank 0's, broadcast)."""
+    n, m, dt = SELFCHECK_N, SELFCHECK_M, 1e-3
+    w = dict(WORKLOADS["nlse3d_512"], n=n)
+    dx = 2 * w["L"] / (n - 1)
+    os.environ.pop("NLS_PEER", None)
+    if peer:
+        os.environ["NLS_PEER"] = "1"
+    rep = {"grid": [n] * 3, "krylov_m": m, "steps": SELFCHECK_STEPS, "tol": SELFCHECK_TOL}
+    try:
+        rid = _bcast(nls_amd.rccl_unique_id() if rank == 0 else None, dist, rank)
+        s = nls_amd.Solver(3, n, n, n, dx, dx, m=m, device=local_rank, nranks=world, rank=rank, rccl_id=rid)
+        cnt, tr = s.comm_size()
+        u = synthetic_ic(w, s.z0, s.nzl)
+        s.set_field(u)
+        s.step(dt, SELFCHECK_STEPS)
+        f = s.get_field()
+        state = s.peer_state()
+        s.close()
+    finally:
+        os.environ.pop("NLS_PEER", None)
+    full = gather_slabs(f, dist, world, rank)
+    counts = [None] * world
+    dist.all_gather_object(counts, (cnt, tr, state))
+    if rank == 0:
+        with nls_amd.Solver(3, n, n, n, dx, dx, m=m, device=local_rank) as s1:
+            s1.set_field(synthetic_ic(w, 0, n))
+            s1.step(dt, SELFCHECK_STEPS)
+            ref = s1.get_field()
+        err = rel_l2(full, ref)
+        rep.update(comm_count=[c[0] for c in counts], transport=counts[0][1], state=counts[0][2],
+                   states=[c[2] for c in counts], rel_l2_vs_1rank=err,
+                   ok=bool(all(c[0] == world for c in counts) and err <= SELFCHECK_TOL))
+    return _bcast(rep, dist, rank)
+
+
+def _selfcheck_ab(nls_amd, dist, world, rank, local_rank, w, peer):
+    """ms per step of the bench workload over one exchange path (max over ranks)."""
+    n = w["n"]
+    dx = 2 * w["L"] / (n - 1)
+    os.environ.pop("NLS_PEER", None)
+    if peer:
+        os.environ["NLS_PEER"] = "1"
+    try:
+        rid = _bcast(nls_amd.rccl_unique_id() if rank == 0 else None, dist, rank)
+        s = nls_amd.Solver(w["dim"], n, n, n if w["dim"] == 3 else 1, dx, dx, equation=w["eq"], m=w["m"],
+                           device=local_rank, nranks=world, rank=rank, rccl_id=rid)
+        s.set_field(synthetic_ic(w, s.z0, s.nzl))
+        s.step(w["dt"], 2)
+        s.sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        s.step(w["dt"], SELFCHECK_AB_STEPS)
+        s.sync()
+        el = time.perf_counter() - t0
+        state = s.peer_state()
+        s.close()
+    finally:
+        os.environ.pop("NLS_PEER", None)
+    return max_over_ranks(el, dist) * 1e3 / SELFCHECK_AB_STEPS, state
+
+
+def selfcheck_main(args, dist, world, rank, local_rank):
+    """The child job (--selfcheck-json): both field checks, the A/B leg, the report."""
+    import nls_amd
+    rep = {"n_ranks": world}
+    if os.environ.get("NLS_BENCH_SELFCHECK_DRY"):
+        # launcher-path test on CPU (tests/test_dist_cpu.py): the same gather / compare and
+        # report plumbing on a synthetic field, no device
+        w = dict(WORKLOADS["nlse3d_512"], n=20)
+        z0, nzl = nls_amd.slab_planes(20, world, rank)
+        full = gather_slabs(synthetic_ic(w, z0, nzl), dist, world, rank)
+        for leg in ("default", "peer"):
+            r = {"comm_count": [world] * world, "state": "active" if leg == "peer" else "off"}
+            if rank == 0:
+                r["rel_l2_vs_1rank"] = rel_l2(full, synthetic_ic(w, 0, 20))
+                r["ok"] = r["rel_l2_vs_1rank"] <= SELFCHECK_TOL
+            rep[leg] = _bcast(r, dist, rank)
+        rep["ab"] = {"default_ms": 2.0, "peer_ms": 1.0, "peer_state": "active"}
+    else:
+        rep["default"] = _selfcheck_field(nls_amd, dist, world, rank, local_rank, False)
+        try:
+            rep["peer"] = _selfcheck_field(nls_amd, dist, world, rank, local_rank, True)
+        except Exception as e:  # noqa: BLE001  (a failed peer leg leaves the default)
+            rep["peer"] = {"ok": False, "error": repr(e)}
+        w = dict(WORKLOADS[args.workload])
+        if args.n:
+            w["n"] = args.n
+        if args.m:
+            w["m"] = args.m
+        ab = {"steps": SELFCHECK_AB_STEPS}
+        ab["default_ms"], _ = _selfcheck_ab(nls_amd, dist, world, rank, local_rank, w, False)
+        if rep["peer"].get("ok"):
+            ab["peer_ms"], ab["peer_state"] = _selfcheck_ab(nls_amd, dist, world, rank, local_rank, w, True)
+        rep["ab"] = ab
+    if rank == 0:
+        with open(args.selfcheck_json, "w") as f:
+            json.dump(rep, f)
+    dist.barrier()
+
+
 def main():
     out = _claim_stdout()
     ap = argparse.ArgumentParser()
@@ -462,6 +653,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full-grid-cpu", action="store_true",
                     help="skip the one-step CPU oracle run at the full 512^3 grid")
+    ap.add_argument("--no-selfcheck", action="store_true",
+                    help="N > 1: skip the multi-GPU self-check job (default exchange)")
+    ap.add_argument("--selfcheck-json", default=None, help=argparse.SUPPRESS)  # the child job
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -480,6 +674,17 @@ def main():
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("gloo")
+    if args.selfcheck_json:
+        selfcheck_main(args, dist, world, rank, local_rank)
+        dist.destroy_process_group()
+        return
+    check = None
+    if world > 1 and not args.no_selfcheck:
+        # before any rank touches a GPU: the child job on the same N GPUs (see run_selfcheck)
+        check = _bcast(run_selfcheck(world, args) if rank == 0 else None, dist, rank)
+        check["exchange"] = choose_exchange(check)
+        if check["exchange"] == "peer":
+            os.environ["NLS_PEER"] = "1"
 
     import nls_amd
 
@@ -498,6 +703,8 @@ def main():
     s = nls_amd.Solver(dim, n, n, n if dim == 3 else 1, dx, dx, equation=w["eq"], m=m,
                        device=local_rank, nranks=world, rank=rank, rccl_id=rid)
     comm_ranks, comm_transport = s.comm_size()  # what the library's transport reports
+    if comm_ranks != world:
+        raise SystemExit(f"library communicator has {comm_ranks} ranks, WORLD_SIZE={world}")
     placement = s.placement()  # basis placement probed at creation (nls_placement)
     u = synthetic_ic(w, s.z0, s.nzl)
     if w["eq"] == 2:
@@ -668,6 +875,11 @@ def main():
         # section 4 "Placement"; candidates 0: no probe on this handle)
         "placement": placement,
     }
+    if world > 1:
+        # the self-check job's report and the exchange this timed run used (peer_state of
+        # this handle: "active" = peer stores, "off" = RCCL send/recv exchange)
+        result["multi_gpu_check"] = check
+        result["config"]["exchange"] = {"used": s.peer_state(), "chosen": (check or {}).get("exchange", "default")}
     s.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, u_full)

@@ -294,6 +294,21 @@ int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value);
  * probed (0: no probe on this handle), *chosen = index kept, ms[0..min(n,cap)) =
  * each candidate's probe time (ms).  No reference counterpart (the reference has one
  * cudaMalloc per buffer, device/nlse_solver_dev.hpp:58-93). */
+/* The boundary-plane transport of a collective handle.  NLS_PEER=1 at
+ * nls_create asks for peer stores (k_p2d writes the neighbours' ghost planes through
+ * IPC-mapped allocations) instead of the RCCL send/recv exchange; the mappings are made
+ * at the first step, and if any rank cannot open one, every rank falls back to the
+ * exchange (agreed by an all-reduce, so the ranks' transport sequences stay identical).
+ * No reference counterpart (the reference runs independent single-GPU solvers,
+ * device/nlse_driver_omp.cpp:103-121). */
+enum nls_peer_state_e {
+  NLS_PEER_OFF = 0,        /* exchange path (not asked for, or not available on this handle) */
+  NLS_PEER_ACTIVE = 1,     /* peer stores in use */
+  NLS_PEER_FELL_BACK = 2,  /* asked for; an IPC open failed on some rank: exchange path */
+  NLS_PEER_PENDING = 3     /* asked for; set up at the first step */
+};
+int nls_peer_state(const nls_handle *h, int32_t *state);
+
 #define NLS_PLACE_MAX 8
 int nls_placement(const nls_handle *h, int32_t *n, int32_t *chosen, float *ms, uint32_t cap);
 

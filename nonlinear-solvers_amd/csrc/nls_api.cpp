@@ -201,6 +201,7 @@ struct nls_handle {
   // (side 0) / above (side 1), nullptr where there is none; a 1-rank handle points both
   // at itself (its out-of-grid ghost planes: a cost probe that changes no result)
   bool peer = false, peer_ready = false, peer_ipc = false;
+  bool peer_fallback = false;  // NLS_PEER=1 asked, an IPC open failed on some rank: exchange path
   char *peer_W[2][2] = {};
   int64_t peer_vs[2] = {}, peer_nzl[2] = {};
   // debug (NLS_OPLOG=1 at nls_create): the transport operations in issue order, with
@@ -450,6 +451,7 @@ struct PeerMsg {
   hipIpcMemHandle_t hd[2];
   int64_t vs, nzl;
 };
+void peer_close(nls_handle *h);
 void peer_setup(nls_handle *h) {
   if (h->peer_ready) return;
   if (h->nranks == 1) {
@@ -487,18 +489,46 @@ void peer_setup(nls_handle *h) {
       (void)hipFree(d);
       throw;
     }
-    (void)hipFree(d);
     h->peer_ipc = true;
-    for (int side = 0; side < 2; ++side) {
+    // An open can fail (a neighbour in the same process: HIP refuses a handle exported by
+    // the importing process; no peer path between the devices).  Every rank must then
+    // leave the peer path together -- the ranks' transport sequences must stay identical
+    // -- so the outcome is agreed by an all-reduce (min) of the ranks' success flags
+    // before any pass uses a mapping.
+    int32_t ok = 1;
+    for (int side = 0; side < 2 && ok; ++side) {
       const int nb = h->rank + (side ? 1 : -1);
       if (nb < 0 || nb >= h->nranks) continue;
-      for (int b = 0; b < h->nbasis; ++b) {
+      for (int b = 0; b < h->nbasis && ok; ++b) {
         void *p = nullptr;
-        hip_check(h, hipIpcOpenMemHandle(&p, all[nb].hd[b], hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+        if (hipIpcOpenMemHandle(&p, all[nb].hd[b], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+          (void)hipGetLastError();
+          ok = 0;
+          break;
+        }
         h->peer_W[side][b] = static_cast<char *>(p);
       }
       h->peer_vs[side] = all[nb].vs;
       h->peer_nzl[side] = all[nb].nzl;
+    }
+    int32_t *dok = reinterpret_cast<int32_t *>(d);
+    try {
+      hip_check(h, hipMemcpyAsync(dok, &ok, sizeof(ok), hipMemcpyHostToDevice, h->stream), "H2D");
+      oplog(h, NLS_OP_ALLREDUCE, 0, 0, -1);
+      rccl_check(h, ncclAllReduce(dok, dok, 1, ncclInt32, ncclMin, h->comm, h->stream), "ncclAllReduce(peer ok)");
+      hip_check(h, hipMemcpyAsync(&ok, dok, sizeof(ok), hipMemcpyDeviceToHost, h->stream), "D2H");
+      hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    } catch (...) {
+      (void)hipFree(d);
+      throw;
+    }
+    (void)hipFree(d);
+    if (!ok) {
+      // back to the exchange path on every rank (partP2 is sized for both launch plans)
+      peer_close(h);
+      h->peer = false;
+      h->peer_fallback = true;
+      return;
     }
   }
   h->peer_ready = true;
@@ -518,6 +548,7 @@ void peer_close(nls_handle *h) {
 void peer_tables(nls_handle *h) {
   if (h->peer_ready) return;
   peer_setup(h);
+  if (!h->peer) return;  // the ranks fell back to the exchange path (peer_setup)
   const int64_t P = h->geo.P, es = (int64_t)h->esize;
   const int NK = p2state_peer_slots();
   for (int b = 0; b < h->nbasis; ++b) {
@@ -1227,6 +1258,11 @@ void alloc_all(nls_handle *h) {
     h->p2order = dim == 3 ? 6 : 0;
     h->p2grid = 0;
     for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
+    if (h->peer) {  // room for the exchange path's launch plan too (peer_setup's fallback)
+      h->peer = false;
+      for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, p2_grid(h, J));
+      h->peer = true;
+    }
     if (h->p2reg)
       for (int J = 0; J < MMAX; J += 2) h->p2grid = std::max(h->p2grid, h->p2mgrid[J]);
     hip_check(h, hipMalloc(&h->p2, p2state_bytes() * h->nbasis), "hipMalloc(p2)");  // one per basis
@@ -2492,6 +2528,13 @@ int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value) {
       default: fail(h, NLS_ERR_ARG, "nls_debug_knob: unknown knob");
     }
   });
+}
+
+int nls_peer_state(const nls_handle *h, int32_t *state) {
+  if (!h || !state) return NLS_ERR_ARG;
+  *state = h->peer_fallback ? NLS_PEER_FELL_BACK : !h->peer ? NLS_PEER_OFF
+           : h->peer_ready  ? NLS_PEER_ACTIVE : NLS_PEER_PENDING;
+  return NLS_OK;
 }
 
 int nls_placement(const nls_handle *h, int32_t *n, int32_t *chosen, float *ms, uint32_t cap) {

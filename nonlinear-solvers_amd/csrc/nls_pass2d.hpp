@@ -999,8 +999,15 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : (D2 ? 3 : 0
   // ghost planes (ps->pdn), of planes nzl-2, nzl-1 into the neighbour above's lower
   // ones (ps->pup): no exchange step and no boundary/interior split.  Read back from
   // this wave's own stores (complete after the wait above), after the march loop, so
-  // the loop and its hand-counted vmcnt are untouched; the pass's all-reduce, which
-  // every rank joins after its pass, orders the stores before the neighbour's next pass.
+  // the loop and its hand-counted vmcnt are untouched.  Ordering: inside a
+  // step, the pass's all-reduce, which every rank joins after its pass, orders the stores
+  // before the neighbour's next pass reads them.  The blind J = 0 pass that opens a step
+  // has no all-reduce before it in that step: its stores into the neighbour's ghost planes
+  // (with m = 3, 4 those of S_{m-2}, which the neighbour's previous tail reads) are ordered
+  // after that tail by the per-step W_0 halo exchange (ss2_step's halo(h, 0, 0) after the
+  // tail: the neighbour's send follows its tail, our J = 0 pass follows our receive).
+  // tests/test_gpu_multirank.py checks m = 3, 4 over several steps bit for bit against
+  // the exchange path.
   // (a separate instantiation: the epilogue's live values cost the plain pass's march
   // loop ~20 instructions per step at J = 12)
   if (PEER && (k0 < 2 || k1 > nzl - 2)) {  // uniform: a tile holding a boundary plane

@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
     "nls_get_field_async", "nls_wait_field", "nls_host_alloc", "nls_host_free", "nls_slab_planes",
     "nls_step_sewi", "nls_debug_oplog", "nls_debug_knob", "nls_placement",
+    "nls_peer_state",
 )
 # nls_debug_oplog entry kinds (include/nls.h enum nls_op_kind)
 OP_ALLREDUCE, OP_SEND, OP_RECV, OP_WAIT_HALO, OP_WAIT_COMPUTE, OP_ALLGATHER, OP_DROPPED = 1, 2, 3, 4, 5, 6, 7
@@ -125,6 +126,7 @@ def lib():
     L.nls_reset_timing.argtypes = [H]
     L.nls_debug_oplog.argtypes = [H, C.POINTER(C.c_int32), C.c_uint64, C.POINTER(C.c_uint64)]
     L.nls_debug_knob.argtypes = [H, C.c_int32, C.c_int32]
+    L.nls_peer_state.argtypes = [H, C.POINTER(C.c_int32)]
     L.nls_placement.argtypes = [H, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_float),
                                 C.c_uint32]
     if L.nls_abi_version() != 6:
@@ -350,6 +352,12 @@ class Solver:
         """Launch-shape knob of this live handle (nls_debug_knob: 1 tail dynamic tile
         queue, 2 tail tile depth, 3 k_p2d tile order), for same-allocation A/B runs."""
         self._call(lib().nls_debug_knob, int(knob), int(value))
+
+    def peer_state(self) -> str:
+        """The boundary-plane transport (nls_peer_state): off / active / fell_back / pending."""
+        v = C.c_int32()
+        self._call(lib().nls_peer_state, C.byref(v))
+        return ("off", "active", "fell_back", "pending")[v.value]
 
     def placement(self) -> dict:
         """The basis placement chosen at creation (nls_placement): candidates probed,

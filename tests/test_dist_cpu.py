@@ -145,3 +145,62 @@ def test_bench_launcher_forwards_rank0_line(tmp_path, monkeypatch):
     rc, line = bench.launch_ranks(2, [])
     assert rc == 0
     assert json.loads(line) == {"metric": "x", "value": 1.0, "n_gpus": 2}
+
+
+def test_bench_selfcheck_env_and_command():
+    """The N > 1 self-check job: its launcher line and an environment without the
+    parent launcher's per-rank variables (the child's own launcher sets them)."""
+    import argparse
+    import bench
+    env = {"RANK": "1", "LOCAL_RANK": "1", "WORLD_SIZE": "8", "MASTER_PORT": "1", "MASTER_ADDR": "x",
+           "TORCHELASTIC_RUN_ID": "r", "NLS_PEER": "1", "PATH": "/bin", "OMP_NUM_THREADS": "16"}
+    e = bench.selfcheck_env(env)
+    assert e["PATH"] == "/bin" and e["OMP_NUM_THREADS"] == "16" and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert not any(k in e for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "MASTER_ADDR",
+                                    "TORCHELASTIC_RUN_ID", "NLS_PEER"))
+    a = argparse.Namespace(workload="nlse3d_512", n=None, m=None)
+    cmd = bench.selfcheck_cmd(8, a, "/tmp/x.json", 29600)
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29600" in cmd
+    i = cmd.index("--selfcheck-json")
+    assert cmd[i + 1] == "/tmp/x.json" and cmd[cmd.index("--gpus") + 1] == "8"
+
+
+def test_bench_choose_exchange():
+    """Peer stores only when their field check passed, they actually ran and were faster."""
+    import bench
+    ok = {"default": {"ok": True}, "peer": {"ok": True, "state": "active"}}
+    assert bench.choose_exchange(dict(ok, ab={"default_ms": 4.4, "peer_ms": 4.1})) == "peer"
+    assert bench.choose_exchange(dict(ok, ab={"default_ms": 4.0, "peer_ms": 4.1})) == "default"
+    assert bench.choose_exchange(dict(ok, ab={"default_ms": 4.4})) == "default"
+    bad = {"default": {"ok": True}, "peer": {"ok": False, "state": "active"}, "ab": {"default_ms": 4.4, "peer_ms": 1}}
+    assert bench.choose_exchange(bad) == "default"
+    fb = {"default": {"ok": True}, "peer": {"ok": True, "state": "fell_back"}, "ab": {"default_ms": 4.4, "peer_ms": 1}}
+    assert bench.choose_exchange(fb) == "default"
+    assert bench.choose_exchange({"default": {"ok": False}, "peer": {"ok": False}, "error": "x"}) == "default"
+
+
+def test_bench_selfcheck_job_over_gloo(monkeypatch):
+    """run_selfcheck starts the real child job (torch.distributed.run, 2 gloo ranks,
+    bench.py --selfcheck-json) and reads its report; NLS_BENCH_SELFCHECK_DRY=1 swaps the
+    device legs for the same gather / compare plumbing on a synthetic field (no GPU here)."""
+    import argparse
+    import bench
+    monkeypatch.setenv("NLS_BENCH_SELFCHECK_DRY", "1")
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    a = argparse.Namespace(workload="nlse3d_512", n=None, m=None)
+    rep = bench.run_selfcheck(2, a)
+    assert rep["child_rc"] == 0, rep
+    assert rep["n_ranks"] == 2
+    for leg in ("default", "peer"):
+        assert rep[leg]["ok"] and rep[leg]["rel_l2_vs_1rank"] == 0.0 and rep[leg]["comm_count"] == [2, 2]
+    assert bench.choose_exchange(rep) == "peer"
+
+
+def test_bench_selfcheck_job_failure_reported(monkeypatch):
+    """A child job that dies leaves the default exchange and a report saying so."""
+    import argparse
+    import bench
+    monkeypatch.setattr(bench, "selfcheck_cmd", lambda n, args, path, port: ["false"])
+    rep = bench.run_selfcheck(2, argparse.Namespace(workload="nlse3d_512", n=None, m=None))
+    assert rep["child_rc"] == 1 and "error" in rep
+    assert bench.choose_exchange(rep) == "default"

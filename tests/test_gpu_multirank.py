@@ -204,13 +204,15 @@ def test_pass2_rccl_collective_path_single_rank(monkeypatch):
     assert rel_l2(got, ref) <= 1e-10
 
 
-@pytest.mark.parametrize("nranks,nz", [(2, 24), (4, 40)])
-def test_peer_slabs_bitwise_equal_exchange(monkeypatch, nranks, nz):
+@pytest.mark.parametrize("nranks,nz,m", [(2, 24, 12), (4, 40, 12), (2, 24, 3), (2, 24, 4), (3, 24, 4)])
+def test_peer_slabs_bitwise_equal_exchange(monkeypatch, nranks, nz, m):
     """The peer-store path moves the same bytes as the exchange: the unsplit two-vector
     passes (one k_p2d launch per pass, the send/recv after it) and NLS_PEER=1 (the same
     launch shape; k_p2d<..., PEER> stores the boundary planes into the neighbours' ghost
-    planes itself) give bit-identical fields."""
-    nx, ny, m = 64, 16, 12
+    planes itself) give bit-identical fields.  m = 3, 4: the blind J = 0 pass that opens
+    each step writes the neighbours' ghost planes of S_{m-2}, which their previous tail
+    read -- ordered by the per-step W_0 halo; several steps over two calls."""
+    nx, ny = 64, 16
     dx = 20.0 / 511
     P = nx * ny
     u0 = field(nx * ny * nz, seed=11)
@@ -227,6 +229,8 @@ def test_peer_slabs_bitwise_equal_exchange(monkeypatch, nranks, nz):
         def body(s):
             s.set_field(u0[s.z0 * P:(s.z0 + s.nzl) * P])
             s.step(1e-3, 4)
+            s.step(1e-3, 2)
+            assert s.peer_state() == ("active" if env.get("NLS_PEER") == "1" else "off")
             return s.z0, s.get_field()
         res = sorted(run_ranks(nranks, mk, body), key=lambda t: t[0])
         return np.concatenate([r[1] for r in res])
