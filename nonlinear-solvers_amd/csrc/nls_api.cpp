@@ -127,6 +127,7 @@ struct nls_handle {
   cplx *partP2 = nullptr;      // per-workgroup partials of the pass
   int p2grid = 0, p2kz = 32;
   int p2kzj = 32;              // tile depth of the register-row passes (pass2_jreg)
+  int p2kz0 = 64;              // tile depth cap of the 3D J = 0 pass (NLS_P2_KZ0)
   bool p2_d2 = false;          // 2D grid seen as planes of 4 rows by k_p2d (p2_geo)
   bool p2_split_on = true;     // collective handles: boundary/interior split (NLS_P2_SPLIT=0: off)
   cplx *zbuf = nullptr;        // one zero row (nx cells): the DMA source of out-of-grid rows
@@ -915,7 +916,7 @@ int p2_kz(const nls_handle *h, int J) {
   // the J = 0 pass (one read, two writes, three workgroups per CU) also streams faster
   // from 64-plane tiles: 512^3 1.29-1.30 vs 1.33-1.34 ms on two boxes; the ring passes at
   // J = 2..6, 12 lose at 64 (profiles/r04/p2ab_512.txt, calls r4g and r4w)
-  if (J == 0) return std::min(h->p2kz, 64);
+  if (J == 0) return std::min(h->p2kz, h->p2kz0);
   return h->p2kz;
 }
 int p2_grid(const nls_handle *h, int J = 0) {
@@ -1252,6 +1253,7 @@ void alloc_all(nls_handle *h) {
     h->p2kz = (int)std::max<int64_t>(std::min<int64_t>(16, span), std::min<int64_t>(256, (span + nzc - 1) / nzc));
     if (const char *e = std::getenv("NLS_P2_KZ")) h->p2kz = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("NLS_P2_KZJ")) h->p2kzj = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("NLS_P2_KZ0")) h->p2kz0 = std::max(1, std::atoi(e));
     // tile order (round 3, tools/order_sweep.py, tools/wl_ab.sh): 3D x-fastest without XCD
     // bands (512^3 passes 25.6 -> 25.1 ms per step; 256^3 -0.5 %); 2D keeps the bands
     // (4096^2 passes 3.14 -> 3.34 ms without them)

@@ -274,6 +274,78 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
 #undef NLS_TQ_NEXT
 }
 
+// march3p: the 3D isotropic march with one row per thread (march<S, 3, 1>'s cells,
+// couplings, arithmetic order and tile order, so its callers' sums are bit-identical),
+// software-pipelined: the stencil vector's own row is loaded two planes ahead and the
+// plane's side values (rows y-1, y+1 and the wave's x-edge cell) one plane ahead, so no
+// load is consumed in the iteration that issues it.  (march loads the y and x-edge values
+// of a plane in the iteration that uses them: their L2 latency is exposed once per plane,
+// k_alpha_l2 at 512^3 waited on memory 0.59 of its cycles with 0.21 issuing,
+// profiles/r05/sq2_nlse3d_512.txt.)  No barrier inside: no tile queue.
+template <class S, class Fn>
+__device__ __forceinline__ void march3p(const S *__restrict__ V, const Geo &g, Fn &&fn) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t ntx64, nty64, ntz64;
+  tile_counts<3, 1>(g, ntx64, nty64, ntz64);
+  const int ntx = (int)ntx64, nty = (int)nty64;
+  const int tiles = (int)(ntx64 * nty64 * ntz64);
+  const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, qa = g.qa, qb = g.qb, kz = g.kz;
+  const int z0 = (int)g.z0, npl = (int)g.npl;
+  for (int t = (int)blockIdx.x; t < tiles; t += (int)gridDim.x) {
+    const int it = t % ntx;
+    const int rest = t / ntx;
+    const int jt = rest % nty;
+    const int kt = rest / nty;
+    const int x = it * 64 + lane;
+    const bool xin = x < nx;
+    const int y = jt * 4 + w;
+    if (y >= nyp) continue;  // wave-uniform
+    const int q0 = qa + kt * kz;
+    const int q1 = q0 + kz < qb ? q0 + kz : qb;
+    const int off = y * nx + x;
+    const bool edge_ld = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin;
+    const int eo = lane == 0 ? -1 : 1;
+    const bool bxy = x == 0 || x == nx - 1 || y == 0 || y == nyp - 1;
+    // the own row of plane q: zero outside the global grid (march's prev / next rules)
+    auto own = [&](int q) -> S {
+      const int gq = z0 + q;
+      return (xin && gq >= 0 && gq < npl) ? V[q * P + off] : zero<S>();
+    };
+    auto side = [&](int q, S &ym, S &yp, S &xe) {
+      const int gq = z0 + q, p = q * P + off;
+      ym = (xin && (gq > 0 || y > 0)) ? V[p - nx] : zero<S>();            // idx - nx >= 0
+      yp = (xin && (gq < npl - 1 || y < nyp - 1)) ? V[p + nx] : zero<S>();  // idx + nx < N
+      xe = edge_ld ? V[p + eo] : zero<S>();
+    };
+    S am = own(q0 - 1), a0 = own(q0), a1 = own(q0 + 1);
+    S a2 = q0 + 2 <= q1 ? own(q0 + 2) : zero<S>();
+    S ym, yp, xe;
+    side(q0, ym, yp, xe);
+    for (int q = q0; q < q1; ++q) {
+      // issue: the side values of plane q+1, the own row of plane q+3 (uniform guards)
+      S ymn = zero<S>(), ypn = zero<S>(), xen = zero<S>();
+      if (q + 1 < q1) side(q + 1, ymn, ypn, xen);
+      const S a3 = q + 3 <= q1 ? own(q + 3) : zero<S>();
+      const int gq = z0 + q;
+      S xm = shfl_up1(a0), xp = shfl_dn1(a0);
+      if (lane == 0) xm = xe;
+      if (lane == 63) xp = xe;
+      if (!(x > 0)) xm = zero<S>();
+      if (!(x + 1 < nx)) xp = zero<S>();
+      const bool bnd = bxy || gq == 0 || gq == npl - 1;
+      const S lap = g.s * (((am + a1) + (xm + xp)) + (ym + yp)) + (bnd ? g.sd_bd : g.sd_in) * a0;
+      if (xin) fn(q * P + off, a0, lap);
+      am = a0;
+      a0 = a1;
+      a1 = a2;
+      a2 = a3;
+      ym = ymn;
+      yp = ypn;
+      xe = xen;
+    }
+  }
+}
+
 #include "nls_march_q.hpp"
 
 #ifndef NLS_UPD_RB_MODE
@@ -304,6 +376,9 @@ constexpr int RB_ALPHA = 4;
 #define NLS_RB_L2 1  // measured at 512^3: RB 1 / kz 32 0.50 ms vs RB 4 / kz 8 0.58 ms (tools/exp_l2.sh)
 #endif
 constexpr int RB_L2 = NLS_RB_L2;  // rows per thread of k_alpha_l2
+#ifndef NLS_L2_PIPE
+#define NLS_L2_PIPE 0  // 3D isotropic k_alpha_l2 through the pipelined march (march3p): measured slower, off
+#endif
 #ifndef NLS_FUSED_RB
 #define NLS_FUSED_RB 1
 #endif
@@ -606,11 +681,15 @@ template <class S, int DIM, bool ANI>
 __global__ __launch_bounds__(NTHREADS) void k_alpha_l2(const S *__restrict__ V, Geo g,
                                                        cplx *__restrict__ part) {
   double a = 0.0, n2 = 0.0, l2 = 0.0;
-  march<S, DIM, RB_L2, false, ANI>(V, g, [&](int, const S &c, const S &lap) {
+  auto body = [&](int, const S &c, const S &lap) {
     a += to_c(cj_mul(c, lap)).re;
     n2 += abs2(c);
     l2 += abs2(lap);
-  });
+  };
+  // 3D isotropic, NLS_L2_PIPE=1: the pipelined march (512^3, same box, two rounds: 0.52-0.54 ms
+  // against 0.50 through march, profiles/r06/ab_alpha_l2_pipe.txt; off)
+  if constexpr (DIM == 3 && !ANI && RB_L2 == 1 && NLS_L2_PIPE) march3p<S>(V, g, body);
+  else march<S, DIM, RB_L2, false, ANI>(V, g, body);
   cplx v[3] = {{a, 0.0}, {n2, 0.0}, {l2, 0.0}};
   block_store<3>(v, part, gridDim.x, 0);
 }
