@@ -1986,6 +1986,7 @@ struct OnStream2 {
 bool sewi_concurrent(nls_handle *h) {
   // (not the register form: its y = L S_J buffer is one per handle)
   if (!NLS_KG_CONCURRENT || h->collective || !h->pass2 || h->p2reg || !use_tail(h, TAIL_SEWI_END)) return false;
+  if (h->timing) return false;  // per-kernel timing: the serial order (bit-identical; see issue_step's KG)
   if (h->B[1].W) return true;
   if (h->sewi_serial) return false;
   if (const char *e = std::getenv("NLS_SEWI_CONCURRENT"))  // 0: the serial order (A/B)
@@ -1993,6 +1994,16 @@ bool sewi_concurrent(nls_handle *h) {
   const size_t bytes = (size_t)h->nvec[0] * h->vs * h->esize;
   const size_t psb = p2state_bytes();
   const size_t na = std::max<size_t>(2 * (size_t)h->grid_alpha, 3 * (size_t)h->grid_alpha2);
+  // The second basis doubles the handle's basis memory (knob table): take
+  // it only with a quarter of the device's memory (at least 4 GB) still free beside it, so
+  // buffers this handle or the application allocate later do not fail where they would
+  // not have; otherwise the step stays serial
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes + std::max(tot / 4, size_t(4) << 30)) {
+    (void)hipGetLastError();
+    h->sewi_serial = true;
+    return false;
+  }
   void *W = nullptr, *st = nullptr, *p2 = nullptr, *pa = nullptr, *pp = nullptr;
   bool ok = hipMalloc(&W, bytes) == hipSuccess && hipMalloc(&st, sizeof(KState)) == hipSuccess &&
             hipMalloc(&p2, 2 * psb) == hipSuccess && hipMalloc(&pa, na * sizeof(cplx)) == hipSuccess &&
@@ -2154,7 +2165,9 @@ void issue_step(nls_handle *h, double dt) {
       // W_0 (TAIL_COMBINE_W0), then the cos basis ends in the Gautschi update that reads
       // that one vector (TAIL_KG_END1).  On one rank the two bases run concurrently
       // (each basis' chain of small reduction kernels then overlaps the other's passes)
-      if (h->stream2) {
+      // (with per-kernel timing on, the serial order -- bit-identical -- so no kernel's
+      // events span another stream's work and the class times add up to wall time)
+      if (h->stream2 && !h->timing) {
         hip_check(h, hipEventRecord(h->ev_fork, h->stream), "hipEventRecord");
         hip_check(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0), "hipStreamWaitEvent");
         {

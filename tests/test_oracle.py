@@ -508,6 +508,19 @@ def ref_kappa(d, m, t, func):
     return abs(t) * (np.sqrt(rho) if func in REAL_FUNCS else rho)
 
 
+def ref_action_err(got, ref):
+    """rel-L2 of an action, scaled by max|ref| first (sinc(t lambda) of an imaginary
+    argument grows like sinh: at kappa ~ 480 its entries are finite but the norm overflows)."""
+    sc = np.abs(ref).max()
+    return rel_l2(got / sc, ref / sc)
+
+
+def ref_overflows(ref):
+    """The reference's own action is not finite (sinc(t lambda) = sinh(|t lambda|)/|t lambda|
+    past ~710): there is nothing to compare but the overflow itself."""
+    return not np.all(np.isfinite(ref))
+
+
 def ref_cases(name):
     """(t, func) pairs checked on a fixture: the real t sqrt|lambda| functions at the
     Gautschi steps' dt (sg_driver_dev.cpp: 5/500) and 10x; the complex conventions at
@@ -552,13 +565,21 @@ def test_ref_krylov_action(name, m):
     dim, n, dx = int(d["dim"]), int(d["n"]), float(d["dx"])
     g = O.grid(dim, n, n, n, dx, dx)
     real = "_real" in name
+    checked = overflow = 0
     for t, func in ref_cases(name):
         kap = ref_kappa(d, m, t, func)
-        if func == 7 and kap > 300:
-            continue
         got = O.krylov_r(g, d["u"], t, m, func) if real else O.krylov_c(g, d["u"], t, m, func)
-        err = rel_l2(got, ref_action(d, m, t, func))
+        with np.errstate(all="ignore"):
+            ref = ref_action(d, m, t, func)
+        if ref_overflows(ref):
+            # (sinc of an imaginary t lambda past kappa ~ 710): the oracle overflows too
+            assert func == 7 and not np.all(np.isfinite(got)), (t, func, kap)
+            overflow += 1
+            continue
+        err = ref_action_err(got, ref)
         assert err <= TOL_REF_ACT_K * (1 + kap), (t, func, err, kap)
+        checked += 1
+    assert checked >= len(ref_cases(name)) - 2  # at most the two sinc(t lambda) cases overflow
 
 
 def test_ref_neumann_bc_2d():
