@@ -257,6 +257,16 @@ static_assert(p2d_rings_ok(0, 2) && p2d_rings_ok(2, 2) && p2d_rings_ok(4, 2) && 
               p2d_rings_ok(8, 2) && p2d_rings_ok(10, 2) && p2d_rings_ok(12, 2) && p2d_rings_ok(14, 2),
               "anisotropic cell-pair rings do not fit the LDS");
 
+// (occupancy experiment: LDS padding that caps the 3D isotropic passes 0 < J <= NLS_P2D_CAP2_MAXJ
+// at two workgroups per CU; 0: off)
+#ifndef NLS_P2D_CAP2_MAXJ
+#define NLS_P2D_CAP2_MAXJ 0
+#endif
+__host__ __device__ constexpr int p2d_cap_pad(int J, int A = 0) {
+  return (A == 0 && J > 0 && J <= NLS_P2D_CAP2_MAXJ && p2d_lds_bytes(J, A) < 56 * 1024) ? 56 * 1024 - p2d_lds_bytes(J, A)
+                                                                                         : 0;
+}
+
 // VMEM ops issued after the last one step i needs, up to its wait (see k_p2d): a
 // replay of the wave's issue order.  After the prologue's full wait the wave issues
 // the S groups of planes k0+2 .. k0+1+DS (NSD DMAs each: 2 S rows, main + halo, and
@@ -448,7 +458,7 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : (D2 ? 3 : 0
   constexpr int NC = (HZ ? 2 * (J + 1) + 3 : J + 2) + (J == 0 ? 1 : 0);
   constexpr int NPD = NP > 0 ? NP : 1;
   constexpr int RW = P2D_SRB / 16;           // cplx per staged S row (68)
-  __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J, KA)];
+  __shared__ __attribute__((aligned(16))) char smem[p2d_lds_bytes(J, KA) + p2d_cap_pad(J, KA)];
   const cplx *Sr = reinterpret_cast<const cplx *>(smem);             // [NSL][P2D_SR][RW]
   const double *Cr = reinterpret_cast<const double *>(smem + p2d_off_c_ring(J, KA));  // A: [NSL][p2d_csb/8]
   cplx *Lr = reinterpret_cast<cplx *>(smem + p2d_off_l(J, KA));       // [2][P2D_LR][64]

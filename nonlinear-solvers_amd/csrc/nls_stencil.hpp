@@ -716,8 +716,14 @@ __device__ __forceinline__ double sin_rl(double x) {
   return sn;
 }
 
+#ifndef NLS_TAIL_LDS_PAD
+#define NLS_TAIL_LDS_PAD 0
+#endif
+#ifndef NLS_TAIL_WPE
+#define NLS_TAIL_WPE 1  // waves per SIMD the fused tail's registers must allow (launch bound; 1: unconstrained)
+#endif
 template <class S, int DIM, int M, bool ANI, int MODE>
-__global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
+__global__ __launch_bounds__(NTHREADS, NLS_TAIL_WPE) void k_tail(TailArgs ta, Geo g) {
   static_assert(M >= 3, "the stencil vector must not be W_0 (updated in place)");
   constexpr int J = M - 2;
   constexpr int NF = tail_nf(MODE);
@@ -725,6 +731,11 @@ __global__ __launch_bounds__(NTHREADS) void k_tail(TailArgs ta, Geo g) {
   constexpr int M2 = MODE == TAIL_KG_END ? M : 1;
   __shared__ S cf[NF][MMAX + 1];  // cf[f][k] for W_k (k <= J), cf[f][J+1] for L W_J
   __shared__ double c2[MMAX];     // KG: combination of the stored basis
+#if NLS_TAIL_LDS_PAD
+  // (occupancy experiment: LDS that caps the workgroups per CU)
+  __shared__ volatile char lds_pad[NLS_TAIL_LDS_PAD];
+  if (threadIdx.x == 0 && g.nx < 0) lds_pad[0] = 1;
+#endif
   const KState *__restrict__ st = ta.st;
   if (threadIdx.x <= J + 1) {
     const int k = threadIdx.x;

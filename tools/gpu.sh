@@ -70,6 +70,9 @@ for st in "$@"; do
       wl=${arg:-nlse3d_512}
       run 300 "$OUT/bench_${wl}_under_rocprof.json" rocprofv3 --kernel-trace --stats -d "$OUT/prof_$wl" -o run \
         --output-format csv -- python3 bench.py --workload "$wl" --steps 10 --warmup 2 --no-cpu-baseline
+      # the bench's own dispatches (after the placement probe's; tools/trace_stats.py)
+      f=$(ls "$OUT/prof_$wl"/*kernel_trace.csv 2>/dev/null | head -n 1)
+      [ -n "$f" ] && python3 tools/trace_stats.py "$f" > "$OUT/prof_$wl/bench_kernel_stats.csv"
       cat "$OUT/bench_${wl}_under_rocprof.json" ;;
     pmc)
       wl=${arg:-nlse3d_512}
