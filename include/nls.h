@@ -288,7 +288,7 @@ int nls_debug_knob(nls_handle *h, int32_t knob, int32_t value);
 /* Basis placement chosen at nls_create.  The streams of one pass run 2-4 % faster or
  * slower depending on which HBM pages back the Krylov basis (DESIGN.md section 4,
  * "Placement"), which no allocation call controls: large single-rank handles allocate
- * up to NLS_PLACE candidate bases (default 6, where free memory allows), time the
+ * up to NLS_PLACE candidate bases (default 8, where free memory allows), time the
  * same probe step sequence on each, keep the fastest and free the rest; the chosen
  * basis is then zeroed, so results do not depend on the choice.  *n = candidates
  * probed (0: no probe on this handle), *chosen = index kept, ms[0..min(n,cap)) =

@@ -161,6 +161,7 @@ struct nls_handle {
   bool p2_pr = false;          // real field marched as cell pairs by k_p2d (p2_geo)
   bool p2_ani = false;         // k_p2d with the G2 operator (nls_pass2a.hip)
   int grid_alpha2 = 1, kz_alpha2 = NLS_KZ_L2, kz_fused = 0;  // kz_fused 0: geo.kz
+  bool l2pipe = false;  // 3D k_alpha_l2 through the pipelined march (small slabs; NLS_L2_PIPE=0/1 forces)
   int tail_grid[TAIL_NMODES] = {};  // per TailMode; 0: no such kernel (unfused path)
   int tail_dyn_grid[TAIL_NMODES] = {};  // resident workgroups of each tail kernel (dynamic tile queue)
   bool tail_dyn = false;      // fused tail through the dynamic tile queue (debug knob 1)
@@ -648,7 +649,7 @@ void alpha_l2_pass(nls_handle *h, int b, int j) {
   Geo gg = h->geo;
   gg.kz = h->kz_alpha2;
   void *args[] = {&vj, &gg, &h->partA};
-  launch(h, 0, j, kernel_alpha_l2(h->cplx_, (int)h->cfg.dim, h->ani), h->grid_alpha2, args);
+  launch(h, 0, j, kernel_alpha_l2(h->cplx_, (int)h->cfg.dim, h->ani, h->l2pipe), h->grid_alpha2, args);
 }
 
 // Launch k_alpha<j> on vector j of basis b
@@ -1279,9 +1280,16 @@ void alloc_all(nls_handle *h) {
   h->fused_tail = h->m >= 3;
   if (const char *e = std::getenv("NLS_FUSED_TAIL")) h->fused_tail = h->fused_tail && (std::atoi(e) != 0 || h->pass2);
   if (h->fused_tail) {
+    // the pipelined march where the alpha pass is latency-bound: slabs below the large
+    // class, whose one-tile-per-workgroup grids leave each wave a whole z column of
+    // exposed plane-by-plane latencies (KG / G2 256^3); the 512^3 slab is bandwidth-bound
+    // and runs the plain march faster (profiles/r06/ab_alpha_l2_pipe.txt)
+    h->l2pipe = dim == 3 && !h->large;
+    if (const char *e = std::getenv("NLS_L2_PIPE")) h->l2pipe = dim == 3 && std::atoi(e) != 0;
     Geo g2 = g;
     g2.kz = h->kz_alpha2;
-    h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani), stencil_tiles(g2, dim, alpha_l2_rows_per_thread()));
+    h->grid_alpha2 = occupancy_grid(h, kernel_alpha_l2(c, dim, ani, h->l2pipe),
+                                    stencil_tiles(g2, dim, alpha_l2_rows_per_thread()));
     // large slabs: one tile per workgroup (the tail reduces nothing, so the grid
     // size only sets the dispatch balance): 512^3 m=16 tail 6.64 -> 6.38 ms against
     // two tiles per workgroup (tools/tail_sweep.sh, same box, two rounds)
@@ -1871,7 +1879,7 @@ void ss2_step(nls_handle *h, double dt) {
 // HBM pages back the basis (profiles/r05/envab_prepad.txt: a 4 GB dummy allocation ahead
 // of the basis selected the fast passes in every process); no allocation call chooses
 // pages.  So the handle chooses among allocations: up to NLS_PLACE candidate bases
-// (default 6; those that fit in free memory beside an 8 GB reserve) are allocated while
+// (default 8; those that fit in free memory beside an 8 GB reserve) are allocated while
 // the earlier ones are held, each runs the same probe -- one cold SS2 step, then
 // PLACE_STEPS timed steps of the real launch sequence on a constant field -- and the
 // fastest is kept.  512^3 m = 16 (profiles/r06/envab_place.txt): 30.40-31.52 ms per step
@@ -1882,7 +1890,7 @@ void ss2_step(nls_handle *h, double dt) {
 // keep their one allocation.
 constexpr int PLACE_STEPS = 3;  // timed probe steps per candidate
 void place_basis(nls_handle *h) {
-  int K = 6;
+  int K = 8;
   if (const char *e = std::getenv("NLS_PLACE")) K = std::atoi(e);
   K = std::min(K, NLS_PLACE_MAX);
   const bool contig = std::getenv("NLS_DEBUG_CONTIG") && std::atoi(std::getenv("NLS_DEBUG_CONTIG"));

@@ -731,8 +731,8 @@ int64_t xtiles(const Geo &g, int dim, int rb) { return dim == 3 ? cdiv(g.nx, 64)
 const void *kernel_reduce_qa(bool cplx_, int dim, bool ani) {
   return table(dim, ani)(NLS_KIND_REDUCE_QA, cplx_, 0);
 }
-const void *kernel_alpha_l2(bool cplx_, int dim, bool ani) {
-  return table(dim, ani)(NLS_KIND_ALPHA_L2, cplx_, 0);
+const void *kernel_alpha_l2(bool cplx_, int dim, bool ani, bool pipe) {
+  return table(dim, ani)(NLS_KIND_ALPHA_L2, cplx_, pipe ? 1 : 0);
 }
 const void *kernel_tail(bool cplx_, int dim, int mode, int M, bool ani) {
   return table(dim, ani)(NLS_KIND_FINAL, cplx_, mode * 64 + M);

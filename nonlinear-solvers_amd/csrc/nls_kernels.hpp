@@ -33,7 +33,7 @@ int64_t xtiles(const Geo &g, int dim, int rows_per_thread);
 //   alpha_l2 : (const S* V, Geo g, cplx* part)  -- 3 partial columns: a, ||V||^2, ||L V||^2
 //   tail(mode, M): (TailArgs a, Geo g)   -- nls_stencil.hpp TailMode, 3 <= M <= 32;
 //                  nullptr where the variant has no such tail (then the unfused path runs)
-const void *kernel_alpha_l2(bool complex_, int dim, bool ani);
+const void *kernel_alpha_l2(bool complex_, int dim, bool ani, bool pipe = false);
 //   reduce_qa  : (KState*, const cplx* partU, int nbU, int j, int do_sum, const cplx* partX,
 //                 int nbX, const S* W_j, Geo ga) -- single workgroup: the reduction after a
 //                 folded-alpha pass, with the direct alpha of W_j as fallback (need_alpha)

@@ -77,7 +77,9 @@ template <class S> const void *pick(int kind, int J) {
   switch (kind) {
     case NLS_KIND_XPAIRS: return reinterpret_cast<const void *>(&k_xpairs<S, NLS_DIM, (NLS_ANI != 0)>);
     case NLS_KIND_REDUCE_QA: return reinterpret_cast<const void *>(&k_reduce_qa<S, NLS_DIM, (NLS_ANI != 0)>);
-    case NLS_KIND_ALPHA_L2: return reinterpret_cast<const void *>(&k_alpha_l2<S, NLS_DIM, (NLS_ANI != 0)>);
+    case NLS_KIND_ALPHA_L2:  // J = 1: the pipelined march (3D)
+      return J && NLS_DIM == 3 ? reinterpret_cast<const void *>(&k_alpha_l2<S, NLS_DIM, (NLS_ANI != 0), true>)
+                               : reinterpret_cast<const void *>(&k_alpha_l2<S, NLS_DIM, (NLS_ANI != 0)>);
     case NLS_KIND_FINAL: return tail_fn(std::is_same<S, cplx>::value, J);
     case NLS_KIND_UPDATE: return update_fn<S>(J);
     case NLS_KIND_ALPHA: return reinterpret_cast<const void *>(&k_alpha<S, NLS_DIM, (NLS_ANI != 0)>);

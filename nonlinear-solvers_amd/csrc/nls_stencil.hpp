@@ -282,8 +282,9 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
 // of a plane in the iteration that uses them: their L2 latency is exposed once per plane,
 // k_alpha_l2 at 512^3 waited on memory 0.59 of its cycles with 0.21 issuing,
 // profiles/r05/sq2_nlse3d_512.txt.)  No barrier inside: no tile queue.
-template <class S, class Fn>
+template <class S, bool ANI, class Fn>
 __device__ __forceinline__ void march3p(const S *__restrict__ V, const Geo &g, Fn &&fn) {
+  const double *__restrict__ C = g.cf;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int64_t ntx64, nty64, ntz64;
   tile_counts<3, 1>(g, ntx64, nty64, ntz64);
@@ -291,6 +292,15 @@ __device__ __forceinline__ void march3p(const S *__restrict__ V, const Geo &g, F
   const int tiles = (int)(ntx64 * nty64 * ntz64);
   const int P = (int)g.P, nx = (int)g.nx, nyp = (int)g.nyp, qa = g.qa, qb = g.qb, kz = g.kz;
   const int z0 = (int)g.z0, npl = (int)g.npl;
+  // the per-plane values of one row: the vector and (ANI) the coefficient field
+  struct Row {
+    S v;
+    double c;
+  };
+  struct Side {
+    S ym, yp, xe;
+    double cym, cyp, cxe;
+  };
   for (int t = (int)blockIdx.x; t < tiles; t += (int)gridDim.x) {
     const int it = t % ntx;
     const int rest = t / ntx;
@@ -307,41 +317,68 @@ __device__ __forceinline__ void march3p(const S *__restrict__ V, const Geo &g, F
     const int eo = lane == 0 ? -1 : 1;
     const bool bxy = x == 0 || x == nx - 1 || y == 0 || y == nyp - 1;
     // the own row of plane q: zero outside the global grid (march's prev / next rules)
-    auto own = [&](int q) -> S {
+    auto own = [&](int q) -> Row {
       const int gq = z0 + q;
-      return (xin && gq >= 0 && gq < npl) ? V[q * P + off] : zero<S>();
+      const bool ld = xin && gq >= 0 && gq < npl;
+      Row r;
+      r.v = ld ? V[q * P + off] : zero<S>();
+      r.c = 0.0;
+      if constexpr (ANI) r.c = ld ? C[q * P + off] : 0.0;
+      return r;
     };
-    auto side = [&](int q, S &ym, S &yp, S &xe) {
+    auto side = [&](int q) -> Side {
       const int gq = z0 + q, p = q * P + off;
-      ym = (xin && (gq > 0 || y > 0)) ? V[p - nx] : zero<S>();            // idx - nx >= 0
-      yp = (xin && (gq < npl - 1 || y < nyp - 1)) ? V[p + nx] : zero<S>();  // idx + nx < N
-      xe = edge_ld ? V[p + eo] : zero<S>();
+      const bool lm = xin && (gq > 0 || y > 0);            // idx - nx >= 0
+      const bool lp = xin && (gq < npl - 1 || y < nyp - 1);  // idx + nx < N
+      Side sd;
+      sd.ym = lm ? V[p - nx] : zero<S>();
+      sd.yp = lp ? V[p + nx] : zero<S>();
+      sd.xe = edge_ld ? V[p + eo] : zero<S>();
+      sd.cym = sd.cyp = sd.cxe = 0.0;
+      if constexpr (ANI) {
+        sd.cym = lm ? C[p - nx] : 0.0;
+        sd.cyp = lp ? C[p + nx] : 0.0;
+        sd.cxe = edge_ld ? C[p + eo] : 0.0;
+      }
+      return sd;
     };
-    S am = own(q0 - 1), a0 = own(q0), a1 = own(q0 + 1);
-    S a2 = q0 + 2 <= q1 ? own(q0 + 2) : zero<S>();
-    S ym, yp, xe;
-    side(q0, ym, yp, xe);
+    const Side zs{zero<S>(), zero<S>(), zero<S>(), 0.0, 0.0, 0.0};
+    const Row zr{zero<S>(), 0.0};
+    Row am = own(q0 - 1), a0 = own(q0), a1 = own(q0 + 1);
+    Row a2 = q0 + 2 <= q1 ? own(q0 + 2) : zr;
+    Side sc = side(q0);
     for (int q = q0; q < q1; ++q) {
       // issue: the side values of plane q+1, the own row of plane q+3 (uniform guards)
-      S ymn = zero<S>(), ypn = zero<S>(), xen = zero<S>();
-      if (q + 1 < q1) side(q + 1, ymn, ypn, xen);
-      const S a3 = q + 3 <= q1 ? own(q + 3) : zero<S>();
+      const Side sn = q + 1 < q1 ? side(q + 1) : zs;
+      const Row a3 = q + 3 <= q1 ? own(q + 3) : zr;
       const int gq = z0 + q;
-      S xm = shfl_up1(a0), xp = shfl_dn1(a0);
-      if (lane == 0) xm = xe;
-      if (lane == 63) xp = xe;
+      S xm = shfl_up1(a0.v), xp = shfl_dn1(a0.v);
+      if (lane == 0) xm = sc.xe;
+      if (lane == 63) xp = sc.xe;
       if (!(x > 0)) xm = zero<S>();
       if (!(x + 1 < nx)) xp = zero<S>();
-      const bool bnd = bxy || gq == 0 || gq == npl - 1;
-      const S lap = g.s * (((am + a1) + (xm + xp)) + (ym + yp)) + (bnd ? g.sd_bd : g.sd_in) * a0;
-      if (xin) fn(q * P + off, a0, lap);
+      S lap;
+      if constexpr (ANI) {
+        const double cc = a0.c;
+        const bool eym = gq > 0 || y > 0, eyp = gq < npl - 1 || y < nyp - 1;
+        double cxm = shfl_up1(cc), cxp = shfl_dn1(cc);
+        if (lane == 0) cxm = sc.cxe;
+        if (lane == 63) cxp = sc.cxe;
+        const double wxm = face_w(x > 0, cc, cxm), wxp = face_w(x + 1 < nx, cc, cxp);
+        const double wym = face_w(eym, cc, sc.cym), wyp = face_w(eyp, cc, sc.cyp);
+        const double wzm = face_w(gq > 0, cc, am.c), wzp = face_w(gq + 1 < npl, cc, a1.c);
+        lap = g.s * ((((wzm * am.v + wzp * a1.v) + (wxm * xm + wxp * xp)) + (wym * sc.ym + wyp * sc.yp)) -
+                     (((wzm + wzp) + (wxm + wxp)) + (wym + wyp)) * a0.v);
+      } else {
+        const bool bnd = bxy || gq == 0 || gq == npl - 1;
+        lap = g.s * (((am.v + a1.v) + (xm + xp)) + (sc.ym + sc.yp)) + (bnd ? g.sd_bd : g.sd_in) * a0.v;
+      }
+      if (xin) fn(q * P + off, a0.v, lap);
       am = a0;
       a0 = a1;
       a1 = a2;
       a2 = a3;
-      ym = ymn;
-      yp = ypn;
-      xe = xen;
+      sc = sn;
     }
   }
 }
@@ -376,9 +413,6 @@ constexpr int RB_ALPHA = 4;
 #define NLS_RB_L2 1  // measured at 512^3: RB 1 / kz 32 0.50 ms vs RB 4 / kz 8 0.58 ms (tools/exp_l2.sh)
 #endif
 constexpr int RB_L2 = NLS_RB_L2;  // rows per thread of k_alpha_l2
-#ifndef NLS_L2_PIPE
-#define NLS_L2_PIPE 0  // 3D isotropic k_alpha_l2 through the pipelined march (march3p): measured slower, off
-#endif
 #ifndef NLS_FUSED_RB
 #define NLS_FUSED_RB 1
 #endif
@@ -677,7 +711,7 @@ __global__ __launch_bounds__(NTHREADS) void k_update(const S *__restrict__ W, S 
 // Last alpha pass of a fused-tail Lanczos (see k_final_fused): full stencil per
 // cell, so besides a = V^H L V and ||V||^2 it also reduces ||L V||^2, from which
 // the norm of the never-stored last vector follows (k_reduce_iter, ncA = 3).
-template <class S, int DIM, bool ANI>
+template <class S, int DIM, bool ANI, bool PIPE = false>
 __global__ __launch_bounds__(NTHREADS) void k_alpha_l2(const S *__restrict__ V, Geo g,
                                                        cplx *__restrict__ part) {
   double a = 0.0, n2 = 0.0, l2 = 0.0;
@@ -688,7 +722,7 @@ __global__ __launch_bounds__(NTHREADS) void k_alpha_l2(const S *__restrict__ V, 
   };
   // 3D isotropic, NLS_L2_PIPE=1: the pipelined march (512^3, same box, two rounds: 0.52-0.54 ms
   // against 0.50 through march, profiles/r06/ab_alpha_l2_pipe.txt; off)
-  if constexpr (DIM == 3 && !ANI && RB_L2 == 1 && NLS_L2_PIPE) march3p<S>(V, g, body);
+  if constexpr (PIPE && DIM == 3 && RB_L2 == 1) march3p<S, ANI>(V, g, body);
   else march<S, DIM, RB_L2, false, ANI>(V, g, body);
   cplx v[3] = {{a, 0.0}, {n2, 0.0}, {l2, 0.0}};
   block_store<3>(v, part, gridDim.x, 0);
