@@ -493,11 +493,18 @@ def run_selfcheck(n, args):
     t0 = time.perf_counter()
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "selfcheck.json")
+        # its own process group: on a timeout the launcher AND its rank processes go
+        p = subprocess.Popen(selfcheck_cmd(n, args, path, free_port()), env=selfcheck_env(os.environ),
+                             stdout=sys.stderr, stderr=sys.stderr, start_new_session=True)
         try:
-            p = subprocess.run(selfcheck_cmd(n, args, path, free_port()), env=selfcheck_env(os.environ),
-                               stdout=sys.stderr, stderr=sys.stderr, timeout=SELFCHECK_TIMEOUT)
-            rc = p.returncode
+            rc = p.wait(timeout=SELFCHECK_TIMEOUT)
         except subprocess.TimeoutExpired:
+            import signal
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except OSError:
+                pass
+            p.wait()
             rc = "timeout"
         rep = None
         if os.path.exists(path):

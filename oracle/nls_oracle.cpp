@@ -249,9 +249,13 @@ void lanczos(const Op &op, const S *u, uint32_t m, std::vector<S> &V,
 
 // Symmetric eigensolver for the real m x m matrix Eigen's SelfAdjointEigenSolver
 // sees: lower triangle of T, real part of the diagonal (Eigen's
-// tridiagonalization reads mat.diagonal().real()).  Cyclic Jacobi: an
-// algorithm independent of the device's implicit-QL, so agreement between
-// the two is a real check.  A (row-major) is overwritten; Q columns = vectors.
+// tridiagonalization reads mat.diagonal().real()).  Cyclic Jacobi.  NOTE: the device
+// eigensolve (k_reduce_final, nls_kernels.hip) runs this same Jacobi algorithm (same
+// rotation and stopping rule, T pre-scaled like Eigen's solver), so a GPU-vs-oracle
+// comparison does not check the eigensolve independently; the reference pins do
+// (tests/test_oracle.py::test_ref_krylov_action and tests/test_gpu_refpin.py build
+// f(T) e_1 with LAPACK eigh on the reference's own T).  A (row-major) is overwritten;
+// Q columns = vectors.
 void jacobi_eig(std::vector<double> A, int m, std::vector<double> &lam,
                 std::vector<double> &Q) {
   Q.assign((size_t)m * m, 0.0);

@@ -204,3 +204,21 @@ def test_bench_selfcheck_job_failure_reported(monkeypatch):
     rep = bench.run_selfcheck(2, argparse.Namespace(workload="nlse3d_512", n=None, m=None))
     assert rep["child_rc"] == 1 and "error" in rep
     assert bench.choose_exchange(rep) == "default"
+
+
+def test_bench_selfcheck_timeout_kills_the_job(monkeypatch, tmp_path):
+    """A hung self-check job is killed with its whole process group at the timeout."""
+    import argparse
+    import bench
+    marker = tmp_path / "child_pid"
+    script = f"import os, time; open({str(marker)!r}, 'w').write(str(os.getpid())); time.sleep(60)"
+    import sys
+    monkeypatch.setattr(bench, "selfcheck_cmd",
+                        lambda n, args, path, port: ["bash", "-c", f"{sys.executable} -c \"{script}\" & wait"])
+    monkeypatch.setattr(bench, "SELFCHECK_TIMEOUT", 3)
+    rep = bench.run_selfcheck(2, argparse.Namespace(workload="nlse3d_512", n=None, m=None))
+    assert rep["child_rc"] == "timeout" and bench.choose_exchange(rep) == "default"
+    pid = int(marker.read_text())
+    import time
+    time.sleep(0.5)
+    assert not os.path.exists(f"/proc/{pid}") or open(f"/proc/{pid}/stat").read().split()[2] == "Z"

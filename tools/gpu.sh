@@ -81,7 +81,10 @@ for st in "$@"; do
       for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
         i=$((i + 1))
         echo "[gpu.sh] $(date +%T) pmc $grp"
-        timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_$wl/p$i" -o run -- \
+        # NLS_PLACE=1: no placement probe (its candidates' dispatches would enter the per-kernel
+        # averages; the bytes a kernel moves do not depend on the placement,
+        # profiles/r06/place_diag.txt), so the tails that write u stay 2 of 7
+        NLS_PLACE=1 timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_$wl/p$i" -o run -- \
           python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/pmc_$wl/p$i.log" 2>&1 || exit $?
       done ;;
     sq)
@@ -89,7 +92,7 @@ for st in "$@"; do
       wl=${arg:-nlse3d_512}
       mkdir -p "$OUT/sq_$wl"
       echo "[gpu.sh] $(date +%T) sq $wl"
-      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+      NLS_PLACE=1 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY \
         SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/sq_$wl/p1" -o run -- \
         python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/sq_$wl/p1.log" 2>&1 || exit $?
       python3 tools/pmc_table.py "$OUT/sq_$wl" > "$OUT/sq_$wl.txt" && cat "$OUT/sq_$wl.txt" ;;
@@ -98,7 +101,7 @@ for st in "$@"; do
       wl=${arg:-nlse3d_512}
       mkdir -p "$OUT/sq2_$wl"
       echo "[gpu.sh] $(date +%T) sq2 $wl"
-      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS \
+      NLS_PLACE=1 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS \
         SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/sq2_$wl/p1" -o run -- \
         python3 bench.py --workload "$wl" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/sq2_$wl/p1.log" 2>&1 || exit $?
       python3 tools/pmc_table.py "$OUT/sq2_$wl" > "$OUT/sq2_$wl.txt" && cat "$OUT/sq2_$wl.txt" ;;
