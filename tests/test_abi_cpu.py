@@ -233,3 +233,16 @@ def test_comm_size_rejects_null_handle():
     n, tr = C.c_int32(-7), C.c_int32(-7)
     assert L.nls_comm_size(None, C.byref(n), C.byref(tr)) == -1
     assert n.value == -7 and tr.value == -7
+
+
+def test_placement_and_peer_state_reject_null_handle():
+    """nls_placement / nls_peer_state (ABI 6) fail cleanly without a handle or an output
+    pointer, leaving the outputs untouched -- no device needed."""
+    import ctypes as C
+    L = nls_amd.lib()
+    n, k = C.c_int32(-7), C.c_int32(-7)
+    ms = (C.c_float * 8)()
+    assert L.nls_placement(None, C.byref(n), C.byref(k), ms, 8) == -1
+    assert n.value == -7 and k.value == -7
+    st = C.c_int32(-7)
+    assert L.nls_peer_state(None, C.byref(st)) == -1 and st.value == -7
