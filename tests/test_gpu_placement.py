@@ -73,3 +73,27 @@ def test_no_probe_off_the_large_slab_class(monkeypatch):
     monkeypatch.setenv("NLS_LARGE_SLAB", "1")
     with nls_amd.Solver(3, 32, 32, 32, 0.5, 0.5, equation=nls_amd.SG_GAUTSCHI, m=10) as s:
         assert s.placement()["candidates"] == 0
+
+
+def test_placement_full_size_512_bitwise(monkeypatch):
+    """The bench's own case: 512^3 m = 16 (large class, up to 8 candidates probed) against
+    one allocation, two steps of one call, bit for bit."""
+    n, m = 512, 16
+    dx = 20.0 / (n - 1)
+    x = np.linspace(-10, 10, n)
+    g = np.exp(-(x ** 2) / 8.0)
+    u0 = ((g[:, None, None] * g[None, :, None]) * (g * np.exp(0.5j * x))[None, None, :]).ravel()
+    out = []
+    for place in ("1", "8"):
+        monkeypatch.setenv("NLS_PLACE", place)
+        with nls_amd.Solver(3, n, n, n, dx, dx, m=m) as s:
+            pl = s.placement()
+            s.set_field(u0)
+            s.step(1e-3, 2)
+            out.append(s.get_field())
+        if place == "1":
+            assert pl["candidates"] == 0
+        else:
+            assert pl["candidates"] >= 2 and pl["probe_ms"][pl["chosen"]] == min(pl["probe_ms"])
+    assert np.array_equal(out[0], out[1])
+    assert rel_l2(out[0], u0) > 1e-8
