@@ -404,6 +404,14 @@ def load_traffic(workload, m, kernel_prefix):
         return None
 
 
+def _build_record(nls_amd):
+    info = nls_amd.build_info()
+    now = nls_amd.sources_sha256()
+    return {"lib_src_sha256": info.get("src_sha256"), "sources_sha256": now,
+            "lib_matches_sources": bool(now) and info.get("src_sha256") == now,
+            "built": info.get("built"), "compiler": info.get("compiler")}
+
+
 def _claim_stdout():
     """The contract's stdout is ONE JSON line, but native libraries print there too
     (RCCL's version banner at communicator init): route fd 1 to stderr for the run and
@@ -881,6 +889,9 @@ def main():
         # the basis allocation kept among the candidates probed at nls_create (DESIGN.md
         # section 4 "Placement"; candidates 0: no probe on this handle)
         "placement": placement,
+        # build provenance: the library's compiled-in source hash against the sources shipped
+        # beside it (a prebuilt libnls_amd.so that does not match them says so here)
+        "build": _build_record(nls_amd),
     }
     if world > 1:
         # the self-check job's report and the exchange this timed run used (peer_state of

@@ -135,6 +135,11 @@ typedef struct nls_handle nls_handle;
 /* Fill cfg with the reference defaults (m=10, CQ sigmas 0.5i / -0.5, 1 rank). */
 void nls_config_default(nls_config *cfg);
 int nls_abi_version(void);
+/* Build provenance: "src_sha256=<sha256 of the library sources> arch=gfx950 compiler=...
+ * built=..." -- the sources are every nonlinear-solvers_amd/csrc/{*.hip,*.hpp,*.cpp} in
+ * sorted path order, then include/nls.h (nls_amd.sources_sha256() recomputes it), so a
+ * prebuilt library can be checked against the tree it ships in.  No reference counterpart. */
+const char *nls_build_info(void);
 
 int nls_create(const nls_config *cfg, nls_handle **out);
 int nls_destroy(nls_handle *h);

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "nls_get_timing", "nls_reset_timing", "nls_set_coefficients", "nls_apply_bc",
     "nls_get_field_async", "nls_wait_field", "nls_host_alloc", "nls_host_free", "nls_slab_planes",
     "nls_step_sewi", "nls_debug_oplog", "nls_debug_knob", "nls_placement",
-    "nls_peer_state",
+    "nls_peer_state", "nls_build_info",
 )
 # nls_debug_oplog entry kinds (include/nls.h enum nls_op_kind)
 OP_ALLREDUCE, OP_SEND, OP_RECV, OP_WAIT_HALO, OP_WAIT_COMPUTE, OP_ALLGATHER, OP_DROPPED = 1, 2, 3, 4, 5, 6, 7
@@ -127,12 +127,46 @@ def lib():
     L.nls_debug_oplog.argtypes = [H, C.POINTER(C.c_int32), C.c_uint64, C.POINTER(C.c_uint64)]
     L.nls_debug_knob.argtypes = [H, C.c_int32, C.c_int32]
     L.nls_peer_state.argtypes = [H, C.POINTER(C.c_int32)]
+    L.nls_build_info.restype = C.c_char_p
+    L.nls_build_info.argtypes = []
     L.nls_placement.argtypes = [H, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_float),
                                 C.c_uint32]
     if L.nls_abi_version() != 6:
         raise RuntimeError("libnls_amd ABI mismatch")
     _LIB = L
     return L
+
+
+def build_info() -> dict:
+    """The library's build provenance (nls_build_info): src_sha256, arch, compiler, built."""
+    txt = lib().nls_build_info().decode()
+    out, key = {}, None
+    for tok in txt.split(" "):
+        if "=" in tok:
+            key, val = tok.split("=", 1)
+            out[key] = val
+        elif key:
+            out[key] += " " + tok
+    return out
+
+
+def sources_sha256() -> str | None:
+    """sha256 of the library sources beside this package, in the Makefile's order (sorted
+    csrc/*.hip, *.hpp, *.cpp, then include/nls.h); None where they are not present."""
+    import glob
+    import hashlib
+    root = os.path.dirname(_PKG)
+    names = sorted(os.path.relpath(p, root) for e in ("hip", "hpp", "cpp")
+                   for p in glob.glob(os.path.join(_PKG, "csrc", f"*.{e}")))
+    names.append(os.path.join("include", "nls.h"))
+    h = hashlib.sha256()
+    for n in names:
+        try:
+            with open(os.path.join(root, n), "rb") as f:
+                h.update(f.read())
+        except OSError:
+            return None
+    return h.hexdigest()
 
 
 def slab_planes(npl: int, nranks: int, rank: int) -> tuple[int, int]:

@@ -246,3 +246,13 @@ def test_placement_and_peer_state_reject_null_handle():
     assert n.value == -7 and k.value == -7
     st = C.c_int32(-7)
     assert L.nls_peer_state(None, C.byref(st)) == -1 and st.value == -7
+
+
+def test_library_build_matches_sources():
+    """Build provenance: the loaded libnls_amd.so was compiled from exactly the library
+    sources of this tree (nls_build_info's compiled-in sha256 of csrc/*.{hip,hpp,cpp} +
+    include/nls.h).  On the GPU box, where the prebuilt library travels with the tree,
+    the same test says whether the two still match."""
+    info = nls_amd.build_info()
+    assert info["arch"] == "gfx950"
+    assert info["src_sha256"] == nls_amd.sources_sha256()
