@@ -233,7 +233,7 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(args, u_full=None):
+def cpu_baseline(args, u_full=None, gpu_one=None):
     """The oracle (C++ restatement of nlse_driver.cpp -> NLSESolver::step ->
     expm_multiply) on a bounded sample of the workload, on the host: all cores
     (OpenMP build, SURVEY 8(d) "all cores" mode) and single-threaded (the
@@ -261,7 +261,7 @@ def cpu_baseline(args, u_full=None):
             out["c1_full_run"] = _cpu_c1(oracle_py, nthr, T=0.5)
             out["c1_nlse_driver_defaults"] = _cpu_c1(oracle_py, nthr, T=1.5)
             if u_full is not None and nthr > 1 and not args.no_full_grid_cpu:
-                full = _cpu_full_grid(args, oracle_py, u_full, nthr)
+                full = _cpu_full_grid(args, oracle_py, u_full, nthr, gpu_one=gpu_one)
                 sub = {k: out[k] for k in ("value", "seconds", "sample", "cores")}
                 out.update(full)
                 out["subgrid_128"] = sub
@@ -272,20 +272,27 @@ def cpu_baseline(args, u_full=None):
     return out
 
 
-def _cpu_full_grid(args, oracle_py, u, nthr, steps=1):
+def _cpu_full_grid(args, oracle_py, u, nthr, steps=1, gpu_one=None):
     """One SS2 step of the headline workload at its full grid (512^3, m = 16) through
-    the oracle on all cores: the CPU baseline at GPU size."""
+    the oracle on all cores: the CPU baseline at GPU size.  With gpu_one (the same step of
+    the same field on the GPU, bench.py main) also the full-size parity of that step."""
     w = WORKLOADS[args.workload]
     n = w["n"]
     dx = 2 * w["L"] / (n - 1)
     g = oracle_py.grid(3, n, n, n, dx, dx)
     t0 = time.perf_counter()
-    oracle_py.nlse_steps(g, u, w["dt"], steps, w["m"], nonlin=w["eq"])
+    ref = oracle_py.nlse_steps(g, u, w["dt"], steps, w["m"], nonlin=w["eq"])
     el = time.perf_counter() - t0
-    return {"value": n ** 3 * steps / el / 1e6, "unit": "Mcells*steps/s", "cores": nthr, "kind": "port",
-            "seconds": el,
-            "sample": f"3D cubic NLSE {n}^3 m={w['m']} (the full workload grid), {steps} SS2 step, "
-                      f"oracle/ C++ -O2 OpenMP {nthr} threads"}
+    out = {"value": n ** 3 * steps / el / 1e6, "unit": "Mcells*steps/s", "cores": nthr, "kind": "port",
+           "seconds": el,
+           "sample": f"3D cubic NLSE {n}^3 m={w['m']} (the full workload grid), {steps} SS2 step, "
+                     f"oracle/ C++ -O2 OpenMP {nthr} threads"}
+    if gpu_one is not None and steps == 1:
+        # north_star: "the final field matches the Eigen CPU path within 1e-10 relative L2"
+        # -- here at the headline size itself, one SS2 step from the bench's own field
+        out["parity_full_grid"] = {"check": f"GPU vs oracle, one SS2 step of the {n}^3 m={w['m']} bench field",
+                                   "rel_l2": rel_l2(gpu_one, ref), "tolerance": 1e-10}
+    return out
 
 
 def _cpu_c1(oracle_py, nthr, T=0.5):
@@ -898,9 +905,15 @@ def main():
         # this handle: "active" = peer stores, "off" = RCCL send/recv exchange)
         result["multi_gpu_check"] = check
         result["config"]["exchange"] = {"used": s.peer_state(), "chosen": (check or {}).get("exchange", "default")}
+    gpu_one = None
+    if u_full is not None and not args.no_full_grid_cpu:
+        # the full-size parity check of the CPU baseline's step (after the timed region)
+        s.set_field(u_full)
+        s.step(dt, 1)
+        gpu_one = s.get_field()
     s.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, u_full)
+        result["cpu_baseline"] = cpu_baseline(args, u_full, gpu_one)
     if rank == 0:
         print(json.dumps(result), file=out, flush=True)
     if dist is not None:
