@@ -265,3 +265,29 @@ def test_kg_pair_passes_slabs_match_single_rank(n, nranks):
     assert not err, err
     assert all(ran)
     assert rel_l2(np.concatenate(out), ref) <= TOL_TRAJ
+
+
+def test_kg_timing_on_is_bitwise_and_serial():
+    """With per-kernel timing on, the KG step runs its two Krylov actions in the serial order
+    (no kernel's events then span the other stream's work) -- bit-identical to
+    the untimed two-stream step, and every timed class is a real launch count."""
+    nx = ny = nz = 24
+    L, dt, steps = 3.0, 5e-3, 4
+    dx = 2 * L / (nx - 1)
+    u0, v0, mf, c = kg_fields(3, nx, ny, nz, L, seed=8)
+    up0 = u0 - dt * v0
+    res = {}
+    for timed in (False, True):
+        with kg_solver(3, nx, ny, nz, dx, m=10) as s:
+            s.set_coefficients(mf, c)
+            s.set_sg_state(u0, up0)
+            s.set_timing(timed)
+            for _ in range(steps):
+                s.step(dt, 1)
+                s.apply_bc()
+            res[timed] = s.get_field()
+            if timed:
+                t = s.timing()
+                assert t["steps"] == steps and t["class_count"]["final"] == 2 * steps
+                assert all(v >= 0 for v in t["class_ms"].values())
+    assert np.array_equal(res[False].view(np.uint64), res[True].view(np.uint64))
