@@ -99,6 +99,9 @@ __device__ __forceinline__ int tq_next(int32_t *tq) {
 #ifndef NLS_TQ_XCD
 #define NLS_TQ_XCD 0
 #endif
+#ifndef NLS_TQ_XCD_PHASE
+#define NLS_TQ_XCD_PHASE 0
+#endif
 constexpr int TQ_STRIDE = 32;
 constexpr int TQ_WORDS = TQ_STRIDE * 9;
 __device__ __forceinline__ int tq_next_xcd(int32_t *tq, int ntx, int nty, int ntz) {
@@ -115,7 +118,9 @@ __device__ __forceinline__ int tq_next_xcd(int32_t *tq, int ntx, int nty, int nt
       const int t = atomicAdd(tq + TQ_STRIDE * h, 1);
       if (t >= cnt) continue;
       const int it = t % ntx, r = t / ntx;
-      const int jt = yb ? lo + r % (hi - lo) : r % nty;
+      // NLS_TQ_XCD_PHASE: band h starts h * PHASE tile rows into its range (the bands'
+      // concurrent rows then sit (band + h * PHASE) rows apart, not a power of two of rows)
+      const int jt = yb ? lo + (r % (hi - lo) + h * NLS_TQ_XCD_PHASE) % (hi - lo) : r % nty;
       const int kt = yb ? r / (hi - lo) : lo + r / nty;
       tile = (kt * nty + jt) * ntx + it;
       break;

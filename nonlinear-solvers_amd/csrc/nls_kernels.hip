@@ -60,24 +60,43 @@ int tq_words() { return NLS_TQ_XCD ? TQ_WORDS : 2; }
 // ---------------------------------------------------------------------------
 // single-workgroup reductions + coefficient math + m x m eigensolve
 
+#ifndef NLS_COLSUM_U
+#define NLS_COLSUM_U 8  // loads in flight per thread of k_colsum (a power of two; 2 -> 8: 512^3 small kernels 0.334 -> 0.293 ms per step, profiles/r06/ab_halo_diag_colsum_tq.txt)
+#endif
 // The same column sums for large partial arrays (one tile per workgroup
 // grids): one workgroup per column, fixed order -> st->sums layout
 // [partA columns 0..ncA) then [partU columns 0..ncU).
-__global__ __launch_bounds__(NTHREADS) void k_colsum(const cplx *__restrict__ partA, int nbA, int ncA,
-                                                     const cplx *__restrict__ partU, int nbU,
-                                                     cplx *__restrict__ dst) {
-  const int v = blockIdx.x;
+__device__ __forceinline__ void colsum_body(const cplx *__restrict__ partA, int nbA, int ncA,
+                                            const cplx *__restrict__ partU, int nbU, cplx *__restrict__ dst,
+                                            const int v) {
   const cplx *__restrict__ col = v < ncA ? partA + (int64_t)v * nbA : partU + (int64_t)(v - ncA) * nbU;
   const int nb = v < ncA ? nbA : nbU;
-  double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
+  // U independent loads per thread and round, one accumulator each (a chain of dependent
+  // rounds over 16384 partials was the kernel's time)
+  constexpr int U = NLS_COLSUM_U;
+  double ac[U], bc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) ac[u] = bc[u] = 0.0;
   int q = threadIdx.x;
-  for (; q + NTHREADS < nb; q += 2 * NTHREADS) {
-    const cplx x0 = col[q], x1 = col[q + NTHREADS];
-    a0 += x0.re; b0 += x0.im;
-    a1 += x1.re; b1 += x1.im;
+  for (; q + (U - 1) * NTHREADS < nb; q += U * NTHREADS) {
+    cplx xs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xs[u] = col[q + u * NTHREADS];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ac[u] += xs[u].re;
+      bc[u] += xs[u].im;
+    }
   }
-  if (q < nb) { const cplx x0 = col[q]; a0 += x0.re; b0 += x0.im; }
-  const double a = wave_sum(a0 + a1), b = wave_sum(b0 + b1);
+  for (; q < nb; q += NTHREADS) { const cplx x0 = col[q]; ac[0] += x0.re; bc[0] += x0.im; }
+#pragma unroll
+  for (int s = 1; s < U; s *= 2)
+#pragma unroll
+    for (int u = 0; u + s < U; u += 2 * s) {
+      ac[u] += ac[u + s];
+      bc[u] += bc[u + s];
+    }
+  const double a = wave_sum(ac[0]), b = wave_sum(bc[0]);
   __shared__ double ra[NTHREADS / 64], rb[NTHREADS / 64];
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { ra[w] = a; rb[w] = b; }
@@ -87,6 +106,11 @@ __global__ __launch_bounds__(NTHREADS) void k_colsum(const cplx *__restrict__ pa
     for (int i = 1; i < NTHREADS / 64; ++i) { sa += ra[i]; sb += rb[i]; }
     dst[v] = {sa, sb};
   }
+}
+__global__ __launch_bounds__(NTHREADS) void k_colsum(const cplx *__restrict__ partA, int nbA, int ncA,
+                                                     const cplx *__restrict__ partU, int nbU,
+                                                     cplx *__restrict__ dst) {
+  colsum_body(partA, nbA, ncA, partU, nbU, dst, blockIdx.x);
 }
 const void *kernel_colsum() { return reinterpret_cast<const void *>(&k_colsum); }
 
@@ -850,6 +874,59 @@ static_assert(offsetof(P2State, bZ2) == offsetof(P2State, bZ1) + sizeof(cplx) &&
 const void *kernel_p2tail() { return reinterpret_cast<const void *>(&k_p2tail); }
 const void *kernel_p2tfin() { return reinterpret_cast<const void *>(&k_p2tfin); }
 const void *kernel_p2coef() { return reinterpret_cast<const void *>(&k_p2coef); }
+
+// A pass's column sums and its k_p2coef in one launch (single-rank handles; the collective
+// path all-reduces between the two): workgroup v sums column v as k_colsum does, and the
+// workgroup that finishes last -- the counter's acquire-release at agent scope publishes
+// every other workgroup's column to it -- runs the coefficient step.  The column sums are
+// the same bits as k_colsum's (same per-column order); only a launch and a kernel
+// boundary per pass go.  cnt: a zeroed device word, reset by the last workgroup.
+__global__ __launch_bounds__(NTHREADS) void k_colsum_p2coef(const cplx *__restrict__ partU, int nbU,
+                                                            cplx *__restrict__ dst, int32_t *__restrict__ cnt,
+                                                            P2State *__restrict__ ps, KState *__restrict__ st,
+                                                            int J, int mode, int ns, int nsn, int real) {
+  colsum_body(nullptr, 0, 0, partU, nbU, dst, blockIdx.x);
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    // thread 0 wrote dst[v]: its release orders that store before the count
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (int)gridDim.x - 1;
+    if (s_last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;  // uniform
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread: no stale line of the sums
+  p2coef_body(ps, st, J, mode, ns, nsn, real);
+}
+const void *kernel_colsum_p2coef() { return reinterpret_cast<const void *>(&k_colsum_p2coef); }
+
+// The end of a fused-tail basis in one launch (single-rank handles): k_alpha_l2's three
+// column sums (one workgroup each), then on the last workgroup k_p2tail, the eigensolve
+// (k_reduce_final with tail = 1) and k_p2tfin -- four launches and three kernel
+// boundaries fewer per basis, the same bits (k_colsum_p2coef's counter protocol).
+__global__ __launch_bounds__(NTHREADS) void k_tail_chain(const cplx *__restrict__ partA, int nbA,
+                                                         cplx *__restrict__ dst, int32_t *__restrict__ cnt,
+                                                         P2State *__restrict__ ps, KState *__restrict__ st, int m,
+                                                         int nf, int f0, int f1, double t_re, double t_im) {
+  colsum_body(partA, nbA, 3, nullptr, 0, dst, blockIdx.x);
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (int)gridDim.x - 1;
+    if (s_last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;  // uniform
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  p2tail_body(ps, st, dst, m);
+  __syncthreads();
+  if (threadIdx.x == 0) st->Td[m - 1] = 0.0;  // k_reduce_final, tail = 1
+  __syncthreads();
+  eigen_phase_jacobi(st, m, nf, f0, f1, t_re, t_im);
+  __syncthreads();
+  p2tfin_body(ps, st, m, nf);
+}
+const void *kernel_tail_chain() { return reinterpret_cast<const void *>(&k_tail_chain); }
 size_t p2state_bytes() { return sizeof(P2State); }
 size_t p2state_sums_offset() { return offsetof(P2State, sums); }
 size_t p2state_peer_offset() { return offsetof(P2State, pdn); }

@@ -74,6 +74,8 @@ int p2m_rows_per_thread(int J);
 //   p2tail: (P2State*, KState*, const cplx* sums, int m);  p2tfin: (const P2State*, KState*, int m, int nf)
 const void *kernel_p2tail();
 const void *kernel_p2tfin();
+const void *kernel_colsum_p2coef();  // (partU, nbU, dst, cnt, then k_p2coef's arguments)
+const void *kernel_tail_chain();  // (partA, nbA, dst, cnt, ps, st, m, nf, f0, f1, t_re, t_im)
 const void *kernel_p2coef();  // (P2State*, KState*, int J, int mode, int ns, int nsn)
 size_t p2state_bytes();
 size_t p2state_sums_offset();

@@ -52,8 +52,8 @@ struct P2State {
 // coefficients (pass_coefficients); nsn = 0: T into the KState for k_reduce_final
 // (s[] = 1, so fin is in the W basis; k_p2tfin converts it).  real: the sums come
 // from a real field marched as cell pairs; their imaginary parts are dropped.
-__global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, KState *__restrict__ st,
-                                                     int J, int mode, int ns, int nsn, int real) {
+__device__ __forceinline__ void p2coef_body(P2State *__restrict__ ps, KState *__restrict__ st, int J, int mode, int ns,
+                                            int nsn, int real) {
   __shared__ cplx q[3][P2M], sv[P2M], lw[P2M], w[2][P2M];
   __shared__ cplx bb[2][4];
   __shared__ double nu[3];
@@ -258,6 +258,10 @@ __global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, K
     ps->D[r][c] = sD[r][c];
     ps->H[r][c] = sH[r][c];
   }
+}
+__global__ __launch_bounds__(NTHREADS) void k_p2coef(P2State *__restrict__ ps, KState *__restrict__ st,
+                                                     int J, int mode, int ns, int nsn, int real) {
+  p2coef_body(ps, st, J, mode, ns, nsn, real);
 }
 
 #endif  // NLS_NO_P2_KERNELS

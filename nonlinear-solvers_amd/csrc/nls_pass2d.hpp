@@ -1070,8 +1070,8 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : (D2 ? 3 : 0
 // (s[] = 1: k_reduce_final's fin is then f(T) e_1 in the W basis) and keeps
 // t, beta in the P2State; k_p2tfin maps fin to the coefficients k_tail reads:
 // fin'[k] over the stored S_k (k <= j), fin'[j+1] for y, coef = e_{j+1}.
-__global__ __launch_bounds__(NTHREADS) void k_p2tail(P2State *__restrict__ ps, KState *__restrict__ st,
-                                                     const cplx *__restrict__ sums, int m) {
+__device__ __forceinline__ void p2tail_body(P2State *__restrict__ ps, KState *__restrict__ st,
+                                            const cplx *__restrict__ sums, int m) {
   __shared__ cplx tk[P2M];
   const int j = m - 2, t = threadIdx.x;
   for (int k = t; k < j; k += NTHREADS) {
@@ -1108,9 +1108,12 @@ __global__ __launch_bounds__(NTHREADS) void k_p2tail(P2State *__restrict__ ps, K
     st->s[t] = 1.0;
   }
 }
+__global__ __launch_bounds__(NTHREADS) void k_p2tail(P2State *__restrict__ ps, KState *__restrict__ st,
+                                                     const cplx *__restrict__ sums, int m) {
+  p2tail_body(ps, st, sums, m);
+}
 
-__global__ __launch_bounds__(NTHREADS) void k_p2tfin(const P2State *__restrict__ ps,
-                                                     KState *__restrict__ st, int m, int nf) {
+__device__ __forceinline__ void p2tfin_body(const P2State *__restrict__ ps, KState *__restrict__ st, int m, int nf) {
   __shared__ cplx fw[2][MMAX];
   const int j = m - 2, t = threadIdx.x;
   for (int e = t; e < nf * m; e += NTHREADS) fw[e / m][e % m] = st->fin[e / m][e % m];
@@ -1131,6 +1134,10 @@ __global__ __launch_bounds__(NTHREADS) void k_p2tfin(const P2State *__restrict__
     st->fin[f][l] = ps->beta * v;
   }
   for (int l = t; l <= j + 1; l += NTHREADS) st->coef[l] = {l == j + 1 ? 1.0 : 0.0, 0.0};
+}
+__global__ __launch_bounds__(NTHREADS) void k_p2tfin(const P2State *__restrict__ ps,
+                                                     KState *__restrict__ st, int m, int nf) {
+  p2tfin_body(ps, st, m, nf);
 }
 
 #endif  // NLS_NO_P2_KERNELS

@@ -31,6 +31,14 @@ namespace nls {
 // tile-edge neighbours (1 lane of 64, wave-boundary rows) use L1/L2 loads.
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Timing diagnostic only (wrong results; never a product build): the 3D march skips the
+// loads from outside its tile -- bit 1 the x-edge cells of lanes 0 / 63, bit 2 the y rows
+// above / below the tile, bit 4 the plane below the tile's first -- so a variant library
+// shows what each kind of halo load costs k_alpha_l2 and k_tail (profiles/r06/ab_halo_diag_colsum_tq.txt)
+#ifndef NLS_DIAG_HALO
+#define NLS_DIAG_HALO 0
+#endif
+
 template <int DIM, int RB> __host__ __device__ inline void tile_counts(const Geo &g, int64_t &ntx,
                                                                         int64_t &nty, int64_t &ntz) {
   const int64_t nq = g.qb - g.qa;  // local planes [qa, qb) covered by this launch
@@ -74,7 +82,9 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
   int32_t *const tq = g.tq;
 #define NLS_TQ_NEXT() (NLS_TQ_XCD ? tq_next_xcd(tq, ntx, nty, (int)ntz64) : tq_next(tq))
   for (int t0 = tq ? NLS_TQ_NEXT() : (int)blockIdx.x; t0 < tiles; t0 = tq ? NLS_TQ_NEXT() : t0 + (int)gridDim.x) {
-    // optional XCD-banded order (workgroups b, b+8 share an XCD): speed only
+    // optional XCD-banded order (workgroups b, b+8 share an XCD): speed only.  (In-plane
+    // y-bands per XCD, x fastest, so that a tile's x- and y-neighbours share its L2, made
+    // k_alpha_l2 slower at 512^3: 0.512 against 0.500 ms, profiles/r06/envab_fuse_l2remap.txt)
     const int t = (g.remap && t0 < 8 * T8) ? (t0 % 8) * T8 + t0 / 8 : t0;
     const int it = t % ntx;
     const int rest = t / ntx;
@@ -98,7 +108,7 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
           rv[r] = yb + r < nyp;
           off[r] = (yb + r) * nx + x;
           const bool ld = xin && rv[r];
-          prev[r] = (ld && z0 + q0 > 0) ? V[(q0 - 1) * P + off[r]] : zero<S>();
+          prev[r] = (ld && z0 + q0 > 0 && !(NLS_DIAG_HALO & 4)) ? V[(q0 - 1) * P + off[r]] : zero<S>();
           cur[r] = ld ? V[q0 * P + off[r]] : zero<S>();
           if constexpr (ANI) {
             cprv[r] = (ld && z0 + q0 > 0) ? C[(q0 - 1) * P + off[r]] : 0.0;
@@ -132,12 +142,14 @@ __device__ __forceinline__ void march(const S *__restrict__ V, const Geo &g, Fn 
             const bool eyp = gq < npl - 1 || y < nyp - 1;  // idx + nx < N
             const bool inner_yp = r + 1 < RB && rv[r + 1 < RB ? r + 1 : r];
             S ym, yp;
+            constexpr bool noyh = (NLS_DIAG_HALO & 2) != 0;
             if (r > 0) ym = cur[r - 1];
-            else ym = (xin && eym) ? V[p - nx] : zero<S>();
+            else ym = (xin && eym && !(noyh && w == 0)) ? V[p - nx] : zero<S>();
             if (inner_yp) yp = cur[r + 1 < RB ? r + 1 : r];
-            else yp = (xin && eyp) ? V[p + nx] : zero<S>();
+            else yp = (xin && eyp && !(noyh && w == 3)) ? V[p + nx] : zero<S>();
             S xm = shfl_up1(cur[r]), xp = shfl_dn1(cur[r]);
-            const bool edge_ld = ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin;
+            const bool edge_ld =
+                ((lane == 0 && x > 0) || (lane == 63 && x + 1 < nx)) && xin && !(NLS_DIAG_HALO & 1);
             const S xe = edge_ld ? V[p + (lane == 0 ? -1 : 1)] : zero<S>();
             if (lane == 0) xm = xe;
             if (lane == 63) xp = xe;

@@ -291,3 +291,25 @@ def test_kg_timing_on_is_bitwise_and_serial():
                 assert t["steps"] == steps and t["class_count"]["final"] == 2 * steps
                 assert all(v >= 0 for v in t["class_ms"].values())
     assert np.array_equal(res[False].view(np.uint64), res[True].view(np.uint64))
+
+
+@pytest.mark.parametrize("nx,ny,nz,m", [(12, 12, 12, 10), (64, 16, 10, 16)])
+def test_kg_fused_colsum_p2coef_bitwise_equal(monkeypatch, nx, ny, nz, m):
+    """The KG step's cell-pair passes with the column sums and k_p2coef in one launch
+    (NLS_P2_FUSE=1; one last-workgroup counter per basis, the two bases on two streams)
+    against the two launches per pass: bit for bit."""
+    L, dt, steps = 3.0, 5e-3, 4
+    dx = 2 * L / (nx - 1)
+    u0, v0, mf, c = kg_fields(3, nx, ny, nz, L, seed=8)
+    up0 = u0 - dt * v0
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("NLS_P2_FUSE", fuse)
+        with kg_solver(3, nx, ny, nz, dx, m=m) as s:
+            s.set_coefficients(mf, c)
+            s.set_sg_state(u0, up0)
+            for _ in range(steps):
+                s.step(dt, 1)
+                s.apply_bc()
+            res[fuse] = s.get_field()
+    assert np.array_equal(res["1"].view(np.uint64), res["0"].view(np.uint64))

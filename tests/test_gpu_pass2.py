@@ -222,3 +222,26 @@ def test_pass2_sg_stiff_matches_oracle():
         u = s.get_field()
         assert _ran_pass2(s, m)
     assert rel_l2(u, ref_u) <= TOL_TRAJ
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,m,large", [(3, 64, 16, 12, 16, "0"), (3, 64, 32, 20, 10, "1"),
+                                                   (3, 130, 8, 9, 5, "0"), (2, 256, 64, 1, 16, "0"),
+                                                   (3, 64, 16, 16, 4, "1")])
+def test_fused_colsum_p2coef_bitwise_equal_separate(monkeypatch, dim, nx, ny, nz, m, large):
+    """NLS_P2_FUSE=1 (k_colsum_p2coef: the pass's column sums and its coefficient step in
+    one launch, the last workgroup running k_p2coef) against the two launches: the same
+    per-column summation order, so the trajectory is the same bits."""
+    L = 10.0
+    dx = spacing(nx, L)
+    u0 = soliton_field(dim, nx, ny, nz, L, seed=17)
+    monkeypatch.setenv("NLS_LARGE_SLAB", large)
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("NLS_P2_FUSE", fuse)
+        with nls_amd.Solver(dim, nx, ny, nz if dim == 3 else 1, dx, dx, m=m) as s:
+            s.set_field(u0)
+            s.step(1e-3, 3)
+            s.step(1e-3, 2)
+            out[fuse] = s.get_field()
+    assert np.all(np.isfinite(out["1"]))
+    assert np.array_equal(out["1"].view(np.uint64), out["0"].view(np.uint64))
