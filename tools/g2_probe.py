@@ -55,7 +55,10 @@ print("   " + " ".join(out), flush=True)
 """
 
 n, m = 256, 25
-variants = [dict(kv.split("=", 1) for kv in a.split(",")) if a else {} for a in (sys.argv[1:] or ["", "NLS_P2_REG=1"])]
+# variants: one argument each, or several in one argument joined by '/' (gpu.sh py steps);
+# '-' = no change
+args = [v for a in sys.argv[1:] for v in a.split("/")] or ["", "NLS_P2_REG=1"]
+variants = [dict(kv.split("=", 1) for kv in a.split(",")) if a and a != "-" else {} for a in args]
 for extra in variants:
     env = dict(os.environ, **extra)
     print(f"# {extra}", flush=True)
