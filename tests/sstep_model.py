@@ -295,16 +295,16 @@ def pass_coefficients(C, D, H, sigma, j, ns):
     w = lw.copy()
     w[j] -= sigma
     w[:j] -= np.conj(H[j, :j])
-    b = np.zeros(4, complex)
+    b = np.zeros(6, complex)  # b[p]: coefficient of L^p S_j, p = 1..ns (ns <= 5)
     b[1] = cjj
     A, B = [], []
     for i in range(ns):
         A.append(C[:j + 1, :j + 1] @ w)
         B.append(b.copy())
         wn = (H[:j + 1, :j] @ w[:j] if j > 0 else np.zeros(j + 1, complex)) + w[j] * lw - sigma * w
-        bn = np.zeros(4, complex)
+        bn = np.zeros(6, complex)
         bn[1] = w[j] * cjj - sigma * b[1]
-        for p in range(1, 3):
+        for p in range(1, 5):
             bn[p + 1] = b[p] - sigma * b[p + 1]
         w, b = wn, bn
     return A, B
@@ -347,19 +347,19 @@ def coef_update(C, D, H, sigma, J, ns, g, G):
     return H[J + ns - 1, J + ns - 1].real if ns > 1 else sigma
 
 
-def lanczos_s(apply, u, m, p3=(2, 5), nstore=None, raw=False):
-    """lanczos2 with the s-step schedule (sstep_schedule); same returns."""
+def lanczos_s(apply, u, m, p3=(2, 5), nstore=None, raw=False, sched=None):
+    """lanczos2 with the s-step schedule (sstep_schedule, or an explicit [(J, ns)]); same returns."""
     u = np.asarray(u, dtype=np.complex128)
     beta = np.linalg.norm(u)
     S = [u / beta]
-    M = m + 3
+    M = m + 5
     C = np.zeros((M, M), complex)
     D = np.zeros((M, M), complex)
     H = np.zeros((M, M), complex)
     C[0, 0] = D[0, 0] = 1.0
     sigma = np.vdot(S[0], apply(S[0])).real  # the start's alpha pass
     mm = m if nstore is None else nstore
-    for J, ns in sstep_schedule(mm, p3):
+    for J, ns in (sched if sched is not None else sstep_schedule(mm, p3)):
         A, B = pass_coefficients(C, D, H, sigma, J, ns)
         Lp = [None, apply(S[J])]
         for p in range(2, ns + 1):
@@ -383,8 +383,8 @@ def lanczos_s(apply, u, m, p3=(2, 5), nstore=None, raw=False):
     return T, S[:m], C[:m, :m], beta, None
 
 
-def krylov_s_tail(apply, u, t, m, func, p3=(2, 5)):
-    S, C, H, _, beta = lanczos_s(apply, u, m, p3, nstore=m - 1, raw=True)
+def krylov_s_tail(apply, u, t, m, func, p3=(2, 5), sched=None):
+    S, C, H, _, beta = lanczos_s(apply, u, m, p3, nstore=m - 1, raw=True, sched=sched)
     j = m - 2
     y = apply(S[j])
     a, l2 = np.vdot(S[j], y), np.vdot(y, y).real
