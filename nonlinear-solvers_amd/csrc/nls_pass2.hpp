@@ -22,8 +22,9 @@ struct P2State {
   cplx C[P2M][P2M];  // C[l][i]: W_i = sum_l S_l C[l][i]
   cplx D[P2M][P2M];  // D[i][l]: S_l = sum_i W_i D[i][l]
   cplx H[P2M][P2M];  // H[k][i] = W_k^H L W_i
-  cplx aX[P2M], aZ[P2M], aY[P2M];  // S coefficients of V_1 (X), V_2 (Z), V_3 (Y)
+  cplx aX[P2M], aZ[P2M], aY[P2M], aW[P2M];  // S coefficients of V_1 (X), V_2 (Z), V_3 (Y), V_4 (W)
   cplx bX1, bZ1, bZ2, bY1, bY2, bY3;  // stencil coefficients: b_i[p] of L^p S_J (bZ1, bZ2 = b_2[1..2])
+  cplx bW[4];                         // b_4[1..4] (the four-vector first pass, k_p4d0)
   double sigma, beta;
   cplx sums[3 * P2M + 8];
   cplx tk[P2M];   // fused tail: t_k = W_k^H L S_{m-2} (k_p2tail)
@@ -38,9 +39,10 @@ struct P2State {
 };
 
 #ifndef NLS_NO_P2_KERNELS  // (defined by translation units that only need the types)
-// Coefficient kernel (one workgroup).  A pass at J writes ns = 1, 2 or 3 new
+// Coefficient kernel (one workgroup).  A pass at J writes ns = 1 .. 4 new
 // vectors V_1 = L W_J - sigma W_J - sum_{k<J} conj(H[J][k]) W_k, V_{i+1} = (L - sigma) V_i
-// (k_p2d: ns <= 2; the recurrences also hold for ns = 3, tests/sstep_model.py) and reduces, in this order, S_l^H V_i (l <= J, per i)
+// (k_p2d: ns <= 2; k_p4d0: ns = 4 at J = 0; the recurrences hold for any ns,
+// tests/sstep_model.py) and reduces, in this order, S_l^H V_i (l <= J, per i)
 // and the Gram V_a^H V_b (a <= b, row by row); J = 0 of a blind start also ||S_0||^2.
 // mode 0: start (after the alpha pass and reduction of W_0: s[0] = beta, H[0][0] =
 // alpha_0); mode 2: blind start, no alpha pass: the J = 0 pass runs on the raw start
@@ -54,9 +56,9 @@ struct P2State {
 // from a real field marched as cell pairs; their imaginary parts are dropped.
 __device__ __forceinline__ void p2coef_body(P2State *__restrict__ ps, KState *__restrict__ st, int J, int mode, int ns,
                                             int nsn, int real) {
-  __shared__ cplx q[3][P2M], sv[P2M], lw[P2M], w[2][P2M];
-  __shared__ cplx bb[2][4];
-  __shared__ double nu[3];
+  __shared__ cplx q[4][P2M], sv[P2M], lw[P2M], w[2][P2M];
+  __shared__ cplx bb[2][6];
+  __shared__ double nu[4];
   __shared__ double s_prev, s_beta;
   // C, D, H staged in LDS for the kernel's lifetime (its loops are chains of dependent
   // reads), written back at the end
@@ -212,11 +214,11 @@ __device__ __forceinline__ void p2coef_body(P2State *__restrict__ ps, KState *__
       if (k < j) x = x - cconj(sH[j][k]);
       w[0][k] = x;
     }
-    if (t == 0) bb[0][0] = bb[0][1] = bb[0][2] = bb[0][3] = {0.0, 0.0};
+    if (t == 0) bb[0][0] = bb[0][1] = bb[0][2] = bb[0][3] = bb[0][4] = {0.0, 0.0};
     if (t == 0) bb[0][1] = cjj;
     __syncthreads();
-    cplx *adst[3] = {ps->aX, ps->aZ, ps->aY};
-    cplx *bdst[3] = {&ps->bX1, &ps->bZ1, &ps->bY1};
+    cplx *adst[4] = {ps->aX, ps->aZ, ps->aY, ps->aW};
+    cplx *bdst[4] = {&ps->bX1, &ps->bZ1, &ps->bY1, ps->bW};
     for (int i = 0; i < nsn; ++i) {
       const int cu = i & 1, nx = cu ^ 1;
       // S-basis coefficients a_i = C w_i
@@ -237,7 +239,7 @@ __device__ __forceinline__ void p2coef_body(P2State *__restrict__ ps, KState *__
         if (t == 0) {
           bb[nx][0] = {0.0, 0.0};
           bb[nx][1] = cmul(w[cu][j], cjj) - sig * bb[cu][1];
-          for (int p = 1; p < 3; ++p) bb[nx][p + 1] = bb[cu][p] - sig * bb[cu][p + 1];
+          for (int p = 1; p < 4; ++p) bb[nx][p + 1] = bb[cu][p] - sig * bb[cu][p + 1];
         }
       }
       __syncthreads();

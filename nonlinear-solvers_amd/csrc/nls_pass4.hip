@@ -1,0 +1,285 @@
+// nls_pass4.hip -- the first basis pass with FOUR new vectors (k_p4d0): from the start
+// vector S_0 alone it writes V_1..V_4 (V_1 = (L - sigma) W_0, V_{i+1} = (L - sigma) V_i as
+// combinations of S_0, L S_0, .., L^4 S_0; coefficients from k_p2coef, P2State aX, aZ, aY,
+// aW and bX1, bZ1..2, bY1..3, bW1..4) and reduces S_0^H V_i, the Gram V_a^H V_b (a <= b)
+// and ||S_0||^2 (the blind start) -- the columns k_p2coef takes for ns = 4 at J = 0.
+// Replaces the J = 0 and J = 2 two-vector passes: the schedule continues with two-vector
+// passes from J = 4, so a step moves 60 instead of 63 vector transfers at m = 16
+// (tests/sstep_model.py sched, tests/test_sstep_model.py: the same Krylov action within
+// 1e-12 at the headline stiffness).  The Lanczos recurrence is the reference's
+// (eigen_krylov_complex.hpp:21-38, device/lanczos_complex.hpp:413-500) in s-step form.
+//
+// 3D isotropic operator (laplacians.hpp:55-105), single-rank handles, nx % 64 == 0,
+// ny % 4 == 0, ny >= 8 (the host checks).  Workgroup = 4 waves = a tile of 64 x-cells x 4
+// rows, marched over the tile's planes.  Per march step the tile takes S_0 plane p (rows
+// y0-4..y0+7, cells x0-4..x0+67: the radius-4 neighbourhood, rows outside [0, ny) wrapped
+// into the adjacent planes exactly as the flat-index y-neighbour of the reference does,
+// cells outside the grid zero) and computes one plane of each stencil level on a shrinking
+// region: L S_0 at plane p-1 (rows/cells of radius 3), L^2 S_0 at p-2 (radius 2), L^3 S_0
+// at p-3 (radius 1), L^4 S_0 at p-4 on the tile; every level lives in a 3-plane LDS ring
+// (120 KiB), level values outside the grid are zero, so each stencil is the plain
+// 7-point form with the reference's diagonal.  S_0 is loaded LA planes ahead into registers
+// (compiler-tracked loads; no hand-counted vmcnt), the outputs of plane p-4 are stored
+// non-temporally.  Barriers: one after each of the four phases per step.
+#include "nls_reduce.hpp"
+#include "nls_kernels.hpp"
+#define NLS_NO_P2_KERNELS
+#include "nls_pass2.hpp"
+
+namespace nls {
+
+#ifndef NLS_P4_LA
+#define NLS_P4_LA 2  // planes of S_0 loaded ahead (registers)
+#endif
+
+namespace p4 {
+constexpr int R = 4;          // stencil radius of the pass (four levels)
+constexpr int TR = 4;         // output rows per tile (one per wave)
+constexpr int XW = 64;        // output cells per row (one per lane)
+constexpr int EH = TR + 2 * R;  // 12 staged rows
+constexpr int EW = XW + 2 * R;  // 72 staged cells per row
+// level l (0 = S_0) covers rows [l, EH - l) and cells [l, EW - l) of the staged grid
+__host__ __device__ constexpr int lw(int l) { return EW - 2 * l; }
+__host__ __device__ constexpr int lh(int l) { return EH - 2 * l; }
+__host__ __device__ constexpr int lsz(int l) { return lw(l) * lh(l); }
+constexpr int OFF1 = 3 * lsz(0), OFF2 = OFF1 + 3 * lsz(1), OFF3 = OFF2 + 3 * lsz(2);
+constexpr int LDS_CPLX = OFF3 + 3 * lsz(3);  // 7512 cplx = 120,192 B
+constexpr int NC = 4 + 10 + 1;                 // S-dots, Gram (a <= b), ||S_0||^2
+// halo positions of level l (its region minus the tile's own 4 x 64 block)
+__host__ __device__ constexpr int nhalo(int l) { return (R - l) * (2 * lw(l) + 2 * TR); }
+static_assert(nhalo(1) == 444 && nhalo(2) == 288 && nhalo(3) == 140, "halo counts");
+}  // namespace p4
+
+// (free functions with value arguments: lambdas capturing the kernel's locals by reference
+// kept the closure on the stack -- scratch accesses in the march loop)
+struct P4C {
+  int nx, ny, nz, x0, y0;
+  double s, sdi, sdb;
+};
+struct P4Cell {
+  int row, pl, x;
+};
+// the grid cell of staged (er, ec) at march plane q: row and plane after the flat-index
+// y-wrap (rows outside [0, ny) belong to the adjacent planes), x
+__device__ __forceinline__ P4Cell p4_cell(const P4C c, int er, int ec, int q) {
+  const int yy = c.y0 - p4::R + er;
+  P4Cell r;
+  r.pl = q + (yy < 0 ? -1 : (yy >= c.ny ? 1 : 0));
+  r.row = yy < 0 ? yy + c.ny : (yy >= c.ny ? yy - c.ny : yy);
+  r.x = c.x0 - p4::R + ec;
+  return r;
+}
+// level-l value at staged (er, ec), plane q, from level l-1's ring slots (planes q-1, q, q+1):
+// the reference's 7-point row (laplacians.hpp:69-102), zero outside the grid
+__device__ __forceinline__ cplx p4_lap(const P4C c, const cplx *sm, const cplx *sc, const cplx *sp, int l, int er,
+                                       int ec, int q) {
+  const int ws = p4::lw(l - 1);
+  const int i = (er - (l - 1)) * ws + (ec - (l - 1));
+  const cplx v0 = sc[i], xm = sc[i - 1], xp = sc[i + 1], ym = sc[i - ws], yp = sc[i + ws];
+  const cplx zm = sm[i], zp = sp[i];
+  const P4Cell e = p4_cell(c, er, ec, q);
+  const bool in = e.x >= 0 && e.x < c.nx && e.pl >= 0 && e.pl < c.nz;
+  const bool bnd = e.x == 0 || e.x == c.nx - 1 || e.row == 0 || e.row == c.ny - 1 || e.pl == 0 || e.pl == c.nz - 1;
+  const cplx v = (bnd ? c.sdb : c.sdi) * v0 + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
+  return in ? v : cplx{0.0, 0.0};
+}
+struct P4Pos {
+  int er, ec;
+};
+// the staged (er, ec) of halo position h of level l: rows above the tile, rows below, then
+// the side cells of the tile's own rows
+__device__ __forceinline__ P4Pos p4_halo(int l, int h) {
+  using namespace p4;
+  const int d = R - l, wl = lw(l);
+  P4Pos r;
+  if (h < d * wl) {
+    r.er = l + h / wl;
+    r.ec = l + h % wl;
+  } else if (h < 2 * d * wl) {
+    const int h2 = h - d * wl;
+    r.er = R + TR + h2 / wl;
+    r.ec = l + h2 % wl;
+  } else {
+    const int h2 = h - 2 * d * wl;
+    r.er = R + h2 / (2 * d);
+    const int cc = h2 % (2 * d);
+    r.ec = cc < d ? l + cc : R + XW + (cc - d);
+  }
+  return r;
+}
+struct P4Ld {
+  cplx m[3], h;
+};
+// S_0 loads of plane p: staged rows w, w+4, w+8 at cells x0..x0+63 (one aligned 1 KiB row
+// per wave-load; row w+4 is the thread's own cell), on threads 0..95 the x-halo cell
+// (hr, hec) of row hr = t/8
+__device__ __forceinline__ P4Ld p4_load(const P4C c, const cplx *__restrict__ S0, int64_t P, int w, int lane, int t,
+                                        int hr, int hec, int p) {
+  P4Ld r;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const P4Cell e = p4_cell(c, w + 4 * j, p4::R + lane, p);
+    const bool ok = e.pl >= 0 && e.pl < c.nz;
+    r.m[j] = ok ? ld_nt(S0 + (int64_t)e.pl * P + (int64_t)e.row * c.nx + e.x) : cplx{0.0, 0.0};
+  }
+  r.h = {0.0, 0.0};
+  if (t < p4::EH * 2 * p4::R) {
+    const P4Cell e = p4_cell(c, hr, hec, p);
+    if (e.pl >= 0 && e.pl < c.nz && e.x >= 0 && e.x < c.nx) r.h = S0[(int64_t)e.pl * P + (int64_t)e.row * c.nx + e.x];
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int64_t vs, Geo g,
+                                                      const P2State *__restrict__ ps,
+                                                      cplx *__restrict__ part, int nb) {
+  using namespace p4;
+  __shared__ __attribute__((aligned(16))) cplx smem[LDS_CPLX];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nx = (int)g.nx, ny = (int)g.nyp, nz = (int)g.npl;
+  const int64_t P = g.P;
+  const int ntx = nx / XW, nty = ny / TR;
+  const int b = blockIdx.x;
+  const int xt = b % ntx, yt = (b / ntx) % nty, zc = b / (ntx * nty);
+  const int x0 = xt * XW, y0 = yt * TR;
+  const int k0 = g.qa + zc * g.kz, k1 = min(k0 + g.kz, g.qb);
+  const double s = g.s, sdi = g.sd_in, sdb = g.sd_bd;
+  // coefficients: V_i = a_i S_0 + sum_{q <= i} b_i[q] L^q S_0
+  const cplx a1 = ps->aX[0], a2 = ps->aZ[0], a3 = ps->aY[0], a4 = ps->aW[0];
+  const cplx b11 = ps->bX1, b21 = ps->bZ1, b22 = ps->bZ2, b31 = ps->bY1, b32 = ps->bY2, b33 = ps->bY3;
+  const cplx b41 = ps->bW[0], b42 = ps->bW[1], b43 = ps->bW[2], b44 = ps->bW[3];
+
+  const P4C cx{nx, ny, nz, x0, y0, s, sdi, sdb};
+  const cplx *__restrict__ S0 = W;
+  const int hr = t >> 3, hcn = t & 7, hec = hcn < R ? hcn : XW + hcn;
+  cplx acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = {0.0, 0.0};
+  constexpr int LA = NLS_P4_LA;
+  P4Ld la[LA];
+#pragma unroll
+  for (int d = 0; d < LA; ++d) la[d] = p4_load(cx, S0, P, w, lane, t, hr, hec, k0 - R + d);
+  // own-cell queues: S_0 at planes p-4..p, L S_0 at p-4..p-1
+  cplx sown[5], l1own[4];
+#pragma unroll
+  for (int d = 0; d < 5; ++d) sown[d] = {0.0, 0.0};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) l1own[d] = {0.0, 0.0};
+  // ring slot of plane q is (q - base) mod 3 with base = k0 - 8 (the lowest plane any phase
+  // names: the first step's L^3 source plane)
+  const int base = k0 - 2 * R;
+  cplx *const rS = smem, *const r1 = smem + OFF1, *const r2 = smem + OFF2, *const r3 = smem + OFF3;
+#define P4_SLOT(q) (((q) - base) % 3)
+  const int orow = R + w, ocol = R + lane;  // the own cell in the staged grid
+  const int ox = x0 + lane, oy = y0 + w;
+
+  for (int p = k0 - R; p < k1 + R; ++p) {
+    // 1. S_0 plane p into its ring slot; the load of plane p + LA
+    const P4Ld cur = la[0];
+#pragma unroll
+    for (int d = 0; d + 1 < LA; ++d) la[d] = la[d + 1];
+    if (p + LA < k1 + R) la[LA - 1] = p4_load(cx, S0, P, w, lane, t, hr, hec, p + LA);  // (uniform)
+    {
+      cplx *dS = rS + P4_SLOT(p) * lsz(0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dS[(w + 4 * j) * EW + R + lane] = cur.m[j];
+      if (t < EH * 2 * R) dS[hr * EW + hec] = cur.h;
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) sown[d] = sown[d + 1];
+    sown[4] = cur.m[1];
+    __syncthreads();
+    // 2. L S_0 at plane p-1
+    {
+      const int q = p - 1;
+      const cplx *sm = rS + P4_SLOT(q - 1) * lsz(0), *sc = rS + P4_SLOT(q) * lsz(0), *sp = rS + P4_SLOT(q + 1) * lsz(0);
+      cplx *d1 = r1 + P4_SLOT(q) * lsz(1);
+      const cplx own = p4_lap(cx, sm, sc, sp, 1, orow, ocol, q);
+      d1[(orow - 1) * lw(1) + (ocol - 1)] = own;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) l1own[d] = l1own[d + 1];
+      l1own[3] = own;
+      for (int h = t; h < nhalo(1); h += NTHREADS) {
+        const P4Pos e = p4_halo(1, h);
+        d1[(e.er - 1) * lw(1) + (e.ec - 1)] = p4_lap(cx, sm, sc, sp, 1, e.er, e.ec, q);
+      }
+    }
+    __syncthreads();
+    // 3. L^2 S_0 at plane p-2
+    {
+      const int q = p - 2;
+      const cplx *sm = r1 + P4_SLOT(q - 1) * lsz(1), *sc = r1 + P4_SLOT(q) * lsz(1), *sp = r1 + P4_SLOT(q + 1) * lsz(1);
+      cplx *d2 = r2 + P4_SLOT(q) * lsz(2);
+      d2[(orow - 2) * lw(2) + (ocol - 2)] = p4_lap(cx, sm, sc, sp, 2, orow, ocol, q);
+      for (int h = t; h < nhalo(2); h += NTHREADS) {
+        const P4Pos e = p4_halo(2, h);
+        d2[(e.er - 2) * lw(2) + (e.ec - 2)] = p4_lap(cx, sm, sc, sp, 2, e.er, e.ec, q);
+      }
+    }
+    __syncthreads();
+    // 4. L^3 S_0 at plane p-3
+    {
+      const int q = p - 3;
+      const cplx *sm = r2 + P4_SLOT(q - 1) * lsz(2), *sc = r2 + P4_SLOT(q) * lsz(2), *sp = r2 + P4_SLOT(q + 1) * lsz(2);
+      cplx *d3 = r3 + P4_SLOT(q) * lsz(3);
+      d3[(orow - 3) * lw(3) + (ocol - 3)] = p4_lap(cx, sm, sc, sp, 3, orow, ocol, q);
+      if (t < nhalo(3)) {
+        const P4Pos e = p4_halo(3, t);
+        d3[(e.er - 3) * lw(3) + (e.ec - 3)] = p4_lap(cx, sm, sc, sp, 3, e.er, e.ec, q);
+      }
+    }
+    __syncthreads();
+    // 5. the outputs of plane k = p-4: L^4 S_0 on the tile, V_1..V_4, their sums
+    const int k = p - R;
+    if (k >= k0) {  // uniform
+      const cplx *sm = r3 + P4_SLOT(k - 1) * lsz(3), *sc = r3 + P4_SLOT(k) * lsz(3), *sp = r3 + P4_SLOT(k + 1) * lsz(3);
+      const cplx L4 = p4_lap(cx, sm, sc, sp, 4, orow, ocol, k);
+      const cplx L3 = sc[(orow - 3) * lw(3) + (ocol - 3)];
+      const cplx L2 = r2[P4_SLOT(k) * lsz(2) + (orow - 2) * lw(2) + (ocol - 2)];
+      const cplx L1 = l1own[0], S = sown[0];
+      const cplx V1 = cmul(a1, S) + cmul(b11, L1);
+      const cplx V2 = (cmul(a2, S) + cmul(b21, L1)) + cmul(b22, L2);
+      const cplx V3 = (cmul(a3, S) + cmul(b31, L1)) + (cmul(b32, L2) + cmul(b33, L3));
+      const cplx V4 = ((cmul(a4, S) + cmul(b41, L1)) + (cmul(b42, L2) + cmul(b43, L3))) + cmul(b44, L4);
+      const int64_t o = (int64_t)k * P + (int64_t)oy * nx + ox;
+      st_nt(W + vs + o, V1);
+      st_nt(W + 2 * vs + o, V2);
+      st_nt(W + 3 * vs + o, V3);
+      st_nt(W + 4 * vs + o, V4);
+      const cplx V[4] = {V1, V2, V3, V4};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] += cj_mul(S, V[i]);
+      int c = 4;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        acc[c].re += abs2(V[a]);
+        ++c;
+#pragma unroll
+        for (int bb = a + 1; bb < 4; ++bb) acc[c++] += cj_mul(V[a], V[bb]);
+      }
+      acc[NC - 1].re += abs2(S);
+    }
+  }
+  // partial sums per workgroup (the staged rings are free after this barrier)
+  __syncthreads();
+  cplx *red = smem;  // [4][NC]
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const double a = wave_sum(acc[c].re), bb = wave_sum(acc[c].im);
+    if (lane == 0) red[w * NC + c] = {a, bb};
+  }
+  __syncthreads();
+  for (int c = t; c < NC; c += NTHREADS) {
+    cplx v = red[c];
+#pragma unroll
+    for (int q = 1; q < TR; ++q) v += red[q * NC + c];
+    part[(int64_t)c * nb + blockIdx.x] = v;
+  }
+}
+
+const void *kernel_pass4() { return reinterpret_cast<const void *>(&k_p4d0); }
+int pass4_tiles(int64_t nx, int64_t ny, int64_t planes, int kz) {
+  return (int)((nx / p4::XW) * (ny / p4::TR) * ((planes + kz - 1) / kz));
+}
+
+}  // namespace nls
