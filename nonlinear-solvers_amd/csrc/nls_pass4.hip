@@ -28,6 +28,9 @@
 
 namespace nls {
 
+#ifndef NLS_P4_NT
+#define NLS_P4_NT 512  // threads per workgroup: 4 output waves (+ 4 waves that take halo positions)
+#endif
 #ifndef NLS_P4_LA
 #define NLS_P4_LA 2  // planes of S_0 loaded ahead (registers)
 #endif
@@ -69,17 +72,34 @@ __device__ __forceinline__ P4Cell p4_cell(const P4C c, int er, int ec, int q) {
   r.x = c.x0 - p4::R + ec;
   return r;
 }
-// level-l value at staged (er, ec), plane q, from level l-1's ring slots (planes q-1, q, q+1):
-// the reference's 7-point row (laplacians.hpp:69-102), zero outside the grid
-__device__ __forceinline__ cplx p4_lap(const P4C c, const cplx *sm, const cplx *sc, const cplx *sp, int l, int er,
-                                       int ec, int q) {
-  const int ws = p4::lw(l - 1);
-  const int i = (er - (l - 1)) * ws + (ec - (l - 1));
-  const cplx v0 = sc[i], xm = sc[i - 1], xp = sc[i + 1], ym = sc[i - ws], yp = sc[i + ws];
+// a stencil position of level l, resolved once per tile (the plane-independent parts):
+// source index in level l-1's buffer, destination index in level l's, the plane shift of
+// the y-wrap, x inside the grid, x or row on the grid boundary
+struct P4Pt {
+  int src, dst, dpl;
+  bool xin, bfix;
+};
+__device__ __forceinline__ P4Pt p4_pt(const P4C c, int l, int er, int ec) {
+  P4Pt r;
+  r.src = (er - (l - 1)) * p4::lw(l - 1) + (ec - (l - 1));
+  r.dst = (er - l) * p4::lw(l) + (ec - l);
+  const P4Cell e = p4_cell(c, er, ec, 0);
+  r.dpl = e.pl;
+  r.xin = e.x >= 0 && e.x < c.nx;
+  r.bfix = e.x == 0 || e.x == c.nx - 1 || e.row == 0 || e.row == c.ny - 1;
+  return r;
+}
+// the stencil at a resolved position, plane q: the reference's 7-point row
+// (laplacians.hpp:69-102) from level l-1's ring slots (planes q-1, q, q+1), zero outside the grid
+template <int WS>
+__device__ __forceinline__ cplx p4_lapt(const P4C c, const cplx *sm, const cplx *sc, const cplx *sp, const P4Pt e,
+                                        int q) {
+  const int i = e.src;
+  const cplx v0 = sc[i], xm = sc[i - 1], xp = sc[i + 1], ym = sc[i - WS], yp = sc[i + WS];
   const cplx zm = sm[i], zp = sp[i];
-  const P4Cell e = p4_cell(c, er, ec, q);
-  const bool in = e.x >= 0 && e.x < c.nx && e.pl >= 0 && e.pl < c.nz;
-  const bool bnd = e.x == 0 || e.x == c.nx - 1 || e.row == 0 || e.row == c.ny - 1 || e.pl == 0 || e.pl == c.nz - 1;
+  const int pl = q + e.dpl;
+  const bool in = e.xin && pl >= 0 && pl < c.nz;
+  const bool bnd = e.bfix || pl == 0 || pl == c.nz - 1;
   const cplx v = (bnd ? c.sdb : c.sdi) * v0 + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
   return in ? v : cplx{0.0, 0.0};
 }
@@ -111,31 +131,36 @@ struct P4Ld {
   cplx m[3], h;
 };
 // S_0 loads of plane p: staged rows w, w+4, w+8 at cells x0..x0+63 (one aligned 1 KiB row
-// per wave-load; row w+4 is the thread's own cell), on threads 0..95 the x-halo cell
-// (hr, hec) of row hr = t/8
-__device__ __forceinline__ P4Ld p4_load(const P4C c, const cplx *__restrict__ S0, int64_t P, int w, int lane, int t,
-                                        int hr, int hec, int p) {
+// per wave-load; row w+4 is the thread's own cell; output waves only), on halo-load
+// threads ht < 96 the x-halo cell (hr, hec) of row hr = ht/8
+__device__ __forceinline__ P4Ld p4_load(const P4C c, const cplx *__restrict__ S0, int64_t P, bool mains, int w,
+                                        int lane, int ht, int hr, int hec, int p) {
   P4Ld r;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const P4Cell e = p4_cell(c, w + 4 * j, p4::R + lane, p);
-    const bool ok = e.pl >= 0 && e.pl < c.nz;
+    const bool ok = mains && e.pl >= 0 && e.pl < c.nz;
     r.m[j] = ok ? ld_nt(S0 + (int64_t)e.pl * P + (int64_t)e.row * c.nx + e.x) : cplx{0.0, 0.0};
   }
   r.h = {0.0, 0.0};
-  if (t < p4::EH * 2 * p4::R) {
+  if (ht < p4::EH * 2 * p4::R) {
     const P4Cell e = p4_cell(c, hr, hec, p);
     if (e.pl >= 0 && e.pl < c.nz && e.x >= 0 && e.x < c.nx) r.h = S0[(int64_t)e.pl * P + (int64_t)e.row * c.nx + e.x];
   }
   return r;
 }
 
-__global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int64_t vs, Geo g,
+// NT = 256: the four output waves do every position; NT = 512: four more waves take the halo
+// positions of each level (at most two stencils per thread and level)
+template <int NT>
+__global__ __launch_bounds__(NT, 1) void k_p4d0(cplx *__restrict__ W, int64_t vs, Geo g,
                                                       const P2State *__restrict__ ps,
                                                       cplx *__restrict__ part, int nb) {
   using namespace p4;
   __shared__ __attribute__((aligned(16))) cplx smem[LDS_CPLX];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const bool outw = t < NTHREADS;         // the tile's output waves (uniform per wave)
+  const int h0 = (t + NTHREADS) % NT;    // first halo position of this thread
   const int nx = (int)g.nx, ny = (int)g.nyp, nz = (int)g.npl;
   const int64_t P = g.P;
   const int ntx = nx / XW, nty = ny / TR;
@@ -151,14 +176,15 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int6
 
   const P4C cx{nx, ny, nz, x0, y0, s, sdi, sdb};
   const cplx *__restrict__ S0 = W;
-  const int hr = t >> 3, hcn = t & 7, hec = hcn < R ? hcn : XW + hcn;
+  const int ht = h0;  // halo-load index: the helper waves' threads first when NT = 512
+  const int hr = ht >> 3, hcn = ht & 7, hec = hcn < R ? hcn : XW + hcn;
   cplx acc[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) acc[c] = {0.0, 0.0};
   constexpr int LA = NLS_P4_LA;
   P4Ld la[LA];
 #pragma unroll
-  for (int d = 0; d < LA; ++d) la[d] = p4_load(cx, S0, P, w, lane, t, hr, hec, k0 - R + d);
+  for (int d = 0; d < LA; ++d) la[d] = p4_load(cx, S0, P, outw, w & 3, lane, ht, hr, hec, k0 - R + d);
   // own-cell queues: S_0 at planes p-4..p, L S_0 at p-4..p-1
   cplx sown[5], l1own[4];
 #pragma unroll
@@ -172,18 +198,45 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int6
 #define P4_SLOT(q) (((q) - base) % 3)
   const int orow = R + w, ocol = R + lane;  // the own cell in the staged grid
   const int ox = x0 + lane, oy = y0 + w;
+  // resolved positions: the own cell at each level, this thread's halo position of levels
+  // 1..3 (NT = 512: at most one per level)
+  static_assert(NT == 512 || NT == 256, "workgroup size");
+  constexpr int NH1 = (nhalo(1) + NT - 1) / NT, NH2 = (nhalo(2) + NT - 1) / NT, NH3 = (nhalo(3) + NT - 1) / NT;
+  P4Pt po[4], ph1[NH1], ph2[NH2], ph3[NH3];
+#pragma unroll
+  for (int l = 1; l <= 4; ++l) po[l - 1] = p4_pt(cx, l, orow, ocol);
+#pragma unroll
+  for (int u = 0; u < NH1; ++u) {
+    const int h = h0 + u * NT;
+    const P4Pos e = p4_halo(1, h < nhalo(1) ? h : 0);
+    ph1[u] = p4_pt(cx, 1, e.er, e.ec);
+  }
+#pragma unroll
+  for (int u = 0; u < NH2; ++u) {
+    const int h = h0 + u * NT;
+    const P4Pos e = p4_halo(2, h < nhalo(2) ? h : 0);
+    ph2[u] = p4_pt(cx, 2, e.er, e.ec);
+  }
+#pragma unroll
+  for (int u = 0; u < NH3; ++u) {
+    const int h = h0 + u * NT;
+    const P4Pos e = p4_halo(3, h < nhalo(3) ? h : 0);
+    ph3[u] = p4_pt(cx, 3, e.er, e.ec);
+  }
 
   for (int p = k0 - R; p < k1 + R; ++p) {
     // 1. S_0 plane p into its ring slot; the load of plane p + LA
     const P4Ld cur = la[0];
 #pragma unroll
     for (int d = 0; d + 1 < LA; ++d) la[d] = la[d + 1];
-    if (p + LA < k1 + R) la[LA - 1] = p4_load(cx, S0, P, w, lane, t, hr, hec, p + LA);  // (uniform)
+    if (p + LA < k1 + R) la[LA - 1] = p4_load(cx, S0, P, outw, w & 3, lane, ht, hr, hec, p + LA);  // (uniform)
     {
       cplx *dS = rS + P4_SLOT(p) * lsz(0);
+      if (outw) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) dS[(w + 4 * j) * EW + R + lane] = cur.m[j];
-      if (t < EH * 2 * R) dS[hr * EW + hec] = cur.h;
+        for (int j = 0; j < 3; ++j) dS[(w + 4 * j) * EW + R + lane] = cur.m[j];
+      }
+      if (ht < EH * 2 * R) dS[hr * EW + hec] = cur.h;
     }
 #pragma unroll
     for (int d = 0; d < 4; ++d) sown[d] = sown[d + 1];
@@ -194,15 +247,16 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int6
       const int q = p - 1;
       const cplx *sm = rS + P4_SLOT(q - 1) * lsz(0), *sc = rS + P4_SLOT(q) * lsz(0), *sp = rS + P4_SLOT(q + 1) * lsz(0);
       cplx *d1 = r1 + P4_SLOT(q) * lsz(1);
-      const cplx own = p4_lap(cx, sm, sc, sp, 1, orow, ocol, q);
-      d1[(orow - 1) * lw(1) + (ocol - 1)] = own;
+      if (outw) {
+        const cplx own = p4_lapt<lw(0)>(cx, sm, sc, sp, po[0], q);
+        d1[po[0].dst] = own;
 #pragma unroll
-      for (int d = 0; d < 3; ++d) l1own[d] = l1own[d + 1];
-      l1own[3] = own;
-      for (int h = t; h < nhalo(1); h += NTHREADS) {
-        const P4Pos e = p4_halo(1, h);
-        d1[(e.er - 1) * lw(1) + (e.ec - 1)] = p4_lap(cx, sm, sc, sp, 1, e.er, e.ec, q);
+        for (int d = 0; d < 3; ++d) l1own[d] = l1own[d + 1];
+        l1own[3] = own;
       }
+#pragma unroll
+      for (int u = 0; u < NH1; ++u)
+        if (h0 + u * NT < nhalo(1)) d1[ph1[u].dst] = p4_lapt<lw(0)>(cx, sm, sc, sp, ph1[u], q);
     }
     __syncthreads();
     // 3. L^2 S_0 at plane p-2
@@ -210,11 +264,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int6
       const int q = p - 2;
       const cplx *sm = r1 + P4_SLOT(q - 1) * lsz(1), *sc = r1 + P4_SLOT(q) * lsz(1), *sp = r1 + P4_SLOT(q + 1) * lsz(1);
       cplx *d2 = r2 + P4_SLOT(q) * lsz(2);
-      d2[(orow - 2) * lw(2) + (ocol - 2)] = p4_lap(cx, sm, sc, sp, 2, orow, ocol, q);
-      for (int h = t; h < nhalo(2); h += NTHREADS) {
-        const P4Pos e = p4_halo(2, h);
-        d2[(e.er - 2) * lw(2) + (e.ec - 2)] = p4_lap(cx, sm, sc, sp, 2, e.er, e.ec, q);
-      }
+      if (outw) d2[po[1].dst] = p4_lapt<lw(1)>(cx, sm, sc, sp, po[1], q);
+#pragma unroll
+      for (int u = 0; u < NH2; ++u)
+        if (h0 + u * NT < nhalo(2)) d2[ph2[u].dst] = p4_lapt<lw(1)>(cx, sm, sc, sp, ph2[u], q);
     }
     __syncthreads();
     // 4. L^3 S_0 at plane p-3
@@ -222,20 +275,19 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int6
       const int q = p - 3;
       const cplx *sm = r2 + P4_SLOT(q - 1) * lsz(2), *sc = r2 + P4_SLOT(q) * lsz(2), *sp = r2 + P4_SLOT(q + 1) * lsz(2);
       cplx *d3 = r3 + P4_SLOT(q) * lsz(3);
-      d3[(orow - 3) * lw(3) + (ocol - 3)] = p4_lap(cx, sm, sc, sp, 3, orow, ocol, q);
-      if (t < nhalo(3)) {
-        const P4Pos e = p4_halo(3, t);
-        d3[(e.er - 3) * lw(3) + (e.ec - 3)] = p4_lap(cx, sm, sc, sp, 3, e.er, e.ec, q);
-      }
+      if (outw) d3[po[2].dst] = p4_lapt<lw(2)>(cx, sm, sc, sp, po[2], q);
+#pragma unroll
+      for (int u = 0; u < NH3; ++u)
+        if (h0 + u * NT < nhalo(3)) d3[ph3[u].dst] = p4_lapt<lw(2)>(cx, sm, sc, sp, ph3[u], q);
     }
     __syncthreads();
     // 5. the outputs of plane k = p-4: L^4 S_0 on the tile, V_1..V_4, their sums
     const int k = p - R;
-    if (k >= k0) {  // uniform
+    if (k >= k0 && outw) {  // uniform
       const cplx *sm = r3 + P4_SLOT(k - 1) * lsz(3), *sc = r3 + P4_SLOT(k) * lsz(3), *sp = r3 + P4_SLOT(k + 1) * lsz(3);
-      const cplx L4 = p4_lap(cx, sm, sc, sp, 4, orow, ocol, k);
-      const cplx L3 = sc[(orow - 3) * lw(3) + (ocol - 3)];
-      const cplx L2 = r2[P4_SLOT(k) * lsz(2) + (orow - 2) * lw(2) + (ocol - 2)];
+      const cplx L4 = p4_lapt<lw(3)>(cx, sm, sc, sp, po[3], k);
+      const cplx L3 = sc[po[2].dst];
+      const cplx L2 = r2[P4_SLOT(k) * lsz(2) + po[1].dst];
       const cplx L1 = l1own[0], S = sown[0];
       const cplx V1 = cmul(a1, S) + cmul(b11, L1);
       const cplx V2 = (cmul(a2, S) + cmul(b21, L1)) + cmul(b22, L2);
@@ -266,10 +318,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int6
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const double a = wave_sum(acc[c].re), bb = wave_sum(acc[c].im);
-    if (lane == 0) red[w * NC + c] = {a, bb};
+    if (lane == 0 && outw) red[w * NC + c] = {a, bb};
   }
   __syncthreads();
-  for (int c = t; c < NC; c += NTHREADS) {
+  for (int c = t; c < NC; c += NT) {
     cplx v = red[c];
 #pragma unroll
     for (int q = 1; q < TR; ++q) v += red[q * NC + c];
@@ -277,7 +329,8 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_p4d0(cplx *__restrict__ W, int6
   }
 }
 
-const void *kernel_pass4() { return reinterpret_cast<const void *>(&k_p4d0); }
+const void *kernel_pass4() { return reinterpret_cast<const void *>(&k_p4d0<NLS_P4_NT>); }
+int pass4_threads() { return NLS_P4_NT; }
 int pass4_tiles(int64_t nx, int64_t ny, int64_t planes, int kz) {
   return (int)((nx / p4::XW) * (ny / p4::TR) * ((planes + kz - 1) / kz));
 }
