@@ -77,3 +77,27 @@ def test_register_row_kinds():
             assert s.waits(J, 2, 0) == s.waits(J, 2, 3)
         else:  # 3D register rows, 2D J ring
             assert s.np(J, 0) == 0 and s.np(J, 3) >= 1
+
+
+def test_new_round6_kernels_have_no_scratch(tmp_path):
+    """The round-6 kernels (the fused column-sum + coefficient launch, the fused basis end,
+    the four-vector first pass) keep everything in registers and LDS: no VGPR spill, no
+    scratch instruction, and no private segment beyond the call frame of the eigensolve
+    (k_tail_chain calls eigen_phase_jacobi, __noinline__, exactly as k_reduce_final does)."""
+    want = ("k_colsum_p2coef", "k_tail_chain", "k_p4d0")
+    seen = set()
+    for co in C.gfx950_objects(LIB, str(tmp_path)):
+        md = C.metadata(co)
+        funcs = C.disassemble(co)
+        frame = [int(v.get("private_segment_fixed_size", "0")) for n, v in md.items() if "k_reduce_final" in n]
+        for name, ins in funcs.items():
+            hit = [w for w in want if w in name]
+            if not hit:
+                continue
+            seen.add(hit[0])
+            meta = md.get(name, {})
+            allowed = max(frame) if hit[0] == "k_tail_chain" and frame else 0
+            assert int(meta.get("private_segment_fixed_size", "0")) <= allowed, name
+            assert str(meta.get("vgpr_spill_count", "0")) == "0", name
+            assert not [m for _a, m, _o in ins if m.startswith("scratch_")], name
+    assert seen == set(want)
