@@ -68,6 +68,13 @@ __host__ __device__ constexpr int p2d_kind(int A) { return A == 3 ? 0 : A; }
 __host__ __device__ constexpr int p2d_csb(int A) {
   return p2d_kind(A) == 2 ? P2D_SR * P2D_SRB : (p2d_kind(A) ? P2D_CSB : 0);
 }
+// Timing diagnostic only (wrong results; never a product build): the S ring takes its halo
+// from the zero row instead of the grid -- bit 1 the x-halo cells, bit 2 the rows above and
+// below the tile -- so a variant library shows what the stencil vector's halo costs a pass
+// (profiles/r06/p2_halo_diag.txt)
+#ifndef NLS_DIAG_P2HALO
+#define NLS_DIAG_P2HALO 0
+#endif
 #ifndef NLS_P2D_OCC2_MAXJ
 #define NLS_P2D_OCC2_MAXJ 6   // two workgroups per CU up to this J (J = 6: late J ring, 512^3 4.08 -> 3.64 ms; J = 8 no gain)
 #endif
@@ -594,12 +601,15 @@ __global__ __launch_bounds__(NTHREADS, p2d_occ(J, A ? (PR ? 2 : 1) : (D2 ? 3 : 0
     char *dst_ = smem + ((sl) * P2D_SR + 2 * w) * P2D_SRB;                              \
     _Pragma("unroll") for (int r_ = 0; r_ < 2; ++r_) {                                  \
       /* the row inside the grid and the allocation and needed (s_lo / s_hi) */       \
-      const bool ok_ = p_ >= (r_ ? s_lo1 : s_lo0) && p_ <= (r_ ? s_hi1 : s_hi0);        \
+      const bool ok_ = p_ >= (r_ ? s_lo1 : s_lo0) && p_ <= (r_ ? s_hi1 : s_hi0) &&       \
+                       !((NLS_DIAG_P2HALO & 2) && (w == 0 || w == 3));                  \
       const int64_t o_ = pb_ + (r_ ? s_yo1 : s_yo0);                                    \
       const char *b_ = ok_ ? SJb + o_ : reinterpret_cast<const char *>(zbuf);           \
       asm volatile("" : "+s"(b_)); /* one select, not a DMA per branch */               \
       dma16(b_, xoff, dst_ + r_ * P2D_SRB, 0);                                          \
-      if (lane < 16) dma4(b_, hoff, dst_ + r_ * P2D_SRB + 1024);                        \
+      if (lane < 16)                                                                    \
+        dma4((NLS_DIAG_P2HALO & 1) ? reinterpret_cast<const char *>(zbuf) : b_,         \
+             (NLS_DIAG_P2HALO & 1) ? (uint32_t)(lane & 3) * 4u : hoff, dst_ + r_ * P2D_SRB + 1024); \
       if constexpr (AK == 2) {                                                          \
         /* cell pairs: the c row of the same S row, staged as S rows are */           \
         char *cd_ = smem + p2d_off_c_ring(J, KA) + ((sl) * P2D_SR + 2 * w + r_) * P2D_SRB; \
