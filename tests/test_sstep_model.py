@@ -117,3 +117,25 @@ def test_four_vector_first_pass_matches_oracle(n, dx, kind):
     sched = [(0, 4), (4, 2), (6, 2), (8, 2), (10, 2), (12, 2)]
     got, _ = sm.krylov_s_tail(ap, u, -1e-3j, m, np_ref.F_EXP_ABS, sched=sched)
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) <= 1e-12
+
+
+@pytest.mark.parametrize("n,dx,kind,tol", [(16, 20 / 511, "smooth", 1e-13), (16, 20 / 511, "noise", 1e-13),
+                                           (12, 20 / 1023, "noise", 5e-12), (12, 0.5, "noise", 1e-13)])
+def test_four_vector_passes_at_every_j_match_oracle(n, dx, kind, tol):
+    """The schedule a general four-vector pass would run: four new
+    vectors at J = 0, 4, 8 and two at J = 12 -- 42 instead of 63 pass transfers at m = 16.
+    At the headline stiffness the fused-tail action stays within 1e-13 of the MGS oracle;
+    at twice it with white noise within 5e-12 (observed 2.2e-12; the two-vector schedule:
+    4.6e-13), far inside the 1e-10 trajectory tolerance."""
+    rng = np.random.default_rng(5)
+    ap = lambda v: np_ref.laplacian_apply(3, n, n, n, dx, dx, v)
+    x = np.linspace(-1, 1, n)
+    Z, Y, X = np.meshgrid(x, x, x, indexing="ij")
+    amp = 1e-3 if kind == "smooth" else 1.0
+    u = (np.exp(-4 * (X * X + Y * Y + Z * Z)) * (1 + 0.2j) + amp * rng.standard_normal(X.shape)).ravel()
+    m = 16
+    ref = np_ref.krylov(ap, u, -1e-3j, m, np_ref.F_EXP_ABS)
+    sched = [(0, 4), (4, 4), (8, 4), (12, 2)]
+    assert sum(J + ns + 1 for J, ns in sched) == 42  # reads S_0..S_J, writes ns
+    got, _ = sm.krylov_s_tail(ap, u, -1e-3j, m, np_ref.F_EXP_ABS, sched=sched)
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) <= tol
