@@ -77,9 +77,9 @@ const void *kernel_p2tfin();
 const void *kernel_colsum_p2coef();  // (partU, nbU, dst, cnt, then k_p2coef's arguments)
 const void *kernel_tail_chain();  // (partA, nbA, dst, cnt, ps, st, m, nf, f0, f1, t_re, t_im)
 const void *kernel_p2coef();
-const void *kernel_pass4();  // k_p4d0 (nls_pass4.hip): (W, vs, Geo, P2State*, part, nb)
+const void *kernel_pass4(int64_t ny);  // k_p4r / k_p4d0 (nls_pass4.hip): (W, vs, Geo, P2State*, part, nb)
 int pass4_tiles(int64_t nx, int64_t ny, int64_t planes, int kz);
-int pass4_threads();  // (P2State*, KState*, int J, int mode, int ns, int nsn)
+int pass4_threads(int64_t ny);  // (P2State*, KState*, int J, int mode, int ns, int nsn)
 size_t p2state_bytes();
 size_t p2state_sums_offset();
 size_t p2state_peer_offset();  // P2State::pdn, then pup (2 x p2state_peer_slots() pointers)

@@ -21,6 +21,8 @@
 // 7-point form with the reference's diagonal.  S_0 is loaded LA planes ahead into registers
 // (compiler-tracked loads; no hand-counted vmcnt), the outputs of plane p-4 are stored
 // non-temporally.  Barriers: one after each of the four phases per step.
+// k_p4r (below, NLS_P4_KIND = 2, the default) computes the same vectors and sums with 64 x 8
+// tiles, register z-queues and one barrier per step.
 #include "nls_reduce.hpp"
 #include "nls_kernels.hpp"
 #define NLS_NO_P2_KERNELS
@@ -329,10 +331,253 @@ __global__ __launch_bounds__(NT, 1) void k_p4d0(cplx *__restrict__ W, int64_t vs
   }
 }
 
-const void *kernel_pass4() { return reinterpret_cast<const void *>(&k_p4d0<NLS_P4_NT>); }
-int pass4_threads() { return NLS_P4_NT; }
+// ---- k_p4r: the same pass with each staged column's z-neighbours in registers ----------
+// Workgroup = 8 waves = a tile of 64 x-cells x 8 rows; staged grid 16 rows x 72 cells (the
+// radius-4 neighbourhood).  Wave w OWNS staged rows w and w + 8 at cells x0..x0+63 (lane =
+// x) for every level, and waves 0 and 7 own the 128 x-halo cells (4 each side of every
+// staged row).  The owner of a staged column computes all its levels, so the stencil's z
+// neighbours (the column's previous-level values at planes q-1, q, q+1) are register queues
+// and only the x / y neighbours come from LDS.  Level l is computed at plane p - l in march
+// step p from level l-1's plane p - l, which step p - 1 wrote into the other half of a
+// ping-pong LDS pair: every read of a step names the previous step's half, every write the
+// current one, so ONE barrier per step orders both (k_p4d0: four).  Each wave owns exactly
+// one output row (rows 4..11), whose queues keep S_0 .. L^3 S_0 of plane p - 4 for the
+// combination.  5.8 stencil evaluations per output cell (k_p4d0: 7.4), 4 LDS reads each
+// (k_p4d0: 7); LDS 2 x 4 levels x 16 x 72 cplx = 144 KiB (one workgroup per CU).
+namespace p4r {
+constexpr int R = 4, TR = 8, XW = 64;
+constexpr int EH = TR + 2 * R, EW = XW + 2 * R, LV = EH * EW;  // 16 x 72 staged cells
+constexpr int NT = 512, NW = NT / 64;
+constexpr int NC = 15;
+static_assert(2 * NW == EH, "two staged rows per wave");
+static_assert(2 * 4 * LV * 16 <= 160 * 1024, "LDS");
+__host__ __device__ constexpr bool mem(int l, int r) { return l <= r && r < EH - l; }
+}  // namespace p4r
+
+// an owned staged cell: LDS index, plane shift of the y-wrap, offset of plane 0's cell,
+// x inside the grid, on the x / row boundary (the reference's -5 diagonal)
+struct P4RPos {
+  int i, dpl;
+  int64_t off;
+  bool xin, bfix;
+};
+__device__ __forceinline__ P4RPos p4r_pos(const P4C c, int er, int ec) {
+  const P4Cell e = p4_cell(c, er, ec, 0);
+  P4RPos r;
+  r.i = er * p4r::EW + ec;
+  r.dpl = e.pl;
+  r.off = (int64_t)e.row * c.nx + e.x;
+  r.xin = e.x >= 0 && e.x < c.nx;
+  r.bfix = e.x == 0 || e.x == c.nx - 1 || e.row == 0 || e.row == c.ny - 1;
+  return r;
+}
+__device__ __forceinline__ cplx p4r_load(const P4C c, const cplx *__restrict__ S0, int64_t P, const P4RPos e, int p) {
+  const int pl = p + e.dpl;
+  return e.xin && pl >= 0 && pl < c.nz ? S0[(int64_t)pl * P + e.off] : cplx{0.0, 0.0};
+}
+// the 7-point row (laplacians.hpp:69-102) at an owned cell, plane q: z neighbours and centre
+// from the owner's queue, x / y neighbours from level l-1's LDS plane q; zero outside the grid
+__device__ __forceinline__ cplx p4r_lap(const P4C c, const cplx *prv, const P4RPos e, cplx zp, cplx cc, cplx zm,
+                                        int q) {
+  const int i = e.i;
+  const cplx xm = prv[i - 1], xp = prv[i + 1], ym = prv[i - p4r::EW], yp = prv[i + p4r::EW];
+  const int pl = q + e.dpl;
+  const bool in = e.xin && pl >= 0 && pl < c.nz;
+  const bool bnd = e.bfix || pl == 0 || pl == c.nz - 1;
+  const cplx v = (bnd ? c.sdb : c.sdi) * cc + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
+  return in ? v : cplx{0.0, 0.0};
+}
+template <int D>
+__device__ __forceinline__ void p4r_push(cplx (&q)[D], cplx v) {
+#pragma unroll
+  for (int d = D - 1; d > 0; --d) q[d] = q[d - 1];
+  q[0] = v;
+}
+
+// OUTB: the wave's output row is its second row (waves 0..3) or its first (4..7)
+template <bool OUTB>
+__device__ __forceinline__ void p4r_march(cplx *lds, cplx *__restrict__ W, int64_t vs, const P4C cx, int64_t P,
+                                          int k0, int k1, const P2State *__restrict__ ps, cplx (&acc)[p4r::NC],
+                                          int w, int lane) {
+  using namespace p4r;
+  const int rO = OUTB ? w + NW : w, rN = OUTB ? w : w + NW;  // output row, the other row
+  const P4RPos eO = p4r_pos(cx, rO, R + lane), eN = p4r_pos(cx, rN, R + lane);
+  const bool hon = w == 0 || w == NW - 1;  // x-halo owners (uniform)
+  const int hidx = (w == 0 ? 0 : 64) + lane, rH = hidx >> 3, cH = hidx & 7, ecH = cH < R ? cH : XW + cH;
+  const P4RPos eH = p4r_pos(cx, rH, ecH);
+  bool hm[4];
+  hm[0] = hon;
+#pragma unroll
+  for (int l = 1; l < 4; ++l) hm[l] = hon && mem(l, rH) && l <= ecH && ecH < EW - l;
+  const cplx *__restrict__ S0 = W;
+  const cplx a1 = ps->aX[0], a2 = ps->aZ[0], a3 = ps->aY[0], a4 = ps->aW[0];
+  const cplx b11 = ps->bX1, b21 = ps->bZ1, b22 = ps->bZ2, b31 = ps->bY1, b32 = ps->bY2, b33 = ps->bY3;
+  const cplx b41 = ps->bW[0], b42 = ps->bW[1], b43 = ps->bW[2], b44 = ps->bW[3];
+  const cplx z{0.0, 0.0};
+  // queues, index 0 = newest: output row S_0 at p..p-4, L at p-1..p-4, L^2 at p-2..p-4,
+  // L^3 at p-3..p-5; the other row and the x-halo cells the three planes their next level needs
+  cplx o0[5], o1[4], o2[3], o3[3], n0[3], n1[3], n2[3], h0[3], h1[3], h2[3];
+#pragma unroll
+  for (int d = 0; d < 5; ++d) o0[d] = z;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o1[d] = z;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) o2[d] = o3[d] = n0[d] = n1[d] = n2[d] = h0[d] = h1[d] = h2[d] = z;
+  cplx laO = p4r_load(cx, S0, P, eO, k0 - R), laN = p4r_load(cx, S0, P, eN, k0 - R);
+  cplx laH = hon ? p4r_load(cx, S0, P, eH, k0 - R) : z;
+  for (int p = k0 - R; p < k1 + R; ++p) {
+    const int par = (p - k0) & 1;
+    cplx *const cur = lds + par * 4 * LV;
+    const cplx *const prv = lds + (par ^ 1) * 4 * LV;
+    const cplx sO = laO, sN = laN, sH = laH;
+    if (p + 1 < k1 + R) {  // uniform
+      laO = p4r_load(cx, S0, P, eO, p + 1);
+      laN = p4r_load(cx, S0, P, eN, p + 1);
+      if (hon) laH = p4r_load(cx, S0, P, eH, p + 1);
+    }
+    // level 0: S_0 at plane p
+    p4r_push(o0, sO);
+    cur[eO.i] = sO;
+    p4r_push(n0, sN);
+    cur[eN.i] = sN;
+    if (hon) {
+      p4r_push(h0, sH);
+      cur[eH.i] = sH;
+    }
+    // level 1 at plane p - 1
+    {
+      const int q = p - 1;
+      const cplx *pv = prv;
+      cplx *cv = cur + LV;
+      const cplx v = p4r_lap(cx, pv, eO, o0[0], o0[1], o0[2], q);
+      p4r_push(o1, v);
+      cv[eO.i] = v;
+      cplx vn = z;
+      if (mem(1, rN)) {
+        vn = p4r_lap(cx, pv, eN, n0[0], n0[1], n0[2], q);
+        cv[eN.i] = vn;
+      }
+      p4r_push(n1, vn);
+      if (hon) {
+        cplx vh = z;
+        if (hm[1]) {
+          vh = p4r_lap(cx, pv, eH, h0[0], h0[1], h0[2], q);
+          cv[eH.i] = vh;
+        }
+        p4r_push(h1, vh);
+      }
+    }
+    // level 2 at plane p - 2
+    {
+      const int q = p - 2;
+      const cplx *pv = prv + LV;
+      cplx *cv = cur + 2 * LV;
+      const cplx v = p4r_lap(cx, pv, eO, o1[0], o1[1], o1[2], q);
+      p4r_push(o2, v);
+      cv[eO.i] = v;
+      cplx vn = z;
+      if (mem(2, rN)) {
+        vn = p4r_lap(cx, pv, eN, n1[0], n1[1], n1[2], q);
+        cv[eN.i] = vn;
+      }
+      p4r_push(n2, vn);
+      if (hon) {
+        cplx vh = z;
+        if (hm[2]) {
+          vh = p4r_lap(cx, pv, eH, h1[0], h1[1], h1[2], q);
+          cv[eH.i] = vh;
+        }
+        p4r_push(h2, vh);
+      }
+    }
+    // level 3 at plane p - 3 (only the output row keeps it: its level 4 needs the z pair)
+    {
+      const int q = p - 3;
+      const cplx *pv = prv + 2 * LV;
+      cplx *cv = cur + 3 * LV;
+      const cplx v = p4r_lap(cx, pv, eO, o2[0], o2[1], o2[2], q);
+      p4r_push(o3, v);
+      cv[eO.i] = v;
+      if (mem(3, rN)) cv[eN.i] = p4r_lap(cx, pv, eN, n2[0], n2[1], n2[2], q);
+      if (hm[3]) cv[eH.i] = p4r_lap(cx, pv, eH, h2[0], h2[1], h2[2], q);
+    }
+    // level 4 and the outputs at plane k = p - 4
+    const int k = p - R;
+    if (k >= k0) {  // uniform
+      const cplx L4 = p4r_lap(cx, prv + 3 * LV, eO, o3[0], o3[1], o3[2], k);
+      const cplx S = o0[4], L1 = o1[3], L2 = o2[2], L3 = o3[1];
+      const cplx V1 = cmul(a1, S) + cmul(b11, L1);
+      const cplx V2 = (cmul(a2, S) + cmul(b21, L1)) + cmul(b22, L2);
+      const cplx V3 = (cmul(a3, S) + cmul(b31, L1)) + (cmul(b32, L2) + cmul(b33, L3));
+      const cplx V4 = ((cmul(a4, S) + cmul(b41, L1)) + (cmul(b42, L2) + cmul(b43, L3))) + cmul(b44, L4);
+      const int64_t o = (int64_t)k * P + eO.off;
+      st_nt(W + vs + o, V1);
+      st_nt(W + 2 * vs + o, V2);
+      st_nt(W + 3 * vs + o, V3);
+      st_nt(W + 4 * vs + o, V4);
+      const cplx V[4] = {V1, V2, V3, V4};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] += cj_mul(S, V[i]);
+      int c = 4;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        acc[c].re += abs2(V[a]);
+        ++c;
+#pragma unroll
+        for (int bb = a + 1; bb < 4; ++bb) acc[c++] += cj_mul(V[a], V[bb]);
+      }
+      acc[NC - 1].re += abs2(S);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(p4r::NT, 1) void k_p4r(cplx *__restrict__ W, int64_t vs, Geo g,
+                                                     const P2State *__restrict__ ps, cplx *__restrict__ part,
+                                                     int nb) {
+  using namespace p4r;
+  __shared__ __attribute__((aligned(16))) cplx lds[2 * 4 * LV];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nx = (int)g.nx, ny = (int)g.nyp, nz = (int)g.npl;
+  const int ntx = nx / XW, nty = ny / TR;
+  const int b = blockIdx.x;
+  const int xt = b % ntx, yt = (b / ntx) % nty, zc = b / (ntx * nty);
+  const int k0 = g.qa + zc * g.kz, k1 = min(k0 + g.kz, g.qb);
+  const P4C cx{nx, ny, nz, xt * XW, yt * TR, g.s, g.sd_in, g.sd_bd};
+  cplx acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = {0.0, 0.0};
+  if (w < NW / 2)  // uniform
+    p4r_march<true>(lds, W, vs, cx, g.P, k0, k1, ps, acc, w, lane);
+  else
+    p4r_march<false>(lds, W, vs, cx, g.P, k0, k1, ps, acc, w, lane);
+  // partial sums per workgroup (the march ended on a barrier: the LDS is free)
+  cplx *red = lds;  // [NW][NC]
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const double a = wave_sum(acc[c].re), bb = wave_sum(acc[c].im);
+    if (lane == 0) red[w * NC + c] = {a, bb};
+  }
+  __syncthreads();
+  for (int c = t; c < NC; c += NT) {
+    cplx v = red[c];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) v += red[q * NC + c];
+    part[(int64_t)c * nb + blockIdx.x] = v;
+  }
+}
+
+#ifndef NLS_P4_KIND
+#define NLS_P4_KIND 2  // 2: k_p4r (register z-queues, one barrier per step) where ny % 8 == 0; 1: k_p4d0
+#endif
+// k_p4r takes grids with ny % 8 == 0, k_p4d0 the others (ny % 4 == 0)
+static bool pass4_r(int64_t ny) { return NLS_P4_KIND == 2 && ny % p4r::TR == 0; }
+const void *kernel_pass4(int64_t ny) {
+  return pass4_r(ny) ? reinterpret_cast<const void *>(&k_p4r) : reinterpret_cast<const void *>(&k_p4d0<NLS_P4_NT>);
+}
+int pass4_threads(int64_t ny) { return pass4_r(ny) ? p4r::NT : NLS_P4_NT; }
 int pass4_tiles(int64_t nx, int64_t ny, int64_t planes, int kz) {
-  return (int)((nx / p4::XW) * (ny / p4::TR) * ((planes + kz - 1) / kz));
+  return (int)((nx / p4::XW) * (ny / (pass4_r(ny) ? p4r::TR : p4::TR)) * ((planes + kz - 1) / kz));
 }
 
 }  // namespace nls
