@@ -532,6 +532,7 @@ __device__ __forceinline__ void p4r_march(cplx *lds, cplx *__restrict__ W, int64
   }
 }
 
+
 __global__ __launch_bounds__(p4r::NT, 1) void k_p4r(cplx *__restrict__ W, int64_t vs, Geo g,
                                                      const P2State *__restrict__ ps, cplx *__restrict__ part,
                                                      int nb) {

@@ -1,8 +1,8 @@
 """CPU: the timing-only diagnostic switches are off in the product build.  NLS_DIAG_HALO
 (nls_stencil.hpp) and NLS_DIAG_P2HALO (nls_pass2d.hpp) drop halo loads and give WRONG
 results; they exist only for variant libraries built by tools/build_lib_variant.sh.  The
-experimental NLS_P4 (the four-vector first pass) and the XCD-banded tail queue stay off
-by default too."""
+XCD-banded tail queue stays off by default too; the four-vector first
+pass (NLS_P4, k_p4r) is on by default since round 6 and k_p4r is its kernel."""
 import os
 import re
 
@@ -20,7 +20,8 @@ def _default(path, macro):
 def test_diagnostic_switches_default_off():
     assert _default("nls_stencil.hpp", "NLS_DIAG_HALO") == 0
     assert _default("nls_pass2d.hpp", "NLS_DIAG_P2HALO") == 0
-    assert _default("nls_api.cpp", "NLS_P4") == 0
+    assert _default("nls_api.cpp", "NLS_P4") == 1
+    assert _default("nls_pass4.hip", "NLS_P4_KIND") == 2
     assert _default("nls_common.hpp", "NLS_TQ_XCD") == 0
 
 
