@@ -376,16 +376,24 @@ __device__ __forceinline__ cplx p4r_load(const P4C c, const cplx *__restrict__ S
   return e.xin && pl >= 0 && pl < c.nz ? S0[(int64_t)pl * P + e.off] : cplx{0.0, 0.0};
 }
 // the 7-point row (laplacians.hpp:69-102) at an owned cell, plane q: z neighbours and centre
-// from the owner's queue, x / y neighbours from level l-1's LDS plane q; zero outside the grid
+// from the owner's queue, x / y neighbours from level l-1's LDS plane q; zero outside the grid.
+// MODE 0: any plane; 1: a plane neither outside the grid nor on its z boundary and a cell
+// inside the grid in x (the owned rows' cells: x0..x0+63) -- the same value without the
+// checks
+template <int MODE>
 __device__ __forceinline__ cplx p4r_lap(const P4C c, const cplx *prv, const P4RPos e, cplx zp, cplx cc, cplx zm,
                                         int q) {
   const int i = e.i;
   const cplx xm = prv[i - 1], xp = prv[i + 1], ym = prv[i - p4r::EW], yp = prv[i + p4r::EW];
-  const int pl = q + e.dpl;
-  const bool in = e.xin && pl >= 0 && pl < c.nz;
-  const bool bnd = e.bfix || pl == 0 || pl == c.nz - 1;
-  const cplx v = (bnd ? c.sdb : c.sdi) * cc + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
-  return in ? v : cplx{0.0, 0.0};
+  if constexpr (MODE == 0) {
+    const int pl = q + e.dpl;
+    const bool in = e.xin && pl >= 0 && pl < c.nz;
+    const bool bnd = e.bfix || pl == 0 || pl == c.nz - 1;
+    const cplx v = (bnd ? c.sdb : c.sdi) * cc + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
+    return in ? v : cplx{0.0, 0.0};
+  } else {
+    return (e.bfix ? c.sdb : c.sdi) * cc + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
+  }
 }
 template <int D>
 __device__ __forceinline__ void p4r_push(cplx (&q)[D], cplx v) {
@@ -393,6 +401,117 @@ __device__ __forceinline__ void p4r_push(cplx (&q)[D], cplx v) {
   for (int d = D - 1; d > 0; --d) q[d] = q[d - 1];
   q[0] = v;
 }
+
+#ifndef NLS_P4R_FAST
+#define NLS_P4R_FAST 1  // 0: every step takes the checked stencil (A/B only)
+#endif
+// one march step; FM / FH: p4r_lap's MODE for the owned rows / the x-halo cells
+#define P4R_BODY(FM, FH)                                                                                  \
+  do {                                                                                                    \
+    const int par = (p - k0) & 1;                                                                         \
+    cplx *const cur = lds + par * 4 * LV;                                                                 \
+    const cplx *const prv = lds + (par ^ 1) * 4 * LV;                                                     \
+    const cplx sO = laO, sN = laN, sH = laH;                                                              \
+    if (p + 1 < k1 + R) {  /* uniform */                                                                  \
+      laO = p4r_load(cx, S0, P, eO, p + 1);                                                               \
+      laN = p4r_load(cx, S0, P, eN, p + 1);                                                               \
+      if (hon) laH = p4r_load(cx, S0, P, eH, p + 1);                                                      \
+    }                                                                                                     \
+    /* level 0: S_0 at plane p */                                                                         \
+    p4r_push(o0, sO);                                                                                     \
+    cur[eO.i] = sO;                                                                                       \
+    p4r_push(n0, sN);                                                                                     \
+    cur[eN.i] = sN;                                                                                       \
+    if (hon) {                                                                                            \
+      p4r_push(h0, sH);                                                                                   \
+      cur[eH.i] = sH;                                                                                     \
+    }                                                                                                     \
+    /* level 1 at plane p - 1 */                                                                          \
+    {                                                                                                     \
+      const int q = p - 1;                                                                                \
+      const cplx *pv = prv;                                                                               \
+      cplx *cv = cur + LV;                                                                                \
+      const cplx v = p4r_lap<FM>(cx, pv, eO, o0[0], o0[1], o0[2], q);                                     \
+      p4r_push(o1, v);                                                                                    \
+      cv[eO.i] = v;                                                                                       \
+      cplx vn = z;                                                                                        \
+      if (mem(1, rN)) {                                                                                   \
+        vn = p4r_lap<FM>(cx, pv, eN, n0[0], n0[1], n0[2], q);                                             \
+        cv[eN.i] = vn;                                                                                    \
+      }                                                                                                   \
+      p4r_push(n1, vn);                                                                                   \
+      if (hon) {                                                                                          \
+        cplx vh = z;                                                                                      \
+        if (hm[1]) {                                                                                      \
+          vh = p4r_lap<FH>(cx, pv, eH, h0[0], h0[1], h0[2], q);                                           \
+          cv[eH.i] = vh;                                                                                  \
+        }                                                                                                 \
+        p4r_push(h1, vh);                                                                                 \
+      }                                                                                                   \
+    }                                                                                                     \
+    /* level 2 at plane p - 2 */                                                                          \
+    {                                                                                                     \
+      const int q = p - 2;                                                                                \
+      const cplx *pv = prv + LV;                                                                          \
+      cplx *cv = cur + 2 * LV;                                                                            \
+      const cplx v = p4r_lap<FM>(cx, pv, eO, o1[0], o1[1], o1[2], q);                                     \
+      p4r_push(o2, v);                                                                                    \
+      cv[eO.i] = v;                                                                                       \
+      cplx vn = z;                                                                                        \
+      if (mem(2, rN)) {                                                                                   \
+        vn = p4r_lap<FM>(cx, pv, eN, n1[0], n1[1], n1[2], q);                                             \
+        cv[eN.i] = vn;                                                                                    \
+      }                                                                                                   \
+      p4r_push(n2, vn);                                                                                   \
+      if (hon) {                                                                                          \
+        cplx vh = z;                                                                                      \
+        if (hm[2]) {                                                                                      \
+          vh = p4r_lap<FH>(cx, pv, eH, h1[0], h1[1], h1[2], q);                                           \
+          cv[eH.i] = vh;                                                                                  \
+        }                                                                                                 \
+        p4r_push(h2, vh);                                                                                 \
+      }                                                                                                   \
+    }                                                                                                     \
+    /* level 3 at plane p - 3 (only the output row keeps it: its level 4 needs the z pair) */             \
+    {                                                                                                     \
+      const int q = p - 3;                                                                                \
+      const cplx *pv = prv + 2 * LV;                                                                      \
+      cplx *cv = cur + 3 * LV;                                                                            \
+      const cplx v = p4r_lap<FM>(cx, pv, eO, o2[0], o2[1], o2[2], q);                                     \
+      p4r_push(o3, v);                                                                                    \
+      cv[eO.i] = v;                                                                                       \
+      if (mem(3, rN)) cv[eN.i] = p4r_lap<FM>(cx, pv, eN, n2[0], n2[1], n2[2], q);                         \
+      if (hm[3]) cv[eH.i] = p4r_lap<FH>(cx, pv, eH, h2[0], h2[1], h2[2], q);                              \
+    }                                                                                                     \
+    /* level 4 and the outputs at plane k = p - 4 */                                                      \
+    const int k = p - R;                                                                                  \
+    if (k >= k0) {  /* uniform */                                                                         \
+      const cplx L4 = p4r_lap<FM>(cx, prv + 3 * LV, eO, o3[0], o3[1], o3[2], k);                          \
+      const cplx S = o0[4], L1 = o1[3], L2 = o2[2], L3 = o3[1];                                           \
+      const cplx V1 = cmul(a1, S) + cmul(b11, L1);                                                        \
+      const cplx V2 = (cmul(a2, S) + cmul(b21, L1)) + cmul(b22, L2);                                      \
+      const cplx V3 = (cmul(a3, S) + cmul(b31, L1)) + (cmul(b32, L2) + cmul(b33, L3));                    \
+      const cplx V4 = ((cmul(a4, S) + cmul(b41, L1)) + (cmul(b42, L2) + cmul(b43, L3))) + cmul(b44, L4);  \
+      const int64_t o = (int64_t)k * P + eO.off;                                                          \
+      st_nt(W + vs + o, V1);                                                                              \
+      st_nt(W + 2 * vs + o, V2);                                                                          \
+      st_nt(W + 3 * vs + o, V3);                                                                          \
+      st_nt(W + 4 * vs + o, V4);                                                                          \
+      const cplx V[4] = {V1, V2, V3, V4};                                                                 \
+_Pragma("unroll")                                                                                         \
+      for (int i = 0; i < 4; ++i) acc[i] += cj_mul(S, V[i]);                                              \
+      int c = 4;                                                                                          \
+_Pragma("unroll")                                                                                         \
+      for (int a = 0; a < 4; ++a) {                                                                       \
+        acc[c].re += abs2(V[a]);                                                                          \
+        ++c;                                                                                              \
+_Pragma("unroll")                                                                                         \
+        for (int bb = a + 1; bb < 4; ++bb) acc[c++] += cj_mul(V[a], V[bb]);                               \
+      }                                                                                                   \
+      acc[NC - 1].re += abs2(S);                                                                          \
+    }                                                                                                     \
+    __syncthreads();                                                                                      \
+  } while (0)
 
 // OUTB: the wave's output row is its second row (waves 0..3) or its first (4..7)
 template <bool OUTB>
@@ -425,112 +544,15 @@ __device__ __forceinline__ void p4r_march(cplx *lds, cplx *__restrict__ W, int64
   for (int d = 0; d < 3; ++d) o2[d] = o3[d] = n0[d] = n1[d] = n2[d] = h0[d] = h1[d] = h2[d] = z;
   cplx laO = p4r_load(cx, S0, P, eO, k0 - R), laN = p4r_load(cx, S0, P, eN, k0 - R);
   cplx laH = hon ? p4r_load(cx, S0, P, eH, k0 - R) : z;
-  for (int p = k0 - R; p < k1 + R; ++p) {
-    const int par = (p - k0) & 1;
-    cplx *const cur = lds + par * 4 * LV;
-    const cplx *const prv = lds + (par ^ 1) * 4 * LV;
-    const cplx sO = laO, sN = laN, sH = laH;
-    if (p + 1 < k1 + R) {  // uniform
-      laO = p4r_load(cx, S0, P, eO, p + 1);
-      laN = p4r_load(cx, S0, P, eN, p + 1);
-      if (hon) laH = p4r_load(cx, S0, P, eH, p + 1);
-    }
-    // level 0: S_0 at plane p
-    p4r_push(o0, sO);
-    cur[eO.i] = sO;
-    p4r_push(n0, sN);
-    cur[eN.i] = sN;
-    if (hon) {
-      p4r_push(h0, sH);
-      cur[eH.i] = sH;
-    }
-    // level 1 at plane p - 1
-    {
-      const int q = p - 1;
-      const cplx *pv = prv;
-      cplx *cv = cur + LV;
-      const cplx v = p4r_lap(cx, pv, eO, o0[0], o0[1], o0[2], q);
-      p4r_push(o1, v);
-      cv[eO.i] = v;
-      cplx vn = z;
-      if (mem(1, rN)) {
-        vn = p4r_lap(cx, pv, eN, n0[0], n0[1], n0[2], q);
-        cv[eN.i] = vn;
-      }
-      p4r_push(n1, vn);
-      if (hon) {
-        cplx vh = z;
-        if (hm[1]) {
-          vh = p4r_lap(cx, pv, eH, h0[0], h0[1], h0[2], q);
-          cv[eH.i] = vh;
-        }
-        p4r_push(h1, vh);
-      }
-    }
-    // level 2 at plane p - 2
-    {
-      const int q = p - 2;
-      const cplx *pv = prv + LV;
-      cplx *cv = cur + 2 * LV;
-      const cplx v = p4r_lap(cx, pv, eO, o1[0], o1[1], o1[2], q);
-      p4r_push(o2, v);
-      cv[eO.i] = v;
-      cplx vn = z;
-      if (mem(2, rN)) {
-        vn = p4r_lap(cx, pv, eN, n1[0], n1[1], n1[2], q);
-        cv[eN.i] = vn;
-      }
-      p4r_push(n2, vn);
-      if (hon) {
-        cplx vh = z;
-        if (hm[2]) {
-          vh = p4r_lap(cx, pv, eH, h1[0], h1[1], h1[2], q);
-          cv[eH.i] = vh;
-        }
-        p4r_push(h2, vh);
-      }
-    }
-    // level 3 at plane p - 3 (only the output row keeps it: its level 4 needs the z pair)
-    {
-      const int q = p - 3;
-      const cplx *pv = prv + 2 * LV;
-      cplx *cv = cur + 3 * LV;
-      const cplx v = p4r_lap(cx, pv, eO, o2[0], o2[1], o2[2], q);
-      p4r_push(o3, v);
-      cv[eO.i] = v;
-      if (mem(3, rN)) cv[eN.i] = p4r_lap(cx, pv, eN, n2[0], n2[1], n2[2], q);
-      if (hm[3]) cv[eH.i] = p4r_lap(cx, pv, eH, h2[0], h2[1], h2[2], q);
-    }
-    // level 4 and the outputs at plane k = p - 4
-    const int k = p - R;
-    if (k >= k0) {  // uniform
-      const cplx L4 = p4r_lap(cx, prv + 3 * LV, eO, o3[0], o3[1], o3[2], k);
-      const cplx S = o0[4], L1 = o1[3], L2 = o2[2], L3 = o3[1];
-      const cplx V1 = cmul(a1, S) + cmul(b11, L1);
-      const cplx V2 = (cmul(a2, S) + cmul(b21, L1)) + cmul(b22, L2);
-      const cplx V3 = (cmul(a3, S) + cmul(b31, L1)) + (cmul(b32, L2) + cmul(b33, L3));
-      const cplx V4 = ((cmul(a4, S) + cmul(b41, L1)) + (cmul(b42, L2) + cmul(b43, L3))) + cmul(b44, L4);
-      const int64_t o = (int64_t)k * P + eO.off;
-      st_nt(W + vs + o, V1);
-      st_nt(W + 2 * vs + o, V2);
-      st_nt(W + 3 * vs + o, V3);
-      st_nt(W + 4 * vs + o, V4);
-      const cplx V[4] = {V1, V2, V3, V4};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] += cj_mul(S, V[i]);
-      int c = 4;
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        acc[c].re += abs2(V[a]);
-        ++c;
-#pragma unroll
-        for (int bb = a + 1; bb < 4; ++bb) acc[c++] += cj_mul(V[a], V[bb]);
-      }
-      acc[NC - 1].re += abs2(S);
-    }
-    __syncthreads();
-  }
+  // the steps whose planes (p - 5 .. p) all lie inside the grid and off its z boundary form
+  // one contiguous range [pf0, pf1): their own loop takes the check-free stencil
+  const int pe = k1 + R, pf0 = min(max(k0 - R, 6), pe), pf1 = NLS_P4R_FAST ? max(min(pe, cx.nz - 1), pf0) : pf0;
+  int p = k0 - R;
+  for (; p < pf0; ++p) P4R_BODY(0, 0);
+  for (; p < pf1; ++p) P4R_BODY(1, 0);
+  for (; p < pe; ++p) P4R_BODY(0, 0);
 }
+#undef P4R_BODY
 
 
 __global__ __launch_bounds__(p4r::NT, 1) void k_p4r(cplx *__restrict__ W, int64_t vs, Geo g,

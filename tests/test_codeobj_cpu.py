@@ -81,10 +81,10 @@ def test_register_row_kinds():
 
 def test_new_round6_kernels_have_no_scratch(tmp_path):
     """The round-6 kernels (the fused column-sum + coefficient launch, the fused basis end,
-    the four-vector first pass) keep everything in registers and LDS: no VGPR spill, no
+    the four-vector first passes k_p4d0 and k_p4r) keep everything in registers and LDS: no VGPR spill, no
     scratch instruction, and no private segment beyond the call frame of the eigensolve
     (k_tail_chain calls eigen_phase_jacobi, __noinline__, exactly as k_reduce_final does)."""
-    want = ("k_colsum_p2coef", "k_tail_chain", "k_p4d0")
+    want = ("k_colsum_p2coef", "k_tail_chain", "k_p4d0", "k_p4r")
     seen = set()
     for co in C.gfx950_objects(LIB, str(tmp_path)):
         md = C.metadata(co)
