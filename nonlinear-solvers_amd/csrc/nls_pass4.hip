@@ -379,7 +379,7 @@ __device__ __forceinline__ cplx p4r_load(const P4C c, const cplx *__restrict__ S
 // from the owner's queue, x / y neighbours from level l-1's LDS plane q; zero outside the grid.
 // MODE 0: any plane; 1: a plane neither outside the grid nor on its z boundary and a cell
 // inside the grid in x (the owned rows' cells: x0..x0+63) -- the same value without the
-// checks
+// checks; 2: such a plane with the x check (the x-halo cells)
 template <int MODE>
 __device__ __forceinline__ cplx p4r_lap(const P4C c, const cplx *prv, const P4RPos e, cplx zp, cplx cc, cplx zm,
                                         int q) {
@@ -392,7 +392,9 @@ __device__ __forceinline__ cplx p4r_lap(const P4C c, const cplx *prv, const P4RP
     const cplx v = (bnd ? c.sdb : c.sdi) * cc + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
     return in ? v : cplx{0.0, 0.0};
   } else {
-    return (e.bfix ? c.sdb : c.sdi) * cc + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
+    const cplx v = (e.bfix ? c.sdb : c.sdi) * cc + c.s * (((zm + zp) + (xm + xp)) + (ym + yp));
+    if constexpr (MODE == 2) return e.xin ? v : cplx{0.0, 0.0};
+    return v;
   }
 }
 template <int D>
@@ -402,6 +404,9 @@ __device__ __forceinline__ void p4r_push(cplx (&q)[D], cplx v) {
   q[0] = v;
 }
 
+#ifndef NLS_P4R_HFAST
+#define NLS_P4R_HFAST 1  // 0: the x-halo cells take the checked stencil on every step (A/B only)
+#endif
 #ifndef NLS_P4R_FAST
 #define NLS_P4R_FAST 1  // 0: every step takes the checked stencil (A/B only)
 #endif
@@ -549,7 +554,7 @@ __device__ __forceinline__ void p4r_march(cplx *lds, cplx *__restrict__ W, int64
   const int pe = k1 + R, pf0 = min(max(k0 - R, 6), pe), pf1 = NLS_P4R_FAST ? max(min(pe, cx.nz - 1), pf0) : pf0;
   int p = k0 - R;
   for (; p < pf0; ++p) P4R_BODY(0, 0);
-  for (; p < pf1; ++p) P4R_BODY(1, 0);
+  for (; p < pf1; ++p) P4R_BODY(1, NLS_P4R_HFAST ? 2 : 0);
   for (; p < pe; ++p) P4R_BODY(0, 0);
 }
 #undef P4R_BODY
